@@ -1,0 +1,86 @@
+/*
+ * svscope.h — C ABI of libsvscope_hip.so, the MI355X (gfx950) engine behind the
+ * SVScope localGraph hot path.  Plain pointers and sizes only; every entry
+ * point returns 0 on success or a negative SVS_E* code, with a message from
+ * svs_last_error() (thread-local).
+ *
+ * Seams replaced (reference = /root/reference/src):
+ *   POA seam   spoa.poa(list_of_str, 1) -> (consensus, msa)   [pyspoa 0.2.1]
+ *              call sites DataScanner.py:206,213 (window MSA) and
+ *              DecisionMaker.py:160,171 (per-cluster consensus)
+ *              -> svs_poa_batch + svs_poa_result_*
+ *   EM seam    ReadsCluster.EMCluster(seqdatamx, initselection=1, max_C=9)
+ *              ReadsCluster.py:221-277 (EM 190-209, E-step 132-155,
+ *              M-step 162-188, loglik 104-122, BIC 211-219)
+ *              -> svs_similarity_batch (pariwiseDistance, :52-59) and
+ *                 svs_em_batch (everything after scipy's ward/fcluster init)
+ */
+#ifndef SVSCOPE_H
+#define SVSCOPE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVS_OK 0
+#define SVS_E_INVALID (-1)     /* bad argument */
+#define SVS_E_NOMEM (-2)       /* host or device allocation failed */
+#define SVS_E_HIP (-3)         /* HIP runtime error (no device, launch failure) */
+#define SVS_E_UNSUPPORTED (-4) /* parameters outside what the kernels implement */
+#define SVS_E_INTERNAL (-5)    /* kernel reported an inconsistent traceback */
+
+typedef struct svs_context svs_context;
+typedef struct svs_poa_result svs_poa_result;
+
+/* Scoring of pyspoa's poa(): defaults m=5 n=-4 g=-8 e=-6 q=-10 c=-4, alignment
+ * type 1 (global NW), min_coverage=-1. Only type 1 with spoa's convex gap
+ * subtype (g<e, g>q, e<c) is implemented on the GPU. */
+typedef struct svs_poa_config {
+  int32_t algorithm;
+  int32_t m, n, g, e, q, c;
+  int32_t min_coverage;
+  int32_t genmsa;
+} svs_poa_config;
+
+typedef struct svs_poa_stats {
+  uint64_t dp_cells;        /* sum over alignments of (|V|+1)*(L+1) */
+  uint64_t alignments;      /* read-vs-graph DP jobs executed on the GPU */
+  uint64_t launches;        /* kernel launches */
+  uint64_t tb_bytes;        /* traceback-code bytes written (HBM) */
+  uint64_t pool_bytes;      /* row-pool bytes written (H,F,O planes) */
+  uint64_t h2d_bytes, d2h_bytes;
+  double kernel_ms;         /* sum of per-launch durations (HIP events) */
+  double host_graph_ms;     /* host graph update / export time */
+  double wall_ms;
+} svs_poa_stats;
+
+/* One context per host thread; owns a HIP stream and device arenas. */
+int svs_init(int device_ordinal, svs_context** out);
+void svs_release(svs_context* ctx);
+const char* svs_last_error(void);
+int svs_device_count(int* out);
+
+/* Batched POA: job j aligns sequences [job_seq_start[j], job_seq_start[j+1])
+ * in order (pyspoa semantics: empty sequences are skipped and produce no MSA
+ * row).  Sequence s occupies seq_bytes[seq_byte_start[s] .. seq_byte_start[s+1]).
+ * *out is library-allocated; free with svs_poa_result_free. */
+int svs_poa_batch(svs_context* ctx, int32_t n_jobs, const int64_t* job_seq_start,
+                  const int64_t* seq_byte_start, const char* seq_bytes,
+                  const svs_poa_config* cfg, svs_poa_result** out);
+int svs_poa_result_consensus(const svs_poa_result* r, int32_t job, const char** data, int64_t* len);
+/* MSA rows are returned as one rows*cols char block (row-major). */
+int svs_poa_result_msa(const svs_poa_result* r, int32_t job, int32_t* rows, int32_t* cols,
+                       const char** data);
+int svs_poa_result_stats(const svs_poa_result* r, svs_poa_stats* out);
+void svs_poa_result_free(svs_poa_result* r);
+
+/* Wave-primitive self test (GPU tests): per 64-lane wave, inclusive prefix max
+ * and shift-right-by-one (lane 0 <- -7). */
+int svs_wave_selftest(svs_context* ctx, const int32_t* in, int32_t* scan, int32_t* shift,
+                      int32_t n_waves);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVSCOPE_H */

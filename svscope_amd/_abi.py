@@ -1,0 +1,135 @@
+"""ctypes binding of libsvscope_hip.so (C ABI declared in include/svscope.h).
+
+The library is built in-tree by svscope_amd.build.  There is no CPU fallback:
+if the library or a HIP device is missing, every entry point raises.
+"""
+import ctypes
+import os
+import threading
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libsvscope_hip.so")
+
+SVS_OK = 0
+_ERRNAMES = {-1: "SVS_E_INVALID", -2: "SVS_E_NOMEM", -3: "SVS_E_HIP", -4: "SVS_E_UNSUPPORTED",
+             -5: "SVS_E_INTERNAL"}
+
+
+
+class SvsError(RuntimeError):
+    pass
+
+
+class PoaConfig(ctypes.Structure):
+    _fields_ = [("algorithm", ctypes.c_int32), ("m", ctypes.c_int32), ("n", ctypes.c_int32),
+                ("g", ctypes.c_int32), ("e", ctypes.c_int32), ("q", ctypes.c_int32), ("c", ctypes.c_int32),
+                ("min_coverage", ctypes.c_int32), ("genmsa", ctypes.c_int32)]
+
+
+class PoaStats(ctypes.Structure):
+    _fields_ = [("dp_cells", ctypes.c_uint64), ("alignments", ctypes.c_uint64), ("launches", ctypes.c_uint64),
+                ("tb_bytes", ctypes.c_uint64), ("pool_bytes", ctypes.c_uint64), ("h2d_bytes", ctypes.c_uint64),
+                ("d2h_bytes", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("host_graph_ms", ctypes.c_double),
+                ("wall_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library():
+    """Loads libsvscope_hip.so and declares its prototypes (no device needed)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise SvsError(f"{LIB_PATH} is missing: build it with `python -m svscope_amd.build` "
+                           "(the MI355X engine has no CPU fallback)")
+        lib = ctypes.CDLL(LIB_PATH)
+        P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        lib.svs_init.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
+        lib.svs_init.restype = ctypes.c_int
+        lib.svs_release.argtypes = [P]
+        lib.svs_release.restype = None
+        lib.svs_last_error.argtypes = []
+        lib.svs_last_error.restype = ctypes.c_char_p
+        lib.svs_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        lib.svs_device_count.restype = ctypes.c_int
+        lib.svs_poa_batch.argtypes = [P, I32, ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.c_char_p,
+                                      ctypes.POINTER(PoaConfig), ctypes.POINTER(P)]
+        lib.svs_poa_batch.restype = ctypes.c_int
+        lib.svs_poa_result_consensus.argtypes = [P, I32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(I64)]
+        lib.svs_poa_result_consensus.restype = ctypes.c_int
+        lib.svs_poa_result_msa.argtypes = [P, I32, ctypes.POINTER(I32), ctypes.POINTER(I32),
+                                           ctypes.POINTER(ctypes.c_void_p)]
+        lib.svs_poa_result_msa.restype = ctypes.c_int
+        lib.svs_poa_result_stats.argtypes = [P, ctypes.POINTER(PoaStats)]
+        lib.svs_poa_result_stats.restype = ctypes.c_int
+        lib.svs_poa_result_free.argtypes = [P]
+        lib.svs_poa_result_free.restype = None
+        lib.svs_wave_selftest.argtypes = [P, P, P, P, I32]
+        lib.svs_wave_selftest.restype = ctypes.c_int
+        _declare_em(lib)
+        _lib = lib
+        return lib
+
+
+def _declare_em(lib):
+    if not hasattr(lib, "svs_em_batch"):
+        return
+    P, I32 = ctypes.c_void_p, ctypes.c_int32
+    lib.svs_similarity_batch.argtypes = [P, I32, P, P, P, P]
+    lib.svs_similarity_batch.restype = ctypes.c_int
+    lib.svs_em_batch.argtypes = [P, I32, P, P, P, P, P, ctypes.POINTER(ctypes.c_void_p)]
+    lib.svs_em_batch.restype = ctypes.c_int
+    lib.svs_em_result_get.argtypes = [P, I32, I32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64)]
+    lib.svs_em_result_get.restype = ctypes.c_int
+    lib.svs_em_result_free.argtypes = [P]
+    lib.svs_em_result_free.restype = None
+
+
+def check(rc, what="svscope call"):
+    if rc != SVS_OK:
+        msg = load_library().svs_last_error()
+        raise SvsError(f"{what} failed ({_ERRNAMES.get(rc, rc)}): {msg.decode() if msg else ''}")
+
+
+class Context:
+    """One HIP stream + device arenas (C++ svs_context)."""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        check(self.lib.svs_init(int(device), ctypes.byref(h)), "svs_init")
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.svs_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_contexts = {}
+_ctx_lock = threading.Lock()
+
+
+def default_context(device=None):
+    """Process-wide context per device (ctypes calls are serialised by the caller)."""
+    if device is None:
+        device = int(os.environ.get("SVS_DEVICE", "0"))
+    with _ctx_lock:
+        ctx = _contexts.get(device)
+        if ctx is None:
+            ctx = Context(device)
+            _contexts[device] = ctx
+        return ctx

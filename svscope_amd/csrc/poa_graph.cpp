@@ -1,0 +1,286 @@
+// Flat-array POA graph: host half of the batched MI355X POA engine.
+// See poa_graph.hpp for the semantic contract (spoa 4.x Graph behaviour).
+#include "poa_graph.hpp"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace svs {
+
+static constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+uint32_t PoaGraph::new_node(char b) {
+  const uint32_t id = static_cast<uint32_t>(base_.size());
+  base_.push_back(b);
+  in_.emplace_back();
+  out_.emplace_back();
+  aligned_.emplace_back();
+  cov_.push_back(0);
+  cov_last_.push_back(0);
+  return id;
+}
+
+void PoaGraph::link(uint32_t tail, uint32_t head, int64_t w, uint32_t seq_id) {
+  const uint32_t tag = seq_id + 1;
+  for (uint32_t x : {tail, head}) {
+    if (cov_last_[x] != tag) { cov_last_[x] = tag; ++cov_[x]; }
+  }
+  for (uint32_t e : out_[tail]) {
+    if (e_head_[e] == head) { e_w_[e] += w; return; }
+  }
+  const uint32_t e = static_cast<uint32_t>(e_tail_.size());
+  e_tail_.push_back(tail);
+  e_head_.push_back(head);
+  e_w_.push_back(w);
+  out_[tail].push_back(e);
+  in_[head].push_back(e);
+}
+
+uint32_t PoaGraph::chain(const std::string& s, uint32_t b, uint32_t e, std::vector<uint32_t>* path) {
+  if (b == e) return kNone;
+  const uint32_t sid = static_cast<uint32_t>(paths_.size());
+  uint32_t prev = new_node(s[b]);
+  path->push_back(prev);
+  for (uint32_t i = b + 1; i < e; ++i) {
+    const uint32_t cur = new_node(s[i]);
+    link(prev, cur, 2, sid);
+    path->push_back(cur);
+    prev = cur;
+  }
+  return (*path)[0];
+}
+
+void PoaGraph::add_alignment_ranks(const std::vector<int32_t>& rank_pairs, const std::string& seq) {
+  std::vector<std::pair<int32_t, int32_t>> np;
+  np.reserve(rank_pairs.size() / 2);
+  for (size_t k = 0; k + 1 < rank_pairs.size(); k += 2) {
+    const int32_t r = rank_pairs[k];
+    np.emplace_back(r < 0 ? -1 : static_cast<int32_t>(rank_to_node_.at(static_cast<size_t>(r))),
+                    rank_pairs[k + 1]);
+  }
+  add_alignment_nodes(np, seq);
+}
+
+void PoaGraph::add_alignment_nodes(const std::vector<std::pair<int32_t, int32_t>>& aln,
+                                   const std::string& seq) {
+  if (seq.empty()) return;
+  const uint32_t sid = static_cast<uint32_t>(paths_.size());
+  std::vector<uint32_t> path;
+  path.reserve(seq.size());
+  if (aln.empty()) {
+    chain(seq, 0, static_cast<uint32_t>(seq.size()), &path);
+    paths_.push_back(std::move(path));
+    sort_ranks();
+    return;
+  }
+  int32_t first = -1, last = -1;
+  for (const auto& p : aln) {
+    if (p.second == -1) continue;
+    if (p.second < 0 || p.second >= static_cast<int32_t>(seq.size()))
+      throw std::runtime_error("alignment position out of range");
+    if (first == -1) first = p.second;
+    last = p.second;
+  }
+  if (first == -1) throw std::runtime_error("alignment consumes no sequence");
+  // spoa creates the prefix chain, then the suffix chain, then the middle.
+  chain(seq, 0, static_cast<uint32_t>(first), &path);
+  uint32_t prev = path.empty() ? kNone : path.back();
+  std::vector<uint32_t> suffix;
+  const uint32_t suffix_head =
+      chain(seq, static_cast<uint32_t>(last) + 1, static_cast<uint32_t>(seq.size()), &suffix);
+  for (const auto& p : aln) {
+    if (p.second == -1) continue;
+    const char letter = seq[static_cast<size_t>(p.second)];
+    uint32_t cur = kNone;
+    if (p.first == -1) {
+      cur = new_node(letter);
+    } else {
+      const uint32_t n = static_cast<uint32_t>(p.first);
+      if (base_[n] == letter) {
+        cur = n;
+      } else {
+        for (uint32_t a : aligned_[n])
+          if (base_[a] == letter) { cur = a; break; }
+        if (cur == kNone) {
+          cur = new_node(letter);
+          for (uint32_t a : aligned_[n]) {
+            aligned_[a].push_back(cur);
+            aligned_[cur].push_back(a);
+          }
+          aligned_[n].push_back(cur);
+          aligned_[cur].push_back(n);
+        }
+      }
+    }
+    if (prev != kNone) link(prev, cur, 2, sid);
+    path.push_back(cur);
+    prev = cur;
+  }
+  if (suffix_head != kNone) {
+    link(prev, suffix_head, 2, sid);
+    path.insert(path.end(), suffix.begin(), suffix.end());
+  }
+  paths_.push_back(std::move(path));
+  sort_ranks();
+}
+
+void PoaGraph::sort_ranks() {
+  const uint32_t n = num_nodes();
+  rank_to_node_.clear();
+  rank_to_node_.reserve(n);
+  std::vector<uint8_t> mark(n, 0), ignored(n, 0);
+  std::vector<uint32_t> stack;
+  for (uint32_t root = 0; root < n; ++root) {
+    if (mark[root] != 0) continue;
+    stack.push_back(root);
+    while (!stack.empty()) {
+      const uint32_t cur = stack.back();
+      bool ready = true;
+      if (mark[cur] != 2) {
+        for (uint32_t e : in_[cur]) {
+          const uint32_t t = e_tail_[e];
+          if (mark[t] != 2) { stack.push_back(t); ready = false; }
+        }
+        if (!ignored[cur]) {
+          for (uint32_t a : aligned_[cur]) {
+            if (mark[a] != 2) { stack.push_back(a); ignored[a] = 1; ready = false; }
+          }
+        }
+        if (ready) {
+          mark[cur] = 2;
+          if (!ignored[cur]) {
+            rank_to_node_.push_back(cur);
+            for (uint32_t a : aligned_[cur]) rank_to_node_.push_back(a);
+          }
+        } else {
+          mark[cur] = 1;
+        }
+      }
+      if (ready) stack.pop_back();
+    }
+  }
+  node_to_rank_.assign(n, 0);
+  for (uint32_t r = 0; r < rank_to_node_.size(); ++r) node_to_rank_[rank_to_node_[r]] = r;
+}
+
+void PoaGraph::export_rows(RowTables* t) const {
+  const uint32_t V = num_nodes();
+  t->info.resize(V);
+  t->slot.resize(V);
+  t->pstart.resize(V + 1);
+  t->pred_row.clear();
+  t->pred_slot.clear();
+  t->max_preds = 0;
+  std::vector<uint32_t> last_use(V);
+  uint32_t np = 0;
+  for (uint32_t r = 0; r < V; ++r) {
+    const uint32_t node = rank_to_node_[r];
+    t->info[r] = static_cast<uint8_t>(base_[node]) | (out_[node].empty() ? 0x100u : 0u);
+    t->pstart[r] = np;
+    last_use[r] = r;
+    for (uint32_t e : in_[node]) {
+      const uint32_t pr = node_to_rank_[e_tail_[e]];
+      t->pred_row.push_back(pr + 1);
+      last_use[pr] = std::max(last_use[pr], r);
+      ++np;
+    }
+    t->max_preds = std::max<uint32_t>(t->max_preds, static_cast<uint32_t>(in_[node].size()));
+  }
+  t->pstart[V] = np;
+  t->pred_slot.resize(np);
+  // Row-pool slot assignment: a row lives from its computation until its last
+  // successor has been computed; slot 0 holds the virtual row 0 for the whole job.
+  std::vector<uint32_t> free_slots;
+  uint32_t next = 1;
+  for (uint32_t r = 0; r < V; ++r) {
+    uint32_t s;
+    if (free_slots.empty()) {
+      s = next++;
+    } else {
+      s = free_slots.back();
+      free_slots.pop_back();
+    }
+    t->slot[r] = s;
+    for (uint32_t k = t->pstart[r]; k < t->pstart[r + 1]; ++k) {
+      const uint32_t pr = t->pred_row[k] - 1;
+      t->pred_slot[k] = t->slot[pr];
+    }
+    for (uint32_t k = t->pstart[r]; k < t->pstart[r + 1]; ++k) {
+      const uint32_t pr = t->pred_row[k] - 1;
+      if (last_use[pr] == r) free_slots.push_back(t->slot[pr]);
+    }
+    if (last_use[r] == r) free_slots.push_back(s);
+  }
+  t->n_slots = next;
+}
+
+std::vector<std::string> PoaGraph::msa() const {
+  std::vector<uint32_t> col(num_nodes(), 0);
+  uint32_t ncol = 0;
+  for (size_t r = 0; r < rank_to_node_.size(); ++r) {
+    const uint32_t node = rank_to_node_[r];
+    col[node] = ncol;
+    for (size_t k = 0; k < aligned_[node].size(); ++k) col[rank_to_node_[++r]] = ncol;
+    ++ncol;
+  }
+  std::vector<std::string> rows;
+  rows.reserve(paths_.size());
+  for (const auto& p : paths_) {
+    std::string row(ncol, '-');
+    for (uint32_t node : p) row[col[node]] = base_[node];
+    rows.push_back(std::move(row));
+  }
+  return rows;
+}
+
+uint32_t PoaGraph::branch_complete(uint32_t rank, std::vector<int64_t>& score, std::vector<int64_t>& pred) {
+  const uint32_t start = rank_to_node_[rank];
+  for (uint32_t e : out_[start])
+    for (uint32_t f : in_[e_head_[e]])
+      if (e_tail_[f] != start) score[e_tail_[f]] = -1;
+  int64_t best = -1;
+  for (uint32_t r = rank + 1; r < rank_to_node_.size(); ++r) {
+    const uint32_t n = rank_to_node_[r];
+    score[n] = -1;
+    pred[n] = -1;
+    for (uint32_t e : in_[n]) {
+      const uint32_t t = e_tail_[e];
+      if (score[t] == -1) continue;
+      if (score[n] < e_w_[e] || (score[n] == e_w_[e] && score[pred[n]] <= score[t])) {
+        score[n] = e_w_[e];
+        pred[n] = t;
+      }
+    }
+    if (pred[n] != -1) score[n] += score[pred[n]];
+    if (best == -1 || score[best] < score[n]) best = n;
+  }
+  return static_cast<uint32_t>(best);
+}
+
+std::string PoaGraph::consensus(int32_t min_coverage) {
+  std::string out;
+  if (rank_to_node_.empty()) return out;
+  const uint32_t n = num_nodes();
+  std::vector<int64_t> score(n, -1), pred(n, -1);
+  int64_t best = -1;
+  for (uint32_t node : rank_to_node_) {
+    for (uint32_t e : in_[node]) {
+      const uint32_t t = e_tail_[e];
+      if (score[node] < e_w_[e] || (score[node] == e_w_[e] && score[pred[node]] <= score[t])) {
+        score[node] = e_w_[e];
+        pred[node] = t;
+      }
+    }
+    if (pred[node] != -1) score[node] += score[pred[node]];
+    if (best == -1 || score[best] < score[node]) best = node;
+  }
+  while (!out_[static_cast<uint32_t>(best)].empty())
+    best = branch_complete(node_to_rank_[static_cast<uint32_t>(best)], score, pred);
+  std::vector<uint32_t> path;
+  for (int64_t x = best; x != -1; x = pred[x]) path.push_back(static_cast<uint32_t>(x));
+  for (auto it = path.rbegin(); it != path.rend(); ++it)
+    if (min_coverage <= 0 || static_cast<int32_t>(cov_[*it]) >= min_coverage) out += base_[*it];
+  return out;
+}
+
+}  // namespace svs

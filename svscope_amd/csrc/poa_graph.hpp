@@ -1,0 +1,66 @@
+// Flat-array partial-order graph used by the batched MI355X POA engine.
+//
+// Semantics follow spoa 4.x Graph (the library behind `poa(seqs, 1)` at
+// /root/reference/src/DataScanner.py:206,213 and DecisionMaker.py:160,171):
+// AddAlignment with aligned-node merging, DFS topological sort with aligned
+// groups kept contiguous, MSA columns from rank groups, heaviest-bundle
+// consensus.  The representation is built for batched device export: every
+// node/edge lives in flat vectors, each sequence keeps its node path (used for
+// the MSA instead of edge-label walks) and export_rows() writes the
+// rank-ordered row tables the HIP DP kernel consumes.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace svs {
+
+// One DP row table for a single read-vs-graph alignment job (host side).
+struct RowTables {
+  std::vector<uint32_t> info;    // per rank row: bits 0-7 base, bit 8 sink
+  std::vector<uint32_t> slot;    // per rank row: pool slot (>=1; slot 0 = virtual row 0)
+  std::vector<uint32_t> pstart;  // n_rows + 1 CSR offsets into pred_row/pred_slot
+  std::vector<uint32_t> pred_row;   // 1-based DP row of each in-edge tail (insertion order)
+  std::vector<uint32_t> pred_slot;  // pool slot of that row
+  uint32_t n_slots = 1;
+  uint32_t max_preds = 0;
+};
+
+class PoaGraph {
+ public:
+  uint32_t num_nodes() const { return static_cast<uint32_t>(base_.size()); }
+  uint32_t num_sequences() const { return static_cast<uint32_t>(paths_.size()); }
+  bool empty() const { return base_.empty(); }
+
+  // pairs are (rank-row index 0-based or -1, sequence position or -1), in
+  // forward order.  Node identity is resolved through the CURRENT rank order.
+  void add_alignment_ranks(const std::vector<int32_t>& rank_pairs, const std::string& seq);
+  // pairs are (node id or -1, position or -1); empty => fresh chain.
+  void add_alignment_nodes(const std::vector<std::pair<int32_t, int32_t>>& node_pairs,
+                           const std::string& seq);
+
+  void export_rows(RowTables* t) const;
+  std::vector<std::string> msa() const;
+  std::string consensus(int32_t min_coverage);
+
+  const std::vector<uint32_t>& rank_to_node() const { return rank_to_node_; }
+
+ private:
+  uint32_t new_node(char b);
+  void link(uint32_t tail, uint32_t head, int64_t w, uint32_t seq_id);
+  uint32_t chain(const std::string& s, uint32_t b, uint32_t e, std::vector<uint32_t>* path);
+  void sort_ranks();
+  uint32_t branch_complete(uint32_t rank, std::vector<int64_t>& score, std::vector<int64_t>& pred);
+
+  std::vector<char> base_;
+  std::vector<std::vector<uint32_t>> in_;    // edge ids into node, insertion order
+  std::vector<std::vector<uint32_t>> out_;   // edge ids out of node
+  std::vector<std::vector<uint32_t>> aligned_;
+  std::vector<uint32_t> cov_, cov_last_;     // distinct sequences touching a node's edges
+  std::vector<uint32_t> e_tail_, e_head_;
+  std::vector<int64_t> e_w_;
+  std::vector<std::vector<uint32_t>> paths_;
+  std::vector<uint32_t> rank_to_node_, node_to_rank_;
+};
+
+}  // namespace svs

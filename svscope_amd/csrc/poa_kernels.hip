@@ -1,0 +1,339 @@
+// MI355X (gfx950) POA alignment kernel: Needleman-Wunsch of one read against a
+// partial-order graph with spoa's convex gap model, plus traceback, for a
+// batch of independent (window, read) jobs.
+//
+// Replaces the DP + backtrack of spoa's SisdAlignmentEngine (kNW, convex),
+// reached by the reference through `poa(seqs, 1)` at
+// /root/reference/src/DataScanner.py:206,213 and DecisionMaker.py:160,171.
+//
+// Mapping (CDNA4-first, not a translation of spoa's SIMD engine):
+//  * one 64-lane wave per job; four independent jobs per 256-thread block;
+//  * graph rows in topological rank order; each row is swept in strips of 64
+//    columns, lane l owning column 64*s + l, so every pool/traceback access is
+//    a coalesced 256-B (int32) / 128-B (uint16) wave access;
+//  * the sequential horizontal recurrences E (g,e) and Q (q,c) are rewritten
+//    as two wave-wide prefix-max scans (DPP row_shr + row_bcast), exact for
+//    parameters satisfying g<=e, q<=c, g<=c, e<=c, g+q<=2c (checked on host):
+//        Q[j] = j*c + max_{k<=j} (Hpre[k-1] + q - k*c)
+//        E[j] = j*e + max_{k<=j} (max(Hpre,Q)[k-1] + g - k*e)
+//    where Hpre = max(diagonal, F, O) over all in-edges;
+//  * H/F/O rows live in a small per-job row pool (slots recycled by the host
+//    planner once a row's last successor is done) instead of full matrices;
+//  * per cell only a 16-bit traceback code is written to HBM: it records the
+//    outcome of every comparison spoa's backtrack makes at that cell, so the
+//    backtrack replays spoa's exact tie-break order without the score planes.
+//
+// Traceback code layout (uint16):
+//   bits 0-1  main move: 0 diagonal, 1 up, 2 left, 3 none
+//   bit  2    extend flag of the main move (extend_up / extend_left)
+//   bits 3-7  in-edge index of the main move (diag/up)
+//   bit  8    left-gap run opened here:  H[j-1]+g==E[j] || H[j-1]+q==Q[j]
+//   bit  9    up-gap run stop flag
+//   bits 10-14 in-edge index continuing an up-gap run (31 = none)
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "svs_device.hpp"
+
+namespace svs {
+
+#define SVS_NEG_INF (INT32_MIN + 1024)
+#define SVS_VNEG (INT32_MIN / 2)
+
+__device__ __forceinline__ int32_t imax(int32_t a, int32_t b) { return a > b ? a : b; }
+
+// Inclusive prefix max over the 64 lanes of a wave (DPP: row_shr 1/2/4/8,
+// then row_bcast15 / row_bcast31).  Lanes with no source keep the identity.
+__device__ __forceinline__ int32_t wave_prefix_max(int32_t x) {
+  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x111, 0xF, 0xF, false));
+  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x112, 0xF, 0xF, false));
+  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x114, 0xF, 0xF, false));
+  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x118, 0xF, 0xF, false));
+  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x142, 0xA, 0xF, false));
+  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x143, 0xC, 0xF, false));
+  return x;
+}
+
+// lane l <- x[l-1]; lane 0 <- fill (wave-uniform)
+__device__ __forceinline__ int32_t wave_shr1(int32_t x, int32_t fill, int lane) {
+  const int32_t y = __shfl_up(x, 1, 64);
+  return lane == 0 ? fill : y;
+}
+
+__device__ __forceinline__ int32_t readlane63(int32_t x) {
+  return __builtin_amdgcn_readlane(x, 63);
+}
+
+// Row-0 (virtual source row) values, spoa Initialize for kNW convex.
+__device__ __forceinline__ int32_t row0_e(const PoaScore& P, int32_t j) { return j == 0 ? 0 : P.g + (j - 1) * P.e; }
+__device__ __forceinline__ int32_t row0_q(const PoaScore& P, int32_t j) { return j == 0 ? 0 : P.q + (j - 1) * P.c; }
+__device__ __forceinline__ int32_t row0_h(const PoaScore& P, int32_t j) {
+  return j == 0 ? 0 : imax(row0_q(P, j), row0_e(P, j));
+}
+
+__global__ __launch_bounds__(256) void poa_nw_convex_kernel(
+    const PoaJob* __restrict__ jobs, int n_jobs, PoaScore P,
+    const uint32_t* __restrict__ row_info, const uint32_t* __restrict__ row_slot,
+    const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
+    const uint32_t* __restrict__ pred_slot, const uint8_t* __restrict__ seqs,
+    uint16_t* __restrict__ tb, int32_t* __restrict__ pool, int32_t* __restrict__ aln,
+    int32_t* __restrict__ aln_len) {
+  const int lane = threadIdx.x & 63;
+  const int job_id = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (job_id >= n_jobs) return;
+  const PoaJob J = jobs[job_id];
+  const int32_t L = static_cast<int32_t>(J.len);
+  const uint64_t LS = J.ls;
+  const uint32_t V = J.n_rows;
+  const uint8_t* __restrict__ seq = seqs + J.seq_off;
+  int32_t* __restrict__ pl = pool + J.pool_off;
+  uint16_t* __restrict__ tbj = tb + J.tb_off;
+  const uint32_t* __restrict__ rinfo = row_info + J.row_off;
+  const uint32_t* __restrict__ rslot = row_slot + J.row_off;
+  const uint32_t* __restrict__ rps = row_pstart + J.pstart_off;
+  const uint32_t* __restrict__ prow = pred_row + J.pred_off;
+  const uint32_t* __restrict__ pslot = pred_slot + J.pred_off;
+  const int32_t nstrips = (L + 1 + 63) >> 6;
+
+  // virtual row 0 -> slot 0 (planes H, F, O at offsets 0, LS, 2LS)
+  for (int32_t j = lane; j <= L; j += 64) {
+    pl[j] = row0_h(P, j);
+    pl[LS + j] = j == 0 ? 0 : SVS_NEG_INF;
+    pl[2 * LS + j] = j == 0 ? 0 : SVS_NEG_INF;
+  }
+
+  int32_t best = SVS_NEG_INF;  // meaningful on the lane owning column L
+  int32_t best_row = 0;
+
+  for (uint32_t r = 0; r < V; ++r) {
+    const uint32_t info = rinfo[r];
+    const uint8_t nb = static_cast<uint8_t>(info & 0xFF);
+    const bool sink = (info >> 8) & 1;
+    const uint64_t so = static_cast<uint64_t>(rslot[r]) * 3 * LS;
+    const uint32_t p0 = rps[r];
+    const uint32_t np = rps[r + 1] - p0;
+    const uint32_t npass = np == 0 ? 1 : np;  // source nodes read virtual row 0
+
+    // column 0 of this row (spoa Initialize): gap runs down the graph
+    int32_t F0, O0;
+    if (np == 0) {
+      F0 = P.g;
+      O0 = P.q;
+    } else {
+      F0 = SVS_NEG_INF;
+      O0 = SVS_NEG_INF;
+      for (uint32_t k = 0; k < np; ++k) {
+        const uint64_t ps = static_cast<uint64_t>(pslot[p0 + k]) * 3 * LS;
+        F0 = imax(F0, pl[ps + LS]);
+        O0 = imax(O0, pl[ps + 2 * LS]);
+      }
+      F0 += P.e;
+      O0 += P.c;
+    }
+    const int32_t H0 = imax(F0, O0);
+
+    int32_t run1 = SVS_VNEG, run2 = SVS_VNEG;  // scan carries across strips
+    int32_t cHpre = H0, cQ = SVS_NEG_INF, cE = SVS_NEG_INF, cH = H0;
+
+    for (int32_t s = 0; s < nstrips; ++s) {
+      const int32_t j = (s << 6) + lane;
+      const bool valid = j <= L;
+      const bool c0 = j == 0;
+      const bool inner = valid && !c0;
+      const int32_t mc = (inner && seq[j - 1] == nb) ? P.m : P.n;
+
+      // ---- pass 1: vertical (F, O) and diagonal terms over all in-edges ----
+      int32_t F = SVS_VNEG, O = SVS_VNEG, Hd = SVS_VNEG;
+      int32_t hpm0 = 0, hp0 = 0, fp0 = 0, op0 = 0;  // first in-edge kept in registers
+      if (inner) {
+        for (uint32_t k = 0; k < npass; ++k) {
+          const uint64_t ps = np == 0 ? 0 : static_cast<uint64_t>(pslot[p0 + k]) * 3 * LS;
+          const int32_t hpm = pl[ps + j - 1];
+          const int32_t hp = pl[ps + j];
+          const int32_t fp = pl[ps + LS + j];
+          const int32_t op = pl[ps + 2 * LS + j];
+          if (k == 0) { hpm0 = hpm; hp0 = hp; fp0 = fp; op0 = op; }
+          F = imax(F, imax(hp + P.g, fp + P.e));
+          O = imax(O, imax(hp + P.q, op + P.c));
+          Hd = imax(Hd, hpm + mc);
+        }
+      } else if (c0) {
+        const uint64_t ps = np == 0 ? 0 : static_cast<uint64_t>(pslot[p0]) * 3 * LS;
+        hp0 = pl[ps];
+        fp0 = pl[ps + LS];
+        op0 = pl[ps + 2 * LS];
+        F = F0;
+        O = O0;
+      }
+      const int32_t Hpre = c0 ? H0 : imax(Hd, imax(F, O));
+
+      // ---- horizontal gaps as two prefix-max scans ----
+      const int32_t prevHpre = wave_shr1(Hpre, cHpre, lane);
+      int32_t x = inner ? prevHpre + P.q - j * P.c : SVS_VNEG;
+      x = imax(wave_prefix_max(x), run1);
+      run1 = readlane63(x);
+      const int32_t Q = inner ? x + j * P.c : SVS_NEG_INF;
+      const int32_t prevQ = wave_shr1(Q, cQ, lane);
+      int32_t y = inner ? imax(prevHpre, prevQ) + P.g - j * P.e : SVS_VNEG;
+      y = imax(wave_prefix_max(y), run2);
+      run2 = readlane63(y);
+      const int32_t E = inner ? y + j * P.e : SVS_NEG_INF;
+      const int32_t H = inner ? imax(Hpre, imax(E, Q)) : H0;
+      const int32_t prevE = wave_shr1(E, cE, lane);
+      const int32_t prevH = wave_shr1(H, cH, lane);
+
+      // ---- traceback code: replay of spoa's backtrack comparisons ----
+      if (valid) {
+        uint32_t diag_k = 31, up_k = 31, up_ext = 0, uc_k = 31, uc_stop = 0;
+        for (uint32_t k = 0; k < npass; ++k) {
+          int32_t hpm, hp, fp, op;
+          if (k == 0) {
+            hpm = hpm0; hp = hp0; fp = fp0; op = op0;
+          } else {
+            const uint64_t ps = static_cast<uint64_t>(pslot[p0 + k]) * 3 * LS;
+            hpm = inner ? pl[ps + j - 1] : 0;
+            hp = pl[ps + j];
+            fp = pl[ps + LS + j];
+            op = pl[ps + 2 * LS + j];
+          }
+          if (inner && diag_k == 31 && H == hpm + mc) diag_k = k;
+          if (up_k == 31) {
+            const bool a = H == fp + P.e, b = H == hp + P.g, c = H == op + P.c, d = H == hp + P.q;
+            if (a || b || c || d) { up_k = k; up_ext = (a || (!b && c)) ? 1u : 0u; }
+          }
+          if (np != 0 && uc_k == 31) {
+            const bool a = F == hp + P.g, b = F == fp + P.e, c = O == hp + P.q, d = O == op + P.c;
+            if (a || b || c || d) { uc_k = k; uc_stop = (a || (!b && c)) ? 1u : 0u; }
+          }
+        }
+        uint32_t code;
+        if (diag_k != 31) {
+          code = 0u | (diag_k << 3);
+        } else if (up_k != 31) {
+          code = 1u | (up_ext << 2) | (up_k << 3);
+        } else {
+          const bool a = inner && H == prevE + P.e, b = inner && H == prevH + P.g;
+          const bool c = inner && H == prevQ + P.c, d = inner && H == prevH + P.q;
+          code = (a || b || c || d) ? (2u | ((a || (!b && c)) ? 4u : 0u)) : 3u;
+        }
+        const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
+        code |= (lbit ? 1u : 0u) << 8;
+        code |= uc_stop << 9;
+        code |= uc_k << 10;
+        tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+        pl[so + j] = H;
+        pl[so + LS + j] = c0 ? F0 : F;
+        pl[so + 2 * LS + j] = c0 ? O0 : O;
+        if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
+      }
+      cHpre = readlane63(Hpre);
+      cQ = readlane63(Q);
+      cE = readlane63(E);
+      cH = readlane63(H);
+    }
+  }
+
+  // Make the wave's traceback-code stores visible to its own lane 0.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+
+  const int owner = L & 63;
+  best_row = __shfl(best_row, owner, 64);
+  if (lane != 0) return;
+
+  // ---- traceback (spoa backtrack order), lane 0 ----
+  int32_t* out = aln + 2 * J.aln_off;
+  const int64_t cap = static_cast<int64_t>(V) + L + 1;
+  int64_t n = 0;
+  int32_t i = best_row, jj = L;
+  bool ok = best_row > 0 || V == 0;
+  auto tbc = [&](int32_t row, int32_t col) -> uint32_t {
+    return tbj[static_cast<uint64_t>(row - 1) * LS + col];
+  };
+  auto pred_of = [&](int32_t row, uint32_t k) -> int32_t {
+    const uint32_t a = rps[row - 1], b = rps[row];
+    return (b == a) ? 0 : static_cast<int32_t>(prow[a + k]);
+  };
+  while (ok && !(i == 0 && jj == 0)) {
+    int32_t pi = i, pj = jj;
+    bool el = false, eu = false;
+    if (i == 0) {
+      const int32_t Hij = row0_h(P, jj);
+      const bool a = Hij == row0_e(P, jj - 1) + P.e, b = Hij == row0_h(P, jj - 1) + P.g;
+      const bool c = Hij == row0_q(P, jj - 1) + P.c, d = Hij == row0_h(P, jj - 1) + P.q;
+      if (!(a || b || c || d)) { ok = false; break; }
+      el = a || (!b && c);
+      pj = jj - 1;
+    } else {
+      const uint32_t code = tbc(i, jj);
+      const uint32_t t = code & 3u, k = (code >> 3) & 31u;
+      if (t == 0) { pi = pred_of(i, k); pj = jj - 1; }
+      else if (t == 1) { pi = pred_of(i, k); eu = (code >> 2) & 1u; }
+      else if (t == 2) { pj = jj - 1; el = (code >> 2) & 1u; }
+      else { ok = false; break; }
+    }
+    if (n >= cap) { ok = false; break; }
+    out[2 * n] = (pi == i) ? -1 : i - 1;
+    out[2 * n + 1] = (pj == jj) ? -1 : jj - 1;
+    ++n;
+    i = pi;
+    jj = pj;
+    if (el) {
+      while (true) {
+        if (n >= cap || jj <= 0) { ok = false; break; }
+        out[2 * n] = -1;
+        out[2 * n + 1] = jj - 1;
+        ++n;
+        --jj;
+        bool stop;
+        if (i == 0) {
+          stop = row0_h(P, jj) + P.g == row0_e(P, jj + 1) || row0_h(P, jj) + P.q == row0_q(P, jj + 1);
+        } else {
+          stop = (tbc(i, jj + 1) >> 8) & 1u;
+        }
+        if (stop) break;
+      }
+    } else if (eu) {
+      while (true) {
+        if (n >= cap || i <= 0) { ok = false; break; }
+        const uint32_t code = tbc(i, jj);
+        const uint32_t k = (code >> 10) & 31u;
+        const bool stop = (code >> 9) & 1u;
+        const int32_t nxt = (k == 31u) ? 0 : pred_of(i, k);
+        out[2 * n] = i - 1;
+        out[2 * n + 1] = -1;
+        ++n;
+        i = nxt;
+        if (stop || i == 0) break;
+      }
+    }
+  }
+  aln_len[job_id] = ok ? static_cast<int32_t>(n) : -1;
+}
+
+hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream) {
+  if (a.n_jobs <= 0) return hipSuccess;
+  const int waves_per_block = 4;
+  const int blocks = (a.n_jobs + waves_per_block - 1) / waves_per_block;
+  hipLaunchKernelGGL(poa_nw_convex_kernel, dim3(blocks), dim3(64 * waves_per_block), 0, stream,
+                     a.jobs, a.n_jobs, a.score, a.row_info, a.row_slot, a.row_pstart, a.pred_row,
+                     a.pred_slot, a.seqs, a.tb, a.pool, a.aln, a.aln_len);
+  return hipGetLastError();
+}
+
+// ---- self-test kernels for the wave primitives (used by the GPU tests) ----
+__global__ void wave_scan_selftest_kernel(const int32_t* in, int32_t* out_scan, int32_t* out_shift) {
+  const int lane = threadIdx.x & 63;
+  const int32_t x = in[blockIdx.x * 64 + lane];
+  out_scan[blockIdx.x * 64 + lane] = wave_prefix_max(x);
+  out_shift[blockIdx.x * 64 + lane] = wave_shr1(x, -7, lane);
+}
+
+hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
+                                hipStream_t stream) {
+  hipLaunchKernelGGL(wave_scan_selftest_kernel, dim3(n_waves), dim3(64), 0, stream, in, scan, shift);
+  return hipGetLastError();
+}
+
+}  // namespace svs

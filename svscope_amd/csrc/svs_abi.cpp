@@ -1,0 +1,209 @@
+// extern "C" surface of libsvscope_hip.so (declared in include/svscope.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/svscope.h"
+#include "svs_context.hpp"
+#include "svs_device.hpp"
+#include "svs_internal.hpp"
+
+struct svs_poa_result {
+  std::vector<std::string> consensus;
+  std::vector<std::string> msa_block;
+  std::vector<int32_t> rows, cols;
+  svs_poa_stats stats{};
+};
+
+namespace {
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return SVS_OK;
+  } catch (const svs::SvsError& e) {
+    return fail(e.code, e.what());
+  } catch (const std::bad_alloc&) {
+    return fail(SVS_E_NOMEM, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(SVS_E_INTERNAL, e.what());
+  }
+}
+
+unsigned host_threads() {
+  if (const char* s = std::getenv("SVS_HOST_THREADS")) {
+    const int v = std::atoi(s);
+    if (v > 0) return static_cast<unsigned>(v);
+  }
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  return std::min(hw, 16u);
+}
+}  // namespace
+
+extern "C" {
+
+const char* svs_last_error(void) { return g_last_error.c_str(); }
+
+int svs_device_count(int* out) {
+  if (!out) return fail(SVS_E_INVALID, "null out");
+  return guarded([&] {
+    int n = 0;
+    SVS_HIP(hipGetDeviceCount(&n));
+    *out = n;
+  });
+}
+
+int svs_init(int device_ordinal, svs_context** out) {
+  if (!out) return fail(SVS_E_INVALID, "null out");
+  *out = nullptr;
+  svs_context* ctx = nullptr;
+  const int rc = guarded([&] {
+    int n = 0;
+    SVS_HIP(hipGetDeviceCount(&n));
+    if (device_ordinal < 0 || device_ordinal >= n)
+      throw svs::SvsError(SVS_E_HIP, "no HIP device " + std::to_string(device_ordinal) + " (found " +
+                                         std::to_string(n) + ")");
+    SVS_HIP(hipSetDevice(device_ordinal));
+    ctx = new svs_context();
+    ctx->device = device_ordinal;
+    SVS_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    SVS_HIP(hipEventCreate(&ctx->ev_start));
+    SVS_HIP(hipEventCreate(&ctx->ev_stop));
+    size_t free_b = 0, total_b = 0;
+    SVS_HIP(hipMemGetInfo(&free_b, &total_b));
+    size_t budget = free_b / 2;
+    if (const char* s = std::getenv("SVS_DEVICE_BUDGET_GB")) {
+      const double gb = std::atof(s);
+      if (gb > 0) budget = static_cast<size_t>(gb * (1ull << 30));
+    }
+    ctx->device_budget = std::max<size_t>(budget, 64ull << 20);
+    ctx->pool = new svs::ThreadPool(host_threads());
+  });
+  if (rc != SVS_OK) {
+    if (ctx) svs_release(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return SVS_OK;
+}
+
+void svs_release(svs_context* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (svs::DeviceBuf* b : {&ctx->d_jobs, &ctx->d_row_info, &ctx->d_row_slot, &ctx->d_row_pstart,
+                            &ctx->d_pred_row, &ctx->d_pred_slot, &ctx->d_seqs, &ctx->d_tb, &ctx->d_pool,
+                            &ctx->d_aln, &ctx->d_aln_len, &ctx->d_em_in, &ctx->d_em_ws, &ctx->d_em_out,
+                            &ctx->d_rng})
+    b->release();
+  for (svs::PinnedBuf* b : {&ctx->h_stage, &ctx->h_aln, &ctx->h_aln_len, &ctx->h_em_in, &ctx->h_em_out})
+    b->release();
+  if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
+  if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx->pool;
+  delete ctx;
+}
+
+int svs_poa_batch(svs_context* ctx, int32_t n_jobs, const int64_t* job_seq_start,
+                  const int64_t* seq_byte_start, const char* seq_bytes, const svs_poa_config* cfg,
+                  svs_poa_result** out) {
+  if (!ctx || !out || !cfg || n_jobs < 0 || (n_jobs > 0 && (!job_seq_start || !seq_byte_start)))
+    return fail(SVS_E_INVALID, "svs_poa_batch: invalid argument");
+  *out = nullptr;
+  svs_poa_result* res = nullptr;
+  const int rc = guarded([&] {
+    SVS_HIP(hipSetDevice(ctx->device));
+    svs::check_poa_config(*cfg);
+    std::vector<svs::PoaTask> tasks(static_cast<size_t>(n_jobs));
+    for (int32_t j = 0; j < n_jobs; ++j) {
+      const int64_t a = job_seq_start[j], b = job_seq_start[j + 1];
+      if (b < a || a < 0) throw svs::SvsError(SVS_E_INVALID, "job_seq_start not monotone");
+      for (int64_t s = a; s < b; ++s) {
+        const int64_t x = seq_byte_start[s], y = seq_byte_start[s + 1];
+        if (y < x || x < 0) throw svs::SvsError(SVS_E_INVALID, "seq_byte_start not monotone");
+        if (y > x && !seq_bytes) throw svs::SvsError(SVS_E_INVALID, "null seq_bytes");
+        tasks[j].seqs.emplace_back(y > x ? seq_bytes + x : "", static_cast<size_t>(y - x));
+      }
+    }
+    res = new svs_poa_result();
+    svs::run_poa_tasks(ctx, tasks, *cfg, res->stats);
+    res->consensus.resize(tasks.size());
+    res->msa_block.resize(tasks.size());
+    res->rows.assign(tasks.size(), 0);
+    res->cols.assign(tasks.size(), 0);
+    for (size_t j = 0; j < tasks.size(); ++j) {
+      res->consensus[j] = std::move(tasks[j].consensus);
+      const auto& m = tasks[j].msa;
+      res->rows[j] = static_cast<int32_t>(m.size());
+      res->cols[j] = m.empty() ? 0 : static_cast<int32_t>(m[0].size());
+      std::string& blk = res->msa_block[j];
+      blk.reserve(m.size() * (m.empty() ? 0 : m[0].size()));
+      for (const auto& row : m) blk += row;
+    }
+  });
+  if (rc != SVS_OK) {
+    delete res;
+    return rc;
+  }
+  *out = res;
+  return SVS_OK;
+}
+
+int svs_poa_result_consensus(const svs_poa_result* r, int32_t job, const char** data, int64_t* len) {
+  if (!r || !data || !len || job < 0 || job >= static_cast<int32_t>(r->consensus.size()))
+    return fail(SVS_E_INVALID, "svs_poa_result_consensus: invalid argument");
+  *data = r->consensus[job].data();
+  *len = static_cast<int64_t>(r->consensus[job].size());
+  return SVS_OK;
+}
+
+int svs_poa_result_msa(const svs_poa_result* r, int32_t job, int32_t* rows, int32_t* cols,
+                       const char** data) {
+  if (!r || !rows || !cols || !data || job < 0 || job >= static_cast<int32_t>(r->rows.size()))
+    return fail(SVS_E_INVALID, "svs_poa_result_msa: invalid argument");
+  *rows = r->rows[job];
+  *cols = r->cols[job];
+  *data = r->msa_block[job].data();
+  return SVS_OK;
+}
+
+int svs_poa_result_stats(const svs_poa_result* r, svs_poa_stats* out) {
+  if (!r || !out) return fail(SVS_E_INVALID, "svs_poa_result_stats: invalid argument");
+  *out = r->stats;
+  return SVS_OK;
+}
+
+void svs_poa_result_free(svs_poa_result* r) { delete r; }
+
+int svs_wave_selftest(svs_context* ctx, const int32_t* in, int32_t* scan, int32_t* shift, int32_t n_waves) {
+  if (!ctx || !in || !scan || !shift || n_waves <= 0) return fail(SVS_E_INVALID, "svs_wave_selftest: invalid argument");
+  return guarded([&] {
+    SVS_HIP(hipSetDevice(ctx->device));
+    const size_t bytes = static_cast<size_t>(n_waves) * 64 * 4;
+    int32_t* d = nullptr;
+    SVS_HIP(hipMalloc(&d, 3 * bytes));
+    hipError_t e = hipMemcpy(d, in, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = svs::launch_wave_selftest(d, d + n_waves * 64, d + 2 * n_waves * 64, n_waves, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipMemcpy(scan, d + n_waves * 64, bytes, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(shift, d + 2 * n_waves * 64, bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    SVS_HIP(e);
+  });
+}
+
+}  // extern "C"

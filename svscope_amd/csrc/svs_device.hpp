@@ -1,0 +1,48 @@
+// Device-side job descriptors shared by the host engine and the HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace svs {
+
+struct PoaScore {
+  int32_t m, n, g, e, q, c;
+};
+
+// One read-vs-graph NW alignment (one wave).  Offsets are element offsets into
+// the batch-wide buffers of PoaLaunch.
+struct PoaJob {
+  uint64_t tb_off;    // uint16 traceback codes, rows 1..n_rows, stride ls
+  uint64_t pool_off;  // int32 row pool: n_slots x {H,F,O} x ls
+  uint64_t aln_off;   // output pairs (2 x int32), capacity n_rows + len + 1
+  uint32_t row_off;   // into row_info / row_slot
+  uint32_t pstart_off;  // into row_pstart (n_rows + 1 entries)
+  uint32_t pred_off;  // base of this job's pred_row / pred_slot entries
+  uint32_t seq_off;   // into seqs (bytes)
+  uint32_t n_rows;    // graph nodes
+  uint32_t len;       // read length
+  uint32_t ls;        // row stride (>= len + 1, multiple of 64)
+  uint32_t n_slots;   // pool slots (slot 0 = virtual row 0)
+};
+
+struct PoaLaunch {
+  const PoaJob* jobs;
+  int n_jobs;
+  PoaScore score;
+  const uint32_t* row_info;
+  const uint32_t* row_slot;
+  const uint32_t* row_pstart;
+  const uint32_t* pred_row;
+  const uint32_t* pred_slot;
+  const uint8_t* seqs;
+  uint16_t* tb;
+  int32_t* pool;
+  int32_t* aln;
+  int32_t* aln_len;
+};
+
+hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream);
+hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
+                                hipStream_t stream);
+
+}  // namespace svs

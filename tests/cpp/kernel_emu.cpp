@@ -1,0 +1,229 @@
+// TEST INFRASTRUCTURE: scalar CPU emulation of svscope_amd/csrc/poa_kernels.hip
+// (lanes become a loop) driven by the product's host graph engine
+// (poa_graph.cpp).  Lets the CPU test suite check the kernel's two-scan
+// recurrence, traceback codes and code-driven traceback against the oracle
+// without a GPU.  Not part of the product library.
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../svscope_amd/csrc/poa_graph.hpp"
+
+namespace {
+constexpr int32_t NEG_INF = INT32_MIN + 1024;
+constexpr int32_t VNEG = INT32_MIN / 2;
+struct Score { int32_t m, n, g, e, q, c; };
+
+int32_t r0e(const Score& P, int32_t j) { return j == 0 ? 0 : P.g + (j - 1) * P.e; }
+int32_t r0q(const Score& P, int32_t j) { return j == 0 ? 0 : P.q + (j - 1) * P.c; }
+int32_t r0h(const Score& P, int32_t j) { return j == 0 ? 0 : std::max(r0q(P, j), r0e(P, j)); }
+
+// returns forward rank pairs
+std::vector<int32_t> emu_align(const svs::RowTables& T, const std::string& seq, const Score& P) {
+  const int32_t L = static_cast<int32_t>(seq.size());
+  const uint64_t LS = (static_cast<uint64_t>(L) + 1 + 63) / 64 * 64;
+  const uint32_t V = static_cast<uint32_t>(T.info.size());
+  std::vector<int32_t> pl(static_cast<size_t>(T.n_slots) * 3 * LS);
+  std::vector<uint16_t> tb(static_cast<size_t>(V) * LS);
+  for (int32_t j = 0; j <= L; ++j) {
+    pl[j] = r0h(P, j);
+    pl[LS + j] = j == 0 ? 0 : NEG_INF;
+    pl[2 * LS + j] = j == 0 ? 0 : NEG_INF;
+  }
+  const int32_t nstrips = (L + 1 + 63) >> 6;
+  int32_t best = NEG_INF, best_row = 0;
+  int32_t Hpre[64], Fv[64], Ov[64], Q[64], E[64], H[64], x[64], y[64], pHpre[64], pQ[64], pE[64], pH[64];
+  for (uint32_t r = 0; r < V; ++r) {
+    const uint8_t nb = T.info[r] & 0xFF;
+    const bool sink = (T.info[r] >> 8) & 1;
+    const uint64_t so = static_cast<uint64_t>(T.slot[r]) * 3 * LS;
+    const uint32_t p0 = T.pstart[r], np = T.pstart[r + 1] - p0, npass = np ? np : 1;
+    int32_t F0, O0;
+    if (np == 0) { F0 = P.g; O0 = P.q; }
+    else {
+      F0 = O0 = NEG_INF;
+      for (uint32_t k = 0; k < np; ++k) {
+        const uint64_t ps = static_cast<uint64_t>(T.pred_slot[p0 + k]) * 3 * LS;
+        F0 = std::max(F0, pl[ps + LS]);
+        O0 = std::max(O0, pl[ps + 2 * LS]);
+      }
+      F0 += P.e; O0 += P.c;
+    }
+    const int32_t H0 = std::max(F0, O0);
+    int32_t run1 = VNEG, run2 = VNEG, cHpre = H0, cQ = NEG_INF, cE = NEG_INF, cH = H0;
+    for (int32_t s = 0; s < nstrips; ++s) {
+      auto pslot = [&](uint32_t k) -> uint64_t {
+        return np == 0 ? 0 : static_cast<uint64_t>(T.pred_slot[p0 + k]) * 3 * LS;
+      };
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = s * 64 + l;
+        const bool valid = j <= L, c0 = j == 0, inner = valid && !c0;
+        const int32_t mc = (inner && static_cast<uint8_t>(seq[j - 1]) == nb) ? P.m : P.n;
+        int32_t F = VNEG, O = VNEG, Hd = VNEG;
+        if (inner) {
+          for (uint32_t k = 0; k < npass; ++k) {
+            const uint64_t ps = pslot(k);
+            F = std::max(F, std::max(pl[ps + j] + P.g, pl[ps + LS + j] + P.e));
+            O = std::max(O, std::max(pl[ps + j] + P.q, pl[ps + 2 * LS + j] + P.c));
+            Hd = std::max(Hd, pl[ps + j - 1] + mc);
+          }
+        } else if (c0) { F = F0; O = O0; }
+        Fv[l] = F; Ov[l] = O;
+        Hpre[l] = c0 ? H0 : std::max(Hd, std::max(F, O));
+      }
+      for (int l = 0; l < 64; ++l) pHpre[l] = l == 0 ? cHpre : Hpre[l - 1];
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = s * 64 + l; const bool inner = j <= L && j != 0;
+        x[l] = inner ? pHpre[l] + P.q - j * P.c : VNEG;
+      }
+      for (int l = 1; l < 64; ++l) x[l] = std::max(x[l], x[l - 1]);
+      for (int l = 0; l < 64; ++l) x[l] = std::max(x[l], run1);
+      run1 = x[63];
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = s * 64 + l; const bool inner = j <= L && j != 0;
+        Q[l] = inner ? x[l] + j * P.c : NEG_INF;
+      }
+      for (int l = 0; l < 64; ++l) pQ[l] = l == 0 ? cQ : Q[l - 1];
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = s * 64 + l; const bool inner = j <= L && j != 0;
+        y[l] = inner ? std::max(pHpre[l], pQ[l]) + P.g - j * P.e : VNEG;
+      }
+      for (int l = 1; l < 64; ++l) y[l] = std::max(y[l], y[l - 1]);
+      for (int l = 0; l < 64; ++l) y[l] = std::max(y[l], run2);
+      run2 = y[63];
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = s * 64 + l; const bool inner = j <= L && j != 0;
+        E[l] = inner ? y[l] + j * P.e : NEG_INF;
+        H[l] = inner ? std::max(Hpre[l], std::max(E[l], Q[l])) : H0;
+      }
+      for (int l = 0; l < 64; ++l) { pE[l] = l == 0 ? cE : E[l - 1]; pH[l] = l == 0 ? cH : H[l - 1]; }
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = s * 64 + l;
+        const bool valid = j <= L, c0 = j == 0, inner = valid && !c0;
+        if (!valid) continue;
+        const int32_t mc = (inner && static_cast<uint8_t>(seq[j - 1]) == nb) ? P.m : P.n;
+        uint32_t dk = 31, uk = 31, ue = 0, ck = 31, cs = 0;
+        for (uint32_t k = 0; k < npass; ++k) {
+          const uint64_t ps = pslot(k);
+          const int32_t hpm = inner ? pl[ps + j - 1] : 0, hp = pl[ps + j], fp = pl[ps + LS + j], op = pl[ps + 2 * LS + j];
+          if (inner && dk == 31 && H[l] == hpm + mc) dk = k;
+          if (uk == 31) {
+            const bool a = H[l] == fp + P.e, b = H[l] == hp + P.g, c = H[l] == op + P.c, d = H[l] == hp + P.q;
+            if (a || b || c || d) { uk = k; ue = (a || (!b && c)) ? 1 : 0; }
+          }
+          if (np != 0 && ck == 31) {
+            const bool a = Fv[l] == hp + P.g, b = Fv[l] == fp + P.e, c = Ov[l] == hp + P.q, d = Ov[l] == op + P.c;
+            if (a || b || c || d) { ck = k; cs = (a || (!b && c)) ? 1 : 0; }
+          }
+        }
+        uint32_t code;
+        if (dk != 31) code = dk << 3;
+        else if (uk != 31) code = 1u | (ue << 2) | (uk << 3);
+        else {
+          const bool a = inner && H[l] == pE[l] + P.e, b = inner && H[l] == pH[l] + P.g;
+          const bool c = inner && H[l] == pQ[l] + P.c, d = inner && H[l] == pH[l] + P.q;
+          code = (a || b || c || d) ? (2u | ((a || (!b && c)) ? 4u : 0u)) : 3u;
+        }
+        const bool lbit = inner && (pH[l] + P.g == E[l] || pH[l] + P.q == Q[l]);
+        code |= (lbit ? 1u : 0u) << 8;
+        code |= cs << 9;
+        code |= ck << 10;
+        tb[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+        if (sink && j == L && H[l] > best) { best = H[l]; best_row = static_cast<int32_t>(r) + 1; }
+      }
+      // stores after all lanes read this strip's pred values (row slots differ from pred slots)
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = s * 64 + l;
+        if (j > L) continue;
+        pl[so + j] = H[l];
+        pl[so + LS + j] = j == 0 ? F0 : Fv[l];
+        pl[so + 2 * LS + j] = j == 0 ? O0 : Ov[l];
+      }
+      cHpre = Hpre[63]; cQ = Q[63]; cE = E[63]; cH = H[63];
+    }
+  }
+  std::vector<int32_t> out;
+  auto tbc = [&](int32_t row, int32_t col) -> uint32_t { return tb[static_cast<uint64_t>(row - 1) * LS + col]; };
+  auto pred_of = [&](int32_t row, uint32_t k) -> int32_t {
+    const uint32_t a = T.pstart[row - 1], b = T.pstart[row];
+    return b == a ? 0 : static_cast<int32_t>(T.pred_row[a + k]);
+  };
+  int32_t i = best_row, jj = L;
+  while (!(i == 0 && jj == 0)) {
+    int32_t pi = i, pj = jj;
+    bool el = false, eu = false;
+    if (i == 0) {
+      const int32_t Hij = r0h(P, jj);
+      const bool a = Hij == r0e(P, jj - 1) + P.e, b = Hij == r0h(P, jj - 1) + P.g;
+      const bool c = Hij == r0q(P, jj - 1) + P.c, d = Hij == r0h(P, jj - 1) + P.q;
+      if (!(a || b || c || d)) throw std::runtime_error("emu: row0 no move");
+      el = a || (!b && c);
+      pj = jj - 1;
+    } else {
+      const uint32_t code = tbc(i, jj), t = code & 3u, k = (code >> 3) & 31u;
+      if (t == 0) { pi = pred_of(i, k); pj = jj - 1; }
+      else if (t == 1) { pi = pred_of(i, k); eu = (code >> 2) & 1u; }
+      else if (t == 2) { pj = jj - 1; el = (code >> 2) & 1u; }
+      else throw std::runtime_error("emu: no move");
+    }
+    out.push_back(pi == i ? -1 : i - 1);
+    out.push_back(pj == jj ? -1 : jj - 1);
+    i = pi; jj = pj;
+    if (el) {
+      while (true) {
+        out.push_back(-1); out.push_back(jj - 1); --jj;
+        const bool stop = i == 0 ? (r0h(P, jj) + P.g == r0e(P, jj + 1) || r0h(P, jj) + P.q == r0q(P, jj + 1))
+                                 : ((tbc(i, jj + 1) >> 8) & 1u);
+        if (stop) break;
+      }
+    } else if (eu) {
+      while (true) {
+        const uint32_t code = tbc(i, jj), k = (code >> 10) & 31u;
+        const bool stop = (code >> 9) & 1u;
+        const int32_t nxt = k == 31u ? 0 : pred_of(i, k);
+        out.push_back(i - 1); out.push_back(-1);
+        i = nxt;
+        if (stop || i == 0) break;
+      }
+    }
+  }
+  std::vector<int32_t> fwd(out.size());
+  const size_t n = out.size() / 2;
+  for (size_t k = 0; k < n; ++k) { fwd[2 * k] = out[2 * (n - 1 - k)]; fwd[2 * k + 1] = out[2 * (n - 1 - k) + 1]; }
+  return fwd;
+}
+
+struct EmuResult { std::string consensus, error; std::vector<std::string> msa; uint32_t max_slots = 0; };
+}  // namespace
+
+extern "C" {
+void* emu_poa(int n, const char* const* seqs, const int* lens, int m, int mis, int g, int e, int q, int c) {
+  auto* r = new EmuResult();
+  try {
+    Score P{m, mis, g, e, q, c};
+    svs::PoaGraph graph;
+    svs::RowTables T;
+    for (int s = 0; s < n; ++s) {
+      std::string seq(seqs[s], static_cast<size_t>(lens[s]));
+      if (seq.empty()) continue;
+      if (graph.empty()) { graph.add_alignment_nodes({}, seq); continue; }
+      graph.export_rows(&T);
+      r->max_slots = std::max(r->max_slots, T.n_slots);
+      graph.add_alignment_ranks(emu_align(T, seq, P), seq);
+    }
+    r->consensus = graph.consensus(-1);
+    r->msa = graph.msa();
+  } catch (const std::exception& ex) { r->error = ex.what(); }
+  return r;
+}
+const char* emu_error(void* h) { auto* r = static_cast<EmuResult*>(h); return r->error.empty() ? nullptr : r->error.c_str(); }
+const char* emu_consensus(void* h) { return static_cast<EmuResult*>(h)->consensus.c_str(); }
+int emu_msa_rows(void* h) { return static_cast<int>(static_cast<EmuResult*>(h)->msa.size()); }
+const char* emu_msa_row(void* h, int i) { return static_cast<EmuResult*>(h)->msa[i].c_str(); }
+int emu_max_slots(void* h) { return static_cast<int>(static_cast<EmuResult*>(h)->max_slots); }
+void emu_free(void* h) { delete static_cast<EmuResult*>(h); }
+}

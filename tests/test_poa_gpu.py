@@ -1,0 +1,85 @@
+"""GPU parity of the POA seam: svscope_amd.poa (HIP kernel through the C ABI)
+against the CPU oracle, bit-exact on consensus and every MSA row."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle.spoa_oracle import poa as oracle_poa
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+
+
+def test_wave_primitives(gpu_ctx):
+    rs = np.random.RandomState(3)
+    n_waves = 64
+    x = rs.randint(-10 ** 6, 10 ** 6, size=n_waves * 64).astype(np.int32)
+    x[::7] = -(2 ** 30)
+    scan = np.zeros_like(x)
+    shift = np.zeros_like(x)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    from svscope_amd import _abi
+    _abi.check(gpu_ctx.lib.svs_wave_selftest(gpu_ctx.handle, p(x), p(scan), p(shift), n_waves))
+    xr = x.reshape(n_waves, 64)
+    np.testing.assert_array_equal(scan.reshape(n_waves, 64), np.maximum.accumulate(xr, axis=1))
+    exp_shift = np.concatenate([np.full((n_waves, 1), -7, np.int32), xr[:, :-1]], axis=1)
+    np.testing.assert_array_equal(shift.reshape(n_waves, 64), exp_shift)
+
+
+def test_handchecked_fixtures_on_gpu():
+    import json, os
+    from svscope_amd.poa import poa
+    cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "poa_handchecked.json")))
+    for c in cases:
+        assert poa(c["seqs"], 1) == (c["consensus"], c["msa"]), c
+
+
+def test_random_cases_batched_match_oracle():
+    from svscope_amd.poa import poa_batch
+    cases = helpers.random_cases(101, 400)
+    got = poa_batch(cases)
+    for seqs, g in zip(cases, got):
+        assert g == oracle_poa(seqs, 1), seqs
+
+
+def test_longer_random_cases_match_oracle():
+    from svscope_amd.poa import poa_batch
+    cases = helpers.random_cases(7, 60, max_seqs=12, max_len=300, edits=25)
+    got = poa_batch(cases)
+    for seqs, g in zip(cases, got):
+        assert g == oracle_poa(seqs, 1)
+
+
+def test_single_equals_batch():
+    from svscope_amd.poa import poa, poa_batch
+    cases = helpers.random_cases(5, 20)
+    batched = poa_batch(cases)
+    for seqs, b in zip(cases, batched):
+        assert poa(seqs, 1) == b
+
+
+def test_synthetic_windows_match_oracle():
+    from svscope_amd import synth
+    from svscope_amd.poa import poa_batch
+    wins = [synth.make_window(w, 16, 2000) for w in range(2)] + [synth.make_window(7, 8, 3000)]
+    got = poa_batch([w[0] for w in wins])
+    for w, g in zip(wins, got):
+        assert g == oracle_poa(w[0], 1)
+
+
+def test_unsupported_modes_raise():
+    from svscope_amd import _abi
+    from svscope_amd.poa import poa
+    with pytest.raises(_abi.SvsError):
+        poa(["ACGT", "ACGA"], 0)
+    with pytest.raises(_abi.SvsError):
+        poa(["ACGT", "ACGA"], 1, g=-2, e=-6)  # linear subtype
+
+
+def test_genmsa_false_and_min_coverage():
+    from svscope_amd.poa import poa
+    seqs = ["ACGTTGCA", "ACGTGCA", "ACGATGCA", "TTACGTTGCA"]
+    cons, msa = poa(seqs, 1, genmsa=False)
+    assert msa == [] and cons == oracle_poa(seqs, 1)[0]
+    assert poa(seqs, 1, min_coverage=3) == oracle_poa(seqs, 1, min_coverage=3)

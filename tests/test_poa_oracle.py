@@ -1,0 +1,43 @@
+"""Oracle (CPU spoa restatement) against hand-derived fixtures, and the kernel
+emulator (CPU restatement of the HIP kernel's wave algorithm + the product's
+host graph engine) against the oracle."""
+import json
+import os
+
+import pytest
+
+from oracle.spoa_oracle import poa as oracle_poa
+from tests import helpers
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "poa_handchecked.json")
+
+
+def test_oracle_hand_checked_fixtures():
+    cases = json.load(open(GOLD))
+    assert len(cases) >= 8
+    for case in cases:
+        cons, msa = oracle_poa(case["seqs"], 1)
+        assert cons == case["consensus"], case
+        assert msa == case["msa"], case
+
+
+def test_oracle_rejects_unsupported_modes():
+    with pytest.raises(RuntimeError):
+        oracle_poa(["ACGT", "ACGT"], 0)
+
+
+@pytest.fixture(scope="module")
+def emu():
+    return helpers.build_emu()
+
+
+def test_emulator_matches_oracle_random(emu):
+    for seqs in helpers.random_cases(11, 250):
+        assert helpers.emu_poa(emu, seqs) == oracle_poa(seqs, 1), seqs
+
+
+def test_emulator_matches_oracle_synthetic_windows(emu):
+    from svscope_amd import synth
+    for w in range(3):
+        win = synth.make_window(w, 8, 500)
+        assert helpers.emu_poa(emu, win[0]) == oracle_poa(win[0], 1)

@@ -1,0 +1,33 @@
+"""Times the batched GPU POA on synthetic windows (window MSA only)."""
+import argparse
+import json
+import sys
+import time
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from svscope_amd import synth
+from svscope_amd.poa import poa_batch
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--windows", type=int, default=64)
+ap.add_argument("--reads", type=int, default=64)
+ap.add_argument("--ref-len", type=int, default=3000)
+ap.add_argument("--check", type=int, default=0, help="oracle-check this many windows")
+a = ap.parse_args()
+t = time.time()
+wins = [synth.make_window(w, a.reads, a.ref_len) for w in range(a.windows)]
+print(f"synth {time.time() - t:.1f}s", flush=True)
+poa_batch([wins[0][0][:3]])  # warm up context
+t = time.time()
+out, st = poa_batch([w[0] for w in wins], return_stats=True)
+wall = time.time() - t
+st["windows_per_s"] = a.windows / wall
+st["gcups_kernel"] = st["dp_cells"] / (st["kernel_ms"] * 1e-3) / 1e9
+st["wall_s"] = wall
+print(json.dumps(st), flush=True)
+if a.check:
+    from oracle.spoa_oracle import poa as oracle_poa
+    for w, g in zip(wins[:a.check], out):
+        assert g == oracle_poa(w[0], 1), "MISMATCH"
+    print("oracle check ok", a.check)
