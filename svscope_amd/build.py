@@ -24,6 +24,7 @@ SOURCES = [
     "poa_kernels.hip",
     "em_kernels.hip",
     "poa_graph.cpp",
+    "svs_threadpool.cpp",
     "svs_poa_engine.cpp",
     "svs_em_engine.cpp",
     "svs_abi.cpp",

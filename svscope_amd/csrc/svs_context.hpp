@@ -3,14 +3,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <atomic>
-#include <condition_variable>
+#include "threadpool.hpp"
+
 #include <cstdint>
-#include <functional>
-#include <mutex>
 #include <stdexcept>
 #include <string>
-#include <thread>
 #include <vector>
 
 namespace svs {
@@ -75,28 +72,6 @@ struct PinnedBuf {
     ptr = nullptr;
     cap = 0;
   }
-};
-
-// Fork-join pool: parallel_for(n, fn) runs fn(i) for i in [0, n).
-class ThreadPool {
- public:
-  explicit ThreadPool(unsigned n);
-  ~ThreadPool();
-  unsigned size() const { return static_cast<unsigned>(workers_.size()) + 1; }
-  void parallel_for(size_t n, const std::function<void(size_t)>& fn);
-
- private:
-  void worker_loop();
-  std::vector<std::thread> workers_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  const std::function<void(size_t)>* fn_ = nullptr;
-  size_t n_ = 0;
-  std::atomic<size_t> next_{0};
-  unsigned active_ = 0;
-  uint64_t generation_ = 0;
-  bool stop_ = false;
-  std::exception_ptr err_;
 };
 
 }  // namespace svs
