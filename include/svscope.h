@@ -75,6 +75,50 @@ int svs_poa_result_msa(const svs_poa_result* r, int32_t job, int32_t* rows, int3
 int svs_poa_result_stats(const svs_poa_result* r, svs_poa_stats* out);
 void svs_poa_result_free(svs_poa_result* r);
 
+/* ---------------------------------------------------------------- EM seam */
+typedef struct svs_em_result svs_em_result;
+
+/* One window's feature matrix: n_reads x n_feat symbols 0..4 (A,T,C,G,-;
+ * DataScanner.SeqEncoder) at X + x_off, row-major; its fcluster labels for
+ * K = 1..kmax-1 (kmax = min(max_c+1, n_reads)), (kmax-1) rows of n_reads int32
+ * at labels + label_off (scipy fcluster(ward linkage(S), K, 'maxclust')). */
+typedef struct svs_em_window {
+  int32_t n_reads;
+  int32_t n_feat;
+  int64_t x_off;
+  int64_t label_off;
+} svs_em_window;
+
+/* EMCluster(seqdatamx, initselection=1, max_C=9): n_step=20 (EM :190),
+ * eps=1e-10 (CheckParam :70), seed=2023 (:42; re-seeded per window). */
+typedef struct svs_em_config {
+  int32_t max_c;
+  int32_t n_step;
+  int32_t seed;
+  int32_t want_params; /* also return gamma/pi/theta of the chosen K */
+  double eps;
+} svs_em_config;
+
+#define SVS_EM_K 0        /* int32[1]  chosen K (after the K=1 -> 2 rule) */
+#define SVS_EM_RCLUST 1   /* int32[N]  argmax gamma (first max) */
+#define SVS_EM_BIC 2      /* double[kmax-1] BICList */
+#define SVS_EM_LIK 3      /* double[N] per-read loglik of the chosen K, last iteration */
+#define SVS_EM_GAMMA 4    /* double[N*K] (want_params) */
+#define SVS_EM_PI 5       /* double[K]   (want_params) */
+#define SVS_EM_THETA 6    /* double[K*nf*5] (want_params) */
+#define SVS_EM_RNG_USED 7 /* int64[1] exponentials consumed by dirichlet re-inits */
+
+/* pariwiseDistance (ReadsCluster.py:52-59): S[i,j] = #equal columns / n_feat,
+ * diagonal 1; window w's N*N block is written at S + s_off[w]. */
+int svs_similarity_batch(svs_context* ctx, int32_t n_windows, const svs_em_window* wins, const uint8_t* X,
+                         const int64_t* s_off, double* S);
+int svs_em_batch(svs_context* ctx, int32_t n_windows, const svs_em_window* wins, const uint8_t* X,
+                 const int32_t* labels, const svs_em_config* cfg, svs_em_result** out);
+int svs_em_result_get(const svs_em_result* r, int32_t window, int32_t field, const void** data, int64_t* count);
+void svs_em_result_free(svs_em_result* r);
+/* Host-only: numpy legacy RandomState(seed).standard_exponential(n), bitwise. */
+int svs_rng_exponential_table(uint32_t seed, int64_t n, double* out);
+
 /* Wave-primitive self test (GPU tests): per 64-lane wave, inclusive prefix max
  * and shift-right-by-one (lane 0 <- -7). */
 int svs_wave_selftest(svs_context* ctx, const int32_t* in, int32_t* scan, int32_t* shift,

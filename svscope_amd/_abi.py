@@ -81,6 +81,8 @@ def _declare_em(lib):
     if not hasattr(lib, "svs_em_batch"):
         return
     P, I32 = ctypes.c_void_p, ctypes.c_int32
+    lib.svs_rng_exponential_table.argtypes = [ctypes.c_uint32, ctypes.c_int64, P]
+    lib.svs_rng_exponential_table.restype = ctypes.c_int
     lib.svs_similarity_batch.argtypes = [P, I32, P, P, P, P]
     lib.svs_similarity_batch.restype = ctypes.c_int
     lib.svs_em_batch.argtypes = [P, I32, P, P, P, P, P, ctypes.POINTER(ctypes.c_void_p)]

@@ -1,0 +1,361 @@
+// MI355X kernels for the read-clustering half of the localGraph hot path:
+//   * pairwise read similarity   (ReadsCluster.pariwiseDistance, ReadsCluster.py:44-59)
+//   * the categorical mixture EM over K = 1..Kmax-1 with BIC model selection
+//     (ReadsCluster.EMCluster :221-277 -> EM :190-209, gamma_updating :132-155,
+//      pitheta_updating :162-188, loglik :104-122, BIC :211-219)
+// One 256-thread workgroup per window; windows are independent, K values are
+// sequential inside a window because numpy's global RNG state (dirichlet
+// re-initialisation, :185-187) carries from one K to the next.  The RNG is a
+// precomputed legacy-MT19937 exponential table (host side, bitwise numpy);
+// each window consumes it from offset 0 (per-window reseed contract).
+//
+// fp64 throughout.  Reduction orders follow numpy where the reference uses
+// plain reductions (gamma.sum(axis=0) row by row, the K-wide exp-sum pairwise,
+// Rlik.sum() pairwise); the BLAS dot products are summed in feature order.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "svs_em_device.hpp"
+
+namespace svs {
+
+__device__ __forceinline__ double clip_eps(double x, double eps) {
+  return fmin(fmax(x, eps), 1.0 - eps);
+}
+
+// numpy pairwise_sum_DOUBLE for n <= 128 (8 accumulators) with the n < 8 path.
+__device__ double np_pairwise_small(const double* a, int n, int stride) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += a[i * stride];
+    return r;
+  }
+  double r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j * stride];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[(i + j) * stride];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i * stride];
+  return res;
+}
+
+// numpy pairwise sum for n > 128 (iterative form of the recursive split).
+__device__ __noinline__ double np_pairwise_large(const double* a, int n) {
+  // explicit stack of (offset, length, stage)
+  int off[32], len[32];
+  double part[32];
+  int st[32];
+  int sp = 0;
+  off[0] = 0; len[0] = n; st[0] = 0;
+  double ret = 0.0;
+  while (sp >= 0) {
+    const int o = off[sp], l = len[sp];
+    if (l <= 128) {
+      ret = np_pairwise_small(a + o, l, 1);
+      --sp;
+      // deliver ret to parent
+      while (sp >= 0) {
+        if (st[sp] == 1) { part[sp] = ret; st[sp] = 2; break; }
+        ret = part[sp] + ret;  // st == 2: left + right
+        --sp;
+      }
+      if (sp < 0) break;
+      // parent now needs its right half
+      int n2 = len[sp] / 2; n2 -= n2 % 8;
+      ++sp; off[sp] = off[sp - 1] + n2; len[sp] = len[sp - 1] - n2; st[sp] = 0;
+      continue;
+    }
+    int n2 = l / 2; n2 -= n2 % 8;
+    st[sp] = 1;
+    ++sp; off[sp] = o; len[sp] = n2; st[sp] = 0;
+  }
+  return ret;
+}
+
+__global__ __launch_bounds__(256) void similarity_kernel(const EmWindow* __restrict__ wins,
+                                                         const uint8_t* __restrict__ X,
+                                                         const int64_t* __restrict__ s_off,
+                                                         double* __restrict__ S) {
+  const EmWindow W = wins[blockIdx.x];
+  const int N = W.n_reads, nf = W.n_feat;
+  const uint8_t* x = X + W.x_off;
+  double* s = S + s_off[blockIdx.x];
+  const double total = nf == 0 ? 1.0 : static_cast<double>(nf);
+  for (int p = threadIdx.x; p < N * N; p += blockDim.x) {
+    const int i = p / N, j = p % N;
+    if (i == j) { s[p] = 1.0; continue; }
+    if (j < i) continue;
+    int cnt = 0;
+    const uint8_t* a = x + static_cast<int64_t>(i) * nf;
+    const uint8_t* b = x + static_cast<int64_t>(j) * nf;
+    for (int f = 0; f < nf; ++f) cnt += a[f] == b[f];
+    const double v = cnt / total;
+    s[p] = v;
+    s[j * N + i] = v;
+  }
+}
+
+__device__ __forceinline__ double np_pairwise(const double* a, int n) {
+  return n <= 128 ? np_pairwise_small(a, n, 1) : np_pairwise_large(a, n);
+}
+
+// Five named accumulators selected by symbol (avoids a runtime-indexed array).
+struct Acc5 {
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0, v4 = 0.0;
+  __device__ __forceinline__ void add(uint8_t a, double x) {
+    v0 += a == 0 ? x : 0.0;
+    v1 += a == 1 ? x : 0.0;
+    v2 += a == 2 ? x : 0.0;
+    v3 += a == 3 ? x : 0.0;
+    v4 += a == 4 ? x : 0.0;
+  }
+};
+
+// numpy's pairwise sum over the K (<= 16) terms exp(clip(M[j] - mi, +-700)).
+__device__ __forceinline__ double exp_row_sum(const double* Mi, int K, double mi) {
+  auto t = [&](int j) { return exp(fmin(fmax(Mi[j] - mi, -700.0), 700.0)); };
+  if (K < 8) {
+    double r = 0.0;
+    for (int j = 0; j < K; ++j) r += t(j);
+    return r;
+  }
+  double r0 = t(0), r1 = t(1), r2 = t(2), r3 = t(3), r4 = t(4), r5 = t(5), r6 = t(6), r7 = t(7);
+  int j = 8;
+  if (K == 16) {
+    r0 += t(8); r1 += t(9); r2 += t(10); r3 += t(11); r4 += t(12); r5 += t(13); r6 += t(14); r7 += t(15);
+    j = 16;
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; j < K; ++j) res += t(j);
+  return res;
+}
+
+struct EmShared {
+  int reinit;
+  int error;
+  uint64_t rng_off;
+};
+
+// M-step (pitheta_updating). Returns via shared flag whether a re-init happened.
+__device__ void m_step(const EmWindow& W, int K, const uint8_t* __restrict__ x, const double* __restrict__ g,
+                       double* __restrict__ pi, double* __restrict__ gsum, double* __restrict__ th,
+                       double* __restrict__ lt, const double* __restrict__ rng, uint64_t rng_len, double eps,
+                       EmShared* sh) {
+  const int N = W.n_reads, nf = W.n_feat, tid = threadIdx.x;
+  if (tid < K) {
+    double s = 0.0;
+    for (int i = 0; i < N; ++i) s += g[i * K + tid];  // numpy axis-0 reduction: row by row
+    gsum[tid] = s;
+    pi[tid] = s / N;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int bad = 0;
+    for (int k = 0; k < K; ++k) bad |= (pi[k] * N < 1.0) || isnan(pi[k]);
+    sh->reinit = bad;
+    if (bad) {
+      const uint64_t need = static_cast<uint64_t>(K) * nf * 5;
+      if (sh->rng_off + need > rng_len) sh->error = 1;
+    }
+  }
+  __syncthreads();
+  if (sh->reinit) {
+    if (tid < K) pi[tid] = 1.0 / K;
+    if (!sh->error) {
+      const double* e = rng + sh->rng_off;
+      for (int r = tid; r < K * nf; r += blockDim.x) {
+        const double e0 = e[5 * r], e1 = e[5 * r + 1], e2 = e[5 * r + 2], e3 = e[5 * r + 3], e4 = e[5 * r + 4];
+        const double inv = 1.0 / ((((e0 + e1) + e2) + e3) + e4);
+        double* t = th + 5 * static_cast<int64_t>(r);
+        t[0] = e0 * inv; t[1] = e1 * inv; t[2] = e2 * inv; t[3] = e3 * inv; t[4] = e4 * inv;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) sh->rng_off += static_cast<uint64_t>(K) * nf * 5;
+  } else {
+    for (int r = tid; r < K * nf; r += blockDim.x) {
+      const int k = r / nf, f = r % nf;
+      Acc5 acc;
+      for (int i = 0; i < N; ++i) acc.add(x[static_cast<int64_t>(i) * nf + f], g[i * K + k]);
+      double* t = th + 5 * static_cast<int64_t>(r);
+      const double d = gsum[k];
+      t[0] = acc.v0 / d; t[1] = acc.v1 / d; t[2] = acc.v2 / d; t[3] = acc.v3 / d; t[4] = acc.v4 / d;
+    }
+  }
+  __syncthreads();
+  for (int r = tid; r < K * nf * 5; r += blockDim.x) lt[r] = log(clip_eps(th[r], eps));
+  __syncthreads();
+}
+
+// E-step (gamma_updating) + the feature part of loglik, A[i,k] = sum_f log theta'[k,f,x_if].
+__device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ x, const double* __restrict__ pi,
+                       const double* __restrict__ lt, double* __restrict__ A, double* __restrict__ M,
+                       double* __restrict__ g) {
+  const int N = W.n_reads, nf = W.n_feat, tid = threadIdx.x;
+  for (int r = tid; r < N * K; r += blockDim.x) {
+    const int i = r / K, k = r % K;
+    Acc5 d;
+    const uint8_t* xi = x + static_cast<int64_t>(i) * nf;
+    const double* lk = lt + static_cast<int64_t>(k) * nf * 5;
+    for (int f = 0; f < nf; ++f) {
+      const uint8_t a = xi[f];
+      d.add(a, lk[5 * f + a]);
+    }
+    const double a_ik = (((d.v0 + d.v1) + d.v2) + d.v3) + d.v4;
+    A[r] = a_ik;
+    M[r] = a_ik + log(pi[k]);
+  }
+  __syncthreads();
+  for (int r = tid; r < N * K; r += blockDim.x) {
+    const int i = r / K, I = r % K;
+    g[r] = 1.0 / exp_row_sum(M + i * K, K, M[i * K + I]);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restrict__ wins,
+                                                         const uint8_t* __restrict__ X,
+                                                         const int32_t* __restrict__ labels,
+                                                         const double* __restrict__ rng, uint64_t rng_len,
+                                                         EmConfig cfg, double* __restrict__ ws,
+                                                         double* __restrict__ outd, int32_t* __restrict__ outi) {
+  __shared__ EmShared sh;
+  const EmWindow W = wins[blockIdx.x];
+  const int N = W.n_reads, nf = W.n_feat, kmax = W.kmax, tid = threadIdx.x;
+  const uint8_t* x = X + W.x_off;
+  const int32_t* lab = labels + W.lab_off;
+  // workspace layout (doubles): per-K theta | lt | gamma per K | pi per K | gsum | A | M | lik per K
+  double* theta_all = ws + W.ws_off;
+  const int nk = kmax - 1;
+  const int64_t th_total = static_cast<int64_t>(nk) * (nk + 1) / 2 * nf * 5;
+  double* lt = theta_all + th_total;
+  double* gamma_all = lt + static_cast<int64_t>(nk) * nf * 5;
+  const int64_t g_total = static_cast<int64_t>(nk) * (nk + 1) / 2 * N;
+  double* pi_all = gamma_all + g_total;
+  double* gsum = pi_all + nk * (nk + 1) / 2;
+  double* A = gsum + 16;
+  double* M = A + static_cast<int64_t>(N) * 16;
+  double* lik_all = M + static_cast<int64_t>(N) * 16;
+  double* bic = outd + W.outd_off;  // nk BICs, then N lik of the chosen K
+  if (tid == 0) { sh.rng_off = 0; sh.error = 0; sh.reinit = 0; }
+  __syncthreads();
+  const double logN = log(static_cast<double>(N));
+  for (int K = 1; K <= nk; ++K) {
+    const int64_t kk = static_cast<int64_t>(K) * (K - 1) / 2;  // sum_{k<K} k
+    double* th = theta_all + kk * nf * 5;
+    double* g = gamma_all + kk * N;
+    double* pi = pi_all + kk;
+    double* lik = lik_all + static_cast<int64_t>(K - 1) * N;
+    const int32_t* lk = lab + static_cast<int64_t>(K - 1) * N;
+    double b0 = NAN;
+    for (int tries = 5; isnan(b0) && tries != 0; --tries) {
+      for (int r = tid; r < N * K; r += blockDim.x) g[r] = (lk[r / K] - 1 == r % K) ? 1.0 : 0.0;
+      __syncthreads();
+      m_step(W, K, x, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh);
+      e_step(W, K, x, pi, lt, A, M, g);
+      for (int it = 0; it < cfg.n_step; ++it) {
+        m_step(W, K, x, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh);
+        e_step(W, K, x, pi, lt, A, M, g);
+        for (int i = tid; i < N; i += blockDim.x) {
+          double s = 0.0;
+          for (int k = 0; k < K; ++k) s += (A[i * K + k] + log(clip_eps(pi[k], cfg.eps))) * g[i * K + k];
+          lik[i] = s;
+        }
+        __syncthreads();
+      }
+      // BIC with ZeroParamNum = 0 decides the NaN retry (EMCluster :249-252)
+      const double tot = np_pairwise(lik, N);
+      b0 = 2.0 * tot - static_cast<double>(K - 1 + static_cast<int64_t>(K) * nf * 4) * logN;
+      __syncthreads();
+    }
+    if (tid == 0) {
+      const double tot = np_pairwise(lik, N);
+      bic[K - 1] = 2.0 * tot - static_cast<double>(K - 1 + static_cast<int64_t>(K) * nf * 4 - W.zero_params) * logN;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int32_t* oi = outi + W.outi_off;  // [K, best, status, pad, rng_used(lo), rng_used(hi), Rclust[N]]
+    int best = -1;
+    for (int k = 0; k < nk; ++k)
+      if (!isnan(bic[k]) && (best < 0 || bic[k] > bic[best])) best = k;
+    int status = sh.error ? 2 : 0;
+    if (best < 0) status = 3;  // nanargmax of an all-NaN list (numpy raises)
+    int K = best + 1;
+    if (status == 0 && K == 1) {
+      if (nk < 2) status = 4;  // reference indexes BICList[1] (IndexError)
+      else if (bic[0] - bic[1] <= nf * logN) { K = 2; best = 1; }
+    }
+    oi[0] = K;
+    oi[1] = best;
+    oi[2] = status;
+    oi[3] = 0;
+    oi[4] = static_cast<int32_t>(sh.rng_off & 0xFFFFFFFFu);
+    oi[5] = static_cast<int32_t>(sh.rng_off >> 32);
+    if (status == 0) {
+      const int64_t kk = static_cast<int64_t>(K) * (K - 1) / 2;
+      const double* g = gamma_all + kk * N;
+      const double* lik = lik_all + static_cast<int64_t>(K - 1) * N;
+      for (int i = 0; i < N; ++i) {
+        int am = 0;
+        for (int k = 1; k < K; ++k)
+          if (g[i * K + k] > g[i * K + am]) am = k;
+        oi[6 + i] = am;
+        bic[nk + i] = lik[i];
+      }
+    }
+  }
+}
+
+hipError_t launch_similarity(const EmWindow* wins, int n, const uint8_t* X, const int64_t* s_off, double* S,
+                             hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(similarity_kernel, dim3(n), dim3(256), 0, stream, wins, X, s_off, S);
+  return hipGetLastError();
+}
+
+hipError_t launch_em_cluster(const EmWindow* wins, int n, const uint8_t* X, const int32_t* labels,
+                             const double* rng, uint64_t rng_len, const EmConfig& cfg, double* ws, double* outd,
+                             int32_t* outi, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(em_cluster_kernel, dim3(n), dim3(256), 0, stream, wins, X, labels, rng, rng_len, cfg, ws,
+                     outd, outi);
+  return hipGetLastError();
+}
+
+}  // namespace svs
+
+namespace svs {
+
+// Copies gamma | pi | theta of each window's selected K into the parameter dump
+// (only when the caller asks for parameters, e.g. parity tests).
+__global__ __launch_bounds__(256) void em_gather_kernel(const EmWindow* __restrict__ wins,
+                                                        const double* __restrict__ ws,
+                                                        const int32_t* __restrict__ outi,
+                                                        double* __restrict__ par) {
+  const EmWindow W = wins[blockIdx.x];
+  const int32_t* oi = outi + W.outi_off;
+  if (oi[2] != 0) return;
+  const int K = oi[0], N = W.n_reads, nf = W.n_feat, nk = W.kmax - 1;
+  const double* theta_all = ws + W.ws_off;
+  const int64_t th_total = static_cast<int64_t>(nk) * (nk + 1) / 2 * nf * 5;
+  const double* gamma_all = theta_all + th_total + static_cast<int64_t>(nk) * nf * 5;
+  const double* pi_all = gamma_all + static_cast<int64_t>(nk) * (nk + 1) / 2 * N;
+  const int64_t kk = static_cast<int64_t>(K) * (K - 1) / 2;
+  double* p = par + W.par_off;
+  for (int64_t r = threadIdx.x; r < static_cast<int64_t>(N) * K; r += blockDim.x) p[r] = gamma_all[kk * N + r];
+  for (int r = threadIdx.x; r < K; r += blockDim.x) p[static_cast<int64_t>(N) * K + r] = pi_all[kk + r];
+  double* t = p + static_cast<int64_t>(N) * K + K;
+  for (int64_t r = threadIdx.x; r < static_cast<int64_t>(K) * nf * 5; r += blockDim.x)
+    t[r] = theta_all[kk * nf * 5 + r];
+}
+
+hipError_t launch_em_gather(const EmWindow* wins, int n, const double* ws, const int32_t* outi, double* par,
+                            hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(em_gather_kernel, dim3(n), dim3(256), 0, stream, wins, ws, outi, par);
+  return hipGetLastError();
+}
+
+}  // namespace svs

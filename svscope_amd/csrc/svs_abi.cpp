@@ -189,6 +189,35 @@ int svs_poa_result_stats(const svs_poa_result* r, svs_poa_stats* out) {
 
 void svs_poa_result_free(svs_poa_result* r) { delete r; }
 
+int svs_similarity_batch(svs_context* ctx, int32_t n_windows, const svs_em_window* wins, const uint8_t* X,
+                         const int64_t* s_off, double* S) {
+  if (!ctx || (n_windows > 0 && (!s_off || !S))) return fail(SVS_E_INVALID, "svs_similarity_batch: invalid argument");
+  std::string err;
+  const int v = svs::em_validate(n_windows, wins, X, &err);
+  if (v != SVS_OK) return fail(v, "svs_similarity_batch: " + err);
+  if (n_windows == 0) return SVS_OK;
+  return guarded([&] {
+    SVS_HIP(hipSetDevice(ctx->device));
+    svs::run_similarity(ctx, n_windows, wins, X, S, s_off);
+  });
+}
+
+int svs_em_batch(svs_context* ctx, int32_t n_windows, const svs_em_window* wins, const uint8_t* X,
+                 const int32_t* labels, const svs_em_config* cfg, svs_em_result** out) {
+  if (!ctx || !cfg || !out || (n_windows > 0 && !labels)) return fail(SVS_E_INVALID, "svs_em_batch: invalid argument");
+  *out = nullptr;
+  std::string err;
+  const int v = svs::em_validate(n_windows, wins, X, &err);
+  if (v != SVS_OK) return fail(v, "svs_em_batch: " + err);
+  svs_em_result* res = nullptr;
+  const int rc = guarded([&] {
+    SVS_HIP(hipSetDevice(ctx->device));
+    res = svs::run_em(ctx, n_windows, wins, X, labels, *cfg);
+  });
+  if (rc == SVS_OK) *out = res;
+  return rc;
+}
+
 int svs_wave_selftest(svs_context* ctx, const int32_t* in, int32_t* scan, int32_t* shift, int32_t n_waves) {
   if (!ctx || !in || !scan || !shift || n_waves <= 0) return fail(SVS_E_INVALID, "svs_wave_selftest: invalid argument");
   return guarded([&] {

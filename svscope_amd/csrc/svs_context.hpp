@@ -90,4 +90,5 @@ struct svs_context {
   svs::DeviceBuf d_em_in, d_em_ws, d_em_out, d_rng;
   svs::PinnedBuf h_em_in, h_em_out;
   size_t rng_len = 0;
+  uint32_t rng_seed = 0;
 };

@@ -1,0 +1,64 @@
+"""GPU parity of the whole per-window path (Decision / TDscope_npz): records
+identical to the reference's own records (goldens) and to the CPU oracle."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import decision_oracle
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "decision_goldens.json")
+
+
+def test_decision_batch_matches_reference_goldens():
+    from svscope_amd.decision_maker import DecisionBatch
+    cases = json.load(open(GOLD))
+    wins = [(c["TDRecord"], c["sequenceList"], np.array(c["ReadIDs"]), c["flank_5"], c["flank_3"]) for c in cases]
+    for c, rec in zip(cases, DecisionBatch(wins)):
+        assert "\t".join(str(x) for x in rec) == c["line"], c["kind"]
+
+
+def test_single_window_decision_signature():
+    from svscope_amd.decision_maker import Decision
+    c = json.load(open(GOLD))[0]
+    rec = Decision(c["TDRecord"], c["sequenceList"], np.array(c["ReadIDs"]), c["flank_5"], c["flank_3"])
+    assert "\t".join(str(x) for x in rec) == c["line"]
+
+
+def test_feature_selection_on_gpu_matches_reference():
+    from svscope_amd.data_scanner import MSAFeatureSelection
+    for c in json.load(open(GOLD)):
+        if not c["features"]:
+            continue
+        enc, feat, rid = MSAFeatureSelection(c["sequenceList"], c["flank_5"], c["flank_3"], np.array(c["ReadIDs"]))
+        assert list(enc.shape) == c["features"]["encoded_shape"]
+        assert feat.tolist() == c["features"]["seqdatamx"]
+        assert list(map(str, rid)) == c["features"]["read_ids"]
+
+
+def test_config1_and_config2_windows_match_oracle():
+    """configs[0]: one 16-read x 2 kb window; configs[1]-shaped: 32 reads x 2 kb."""
+    from svscope_amd import synth
+    from svscope_amd.som_td_detector import TDscope_npz_batch
+    rows = synth.make_windows(config=1) + [synth.make_window(3, 32, 2000)]
+    for r, g in zip(rows, TDscope_npz_batch(rows)):
+        exp = decision_oracle.tdscope_npz(r[4], r[0], np.asarray(r[1]), r[2], r[3])
+        assert decision_oracle.record_line(g) == decision_oracle.record_line(exp)
+
+
+def test_local_graph_npz_end_to_end(tmp_path):
+    from svscope_amd import synth
+    from svscope_amd.local_graph import main
+    rows = [synth.make_window(w, 10, 400) for w in range(6)]
+    synth.save_npz(str(tmp_path / "T1.vs.N1.TandemRepeat.batch0.npz"), rows[:4])
+    synth.save_npz(str(tmp_path / "T1.vs.N1.TandemRepeat.batch1.npz"), rows[4:])
+    main(["-t", "T1", "-n", "N1", "-s", str(tmp_path), "--batch", "4"])
+    lines = open(tmp_path / "T1.vs.N1.TandemRepeat.Raw.bed").read().splitlines()
+    exp = sorted((decision_oracle.record_line(decision_oracle.tdscope_npz(r[4], r[0], np.asarray(r[1]), r[2], r[3]))
+                  for r in rows), key=lambda l: (l.split("\t")[0], int(l.split("\t")[1]), l))
+    assert lines == exp
+    # --Continue skips everything already written
+    main(["-t", "T1", "-n", "N1", "-s", str(tmp_path), "-C"])
+    assert open(tmp_path / "T1.vs.N1.TandemRepeat.Raw.bed").read().splitlines() == exp

@@ -1,0 +1,69 @@
+"""GPU parity of the EM seam against the reference-generated goldens and the
+numpy oracle: identical K and read->component labels, BIC and per-read
+log-likelihoods within 1e-5 (north_star tolerance)."""
+import numpy as np
+import pytest
+
+from oracle import em_oracle
+
+pytestmark = pytest.mark.gpu
+
+import os
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "em_goldens.npz")
+
+
+def test_similarity_matches_oracle():
+    from svscope_amd.reads_cluster import similarity_batch
+    rs = np.random.RandomState(1)
+    mats = [rs.randint(0, 5, size=(n, nf)) for n, nf in [(6, 10), (16, 200), (64, 1000), (5, 0)]]
+    for X, S in zip(mats, similarity_batch(mats)):
+        np.testing.assert_array_equal(S, em_oracle.similarity(X))
+
+
+def test_em_matches_reference_goldens():
+    from svscope_amd.reads_cluster import em_cluster_batch
+    gold = np.load(GOLD)
+    n = int(gold["n_cases"])
+    mats = [gold[f"c{c:02d}_X"].astype(np.int64) for c in range(n)]
+    got = em_cluster_batch(mats, want_params=True)
+    for c, r in enumerate(got):
+        p = f"c{c:02d}_"
+        assert r["K"] == int(gold[p + "K"]), c
+        np.testing.assert_array_equal(r["Rclust"], gold[p + "Rclust"])
+        np.testing.assert_allclose(r["BICList"], gold[p + "BICList"], rtol=1e-9, atol=1e-5)
+        np.testing.assert_allclose(r["lik"], gold[p + "lik"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(r["gamma"], gold[p + "gamma"], rtol=0, atol=1e-7)
+        np.testing.assert_allclose(r["pi"], gold[p + "pi"], rtol=0, atol=1e-9)
+        np.testing.assert_allclose(r["theta"].sum(axis=(1, 2)), gold[p + "theta_sum"], rtol=1e-9)
+
+
+def test_em_matches_oracle_random_and_reinit_heavy():
+    from svscope_amd.reads_cluster import em_cluster_batch
+    rs = np.random.RandomState(42)
+    mats = []
+    for k in range(24):
+        n = int(rs.choice([6, 9, 16, 33, 64]))
+        nf = int(rs.choice([10, 37, 150, 600]))
+        protos = rs.randint(0, 5, size=(3, nf))
+        X = protos[rs.randint(0, 3, size=n)]
+        flip = rs.random_sample(X.shape) < 0.1
+        X[flip] = rs.randint(0, 5, size=int(flip.sum()))
+        if k % 3 == 0:
+            X[n // 2:] = X[0]  # duplicates force dirichlet re-initialisation
+        mats.append(X)
+    got = em_cluster_batch(mats, want_params=True)
+    for X, r in zip(mats, got):
+        o = em_oracle.em_cluster(X)
+        assert r["K"] == o["K"]
+        np.testing.assert_array_equal(r["Rclust"], o["Rclust"])
+        np.testing.assert_allclose(r["BICList"], o["BICList"], rtol=1e-9, atol=1e-5)
+        np.testing.assert_allclose(r["lik"], o["lik"], rtol=0, atol=1e-5)
+
+
+def test_emcluster_signature():
+    from svscope_amd.reads_cluster import EMCluster
+    gold = np.load(GOLD)
+    X = gold["c05_X"].astype(np.int64)
+    K, Xo, R, theta, gamma, pie, bics = EMCluster(X, initselection=1)
+    assert K == int(gold["c05_K"]) and Xo is X
+    assert theta.shape == (K, X.shape[1], 5) and gamma.shape == (X.shape[0], K) and pie.shape == (K,)
