@@ -25,6 +25,16 @@ class PoaConfig(ctypes.Structure):
                 ("min_coverage", ctypes.c_int32), ("genmsa", ctypes.c_int32)]
 
 
+class EmWindow(ctypes.Structure):
+    _fields_ = [("n_reads", ctypes.c_int32), ("n_feat", ctypes.c_int32), ("x_off", ctypes.c_int64),
+                ("label_off", ctypes.c_int64)]
+
+
+class EmConfig(ctypes.Structure):
+    _fields_ = [("max_c", ctypes.c_int32), ("n_step", ctypes.c_int32), ("seed", ctypes.c_int32),
+                ("want_params", ctypes.c_int32), ("eps", ctypes.c_double)]
+
+
 class PoaStats(ctypes.Structure):
     _fields_ = [("dp_cells", ctypes.c_uint64), ("alignments", ctypes.c_uint64), ("launches", ctypes.c_uint64),
                 ("tb_bytes", ctypes.c_uint64), ("pool_bytes", ctypes.c_uint64), ("h2d_bytes", ctypes.c_uint64),
@@ -83,9 +93,10 @@ def _declare_em(lib):
     P, I32 = ctypes.c_void_p, ctypes.c_int32
     lib.svs_rng_exponential_table.argtypes = [ctypes.c_uint32, ctypes.c_int64, P]
     lib.svs_rng_exponential_table.restype = ctypes.c_int
-    lib.svs_similarity_batch.argtypes = [P, I32, P, P, P, P]
+    lib.svs_similarity_batch.argtypes = [P, I32, ctypes.POINTER(EmWindow), P, P, P]
     lib.svs_similarity_batch.restype = ctypes.c_int
-    lib.svs_em_batch.argtypes = [P, I32, P, P, P, P, P, ctypes.POINTER(ctypes.c_void_p)]
+    lib.svs_em_batch.argtypes = [P, I32, ctypes.POINTER(EmWindow), P, P, ctypes.POINTER(EmConfig),
+                                 ctypes.POINTER(ctypes.c_void_p)]
     lib.svs_em_batch.restype = ctypes.c_int
     lib.svs_em_result_get.argtypes = [P, I32, I32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64)]
     lib.svs_em_result_get.restype = ctypes.c_int

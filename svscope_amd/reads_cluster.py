@@ -21,14 +21,8 @@ from scipy.cluster.hierarchy import fcluster, linkage
 from . import _abi
 
 
-class EmWindowStruct(ctypes.Structure):
-    _fields_ = [("n_reads", ctypes.c_int32), ("n_feat", ctypes.c_int32), ("x_off", ctypes.c_int64),
-                ("label_off", ctypes.c_int64)]
-
-
-class EmConfigStruct(ctypes.Structure):
-    _fields_ = [("max_c", ctypes.c_int32), ("n_step", ctypes.c_int32), ("seed", ctypes.c_int32),
-                ("want_params", ctypes.c_int32), ("eps", ctypes.c_double)]
+EmWindowStruct = _abi.EmWindow
+EmConfigStruct = _abi.EmConfig
 
 
 _F_K, _F_RCLUST, _F_BIC, _F_LIK, _F_GAMMA, _F_PI, _F_THETA, _F_RNG = range(8)
@@ -63,7 +57,7 @@ def similarity_batch(mats, context=None):
         s_off[w] = tot
         tot += X.shape[0] ** 2
     S = np.zeros(max(1, tot), np.float64)
-    _abi.check(ctx.lib.svs_similarity_batch(ctx.handle, len(mats), ctypes.cast(wins, ctypes.c_void_p),
+    _abi.check(ctx.lib.svs_similarity_batch(ctx.handle, len(mats), wins,
                                             blob.ctypes.data_as(ctypes.c_void_p),
                                             s_off.ctypes.data_as(ctypes.c_void_p),
                                             S.ctypes.data_as(ctypes.c_void_p)), "svs_similarity_batch")
@@ -104,7 +98,7 @@ def em_cluster_batch(mats, max_C=9, n_step=20, seed=2023, want_params=False, con
         wins[w].label_off = label_off[w]
     cfg = EmConfigStruct(int(max_C), int(n_step), int(seed), 1 if want_params else 0, 1e-10)
     res = ctypes.c_void_p()
-    _abi.check(ctx.lib.svs_em_batch(ctx.handle, len(mats), ctypes.cast(wins, ctypes.c_void_p),
+    _abi.check(ctx.lib.svs_em_batch(ctx.handle, len(mats), wins,
                                     blob.ctypes.data_as(ctypes.c_void_p), lab_blob.ctypes.data_as(ctypes.c_void_p),
                                     ctypes.byref(cfg), ctypes.byref(res)), "svs_em_batch")
     out = []
