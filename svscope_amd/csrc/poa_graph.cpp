@@ -3,6 +3,7 @@
 #include "poa_graph.hpp"
 
 #include <algorithm>
+#include <climits>
 #include <stdexcept>
 
 namespace svs {
@@ -212,6 +213,31 @@ void PoaGraph::export_rows(RowTables* t) const {
     if (last_use[r] == r) free_slots.push_back(s);
   }
   t->n_slots = next;
+}
+
+void fill_col0(RowTables* t, int32_t g, int32_t e, int32_t q, int32_t c) {
+  const size_t V = t->info.size();
+  t->col0.resize(3 * V);
+  for (size_t r = 0; r < V; ++r) {
+    int32_t F0, O0;
+    if (t->pstart[r] == t->pstart[r + 1]) {
+      F0 = g;
+      O0 = q;
+    } else {
+      F0 = INT32_MIN + 1024;
+      O0 = INT32_MIN + 1024;
+      for (uint32_t k = t->pstart[r]; k < t->pstart[r + 1]; ++k) {
+        const size_t p = t->pred_row[k] - 1;
+        F0 = std::max(F0, t->col0[3 * p + 1]);
+        O0 = std::max(O0, t->col0[3 * p + 2]);
+      }
+      F0 += e;
+      O0 += c;
+    }
+    t->col0[3 * r] = std::max(F0, O0);
+    t->col0[3 * r + 1] = F0;
+    t->col0[3 * r + 2] = O0;
+  }
 }
 
 std::vector<std::string> PoaGraph::msa() const {

@@ -22,9 +22,15 @@ struct RowTables {
   std::vector<uint32_t> pstart;  // n_rows + 1 CSR offsets into pred_row/pred_slot
   std::vector<uint32_t> pred_row;   // 1-based DP row of each in-edge tail (insertion order)
   std::vector<uint32_t> pred_slot;  // pool slot of that row
+  std::vector<int32_t> col0;        // per rank row: H, F, O of DP column 0 (fill_col0)
   uint32_t n_slots = 1;
   uint32_t max_preds = 0;
 };
+
+// Column 0 of the NW matrix depends only on the graph (gap runs down the
+// in-edges, spoa Initialize): F0 = max_p F0[p] + e (g for sources), O0 likewise
+// with q/c, H0 = max(F0, O0).  Computed once per job on the host.
+void fill_col0(RowTables* t, int32_t g, int32_t e, int32_t q, int32_t c);
 
 class PoaGraph {
  public:

@@ -71,13 +71,23 @@ __device__ __forceinline__ int32_t row0_h(const PoaScore& P, int32_t j) {
   return j == 0 ? 0 : imax(row0_q(P, j), row0_e(P, j));
 }
 
+// Traceback-code assembly shared by both row paths.
+__device__ __forceinline__ uint32_t assemble_code(uint32_t diag_k, uint32_t up_k, uint32_t up_ext, bool left_ok,
+                                                  bool left_ext, bool lbit, uint32_t uc_k, uint32_t uc_stop) {
+  uint32_t code;
+  if (diag_k != 31) code = diag_k << 3;
+  else if (up_k != 31) code = 1u | (up_ext << 2) | (up_k << 3);
+  else code = left_ok ? (2u | (left_ext ? 4u : 0u)) : 3u;
+  return code | ((lbit ? 1u : 0u) << 8) | (uc_stop << 9) | (uc_k << 10);
+}
+
 __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore P,
     const uint32_t* __restrict__ row_info, const uint32_t* __restrict__ row_slot,
     const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
-    const uint32_t* __restrict__ pred_slot, const uint8_t* __restrict__ seqs,
-    uint16_t* __restrict__ tb, int32_t* __restrict__ pool, int32_t* __restrict__ aln,
-    int32_t* __restrict__ aln_len) {
+    const uint32_t* __restrict__ pred_slot, const int32_t* __restrict__ col0,
+    const uint8_t* __restrict__ seqs, uint16_t* __restrict__ tb, int32_t* __restrict__ pool,
+    int32_t* __restrict__ aln, int32_t* __restrict__ aln_len) {
   const int lane = threadIdx.x & 63;
   const int job_id = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (job_id >= n_jobs) return;
@@ -85,18 +95,19 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
   const int32_t L = static_cast<int32_t>(J.len);
   const uint64_t LS = J.ls;
   const uint32_t V = J.n_rows;
-  const uint8_t* __restrict__ seq = seqs + J.seq_off;
+  const uint8_t* __restrict__ seq = seqs + J.seq_off;  // padded to LS bytes
   int32_t* __restrict__ pl = pool + J.pool_off;
   uint16_t* __restrict__ tbj = tb + J.tb_off;
   const uint32_t* __restrict__ rinfo = row_info + J.row_off;
   const uint32_t* __restrict__ rslot = row_slot + J.row_off;
+  const int32_t* __restrict__ rc0 = col0 + 3ull * J.row_off;
   const uint32_t* __restrict__ rps = row_pstart + J.pstart_off;
   const uint32_t* __restrict__ prow = pred_row + J.pred_off;
   const uint32_t* __restrict__ pslot = pred_slot + J.pred_off;
-  const int32_t nstrips = (L + 1 + 63) >> 6;
+  const int32_t nstrips = static_cast<int32_t>(LS >> 6);  // LS = 64 * ceil((L+1)/64)
 
-  // virtual row 0 -> slot 0 (planes H, F, O at offsets 0, LS, 2LS)
-  for (int32_t j = lane; j <= L; j += 64) {
+  // virtual row 0 -> slot 0 (planes H, F, O at offsets 0, LS, 2LS), full row width
+  for (int32_t j = lane; j < static_cast<int32_t>(LS); j += 64) {
     pl[j] = row0_h(P, j);
     pl[LS + j] = j == 0 ? 0 : SVS_NEG_INF;
     pl[2 * LS + j] = j == 0 ? 0 : SVS_NEG_INF;
@@ -112,29 +123,80 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
     const uint64_t so = static_cast<uint64_t>(rslot[r]) * 3 * LS;
     const uint32_t p0 = rps[r];
     const uint32_t np = rps[r + 1] - p0;
-    const uint32_t npass = np == 0 ? 1 : np;  // source nodes read virtual row 0
-
-    // column 0 of this row (spoa Initialize): gap runs down the graph
-    int32_t F0, O0;
-    if (np == 0) {
-      F0 = P.g;
-      O0 = P.q;
-    } else {
-      F0 = SVS_NEG_INF;
-      O0 = SVS_NEG_INF;
-      for (uint32_t k = 0; k < np; ++k) {
-        const uint64_t ps = static_cast<uint64_t>(pslot[p0 + k]) * 3 * LS;
-        F0 = imax(F0, pl[ps + LS]);
-        O0 = imax(O0, pl[ps + 2 * LS]);
-      }
-      F0 += P.e;
-      O0 += P.c;
-    }
-    const int32_t H0 = imax(F0, O0);
+    const int32_t H0 = rc0[3 * r], F0 = rc0[3 * r + 1], O0 = rc0[3 * r + 2];
 
     int32_t run1 = SVS_VNEG, run2 = SVS_VNEG;  // scan carries across strips
     int32_t cHpre = H0, cQ = SVS_NEG_INF, cE = SVS_NEG_INF, cH = H0;
 
+    if (np <= 1) {
+      // ---- fast path: zero or one in-edge (the common POA row) ----
+      // Next strip's predecessor values are loaded before this strip's stores;
+      // H_p[j-1] comes from a wave shift of H_p[j] with a scalar carry.
+      const uint64_t ps = np == 0 ? 0 : static_cast<uint64_t>(pslot[p0]) * 3 * LS;
+      int32_t hp = pl[ps + lane], fp = pl[ps + LS + lane], op = pl[ps + 2 * LS + lane];
+      uint8_t rc = seq[lane == 0 ? 0 : lane - 1];
+      int32_t cHp = 0;
+      for (int32_t s = 0; s < nstrips; ++s) {
+        const int32_t j = (s << 6) + lane;
+        const bool valid = j <= L;
+        const bool c0 = j == 0;
+        const bool inner = valid && !c0;
+        int32_t hpn = 0, fpn = 0, opn = 0;
+        uint8_t rcn = 0;
+        if (s + 1 < nstrips) {
+          const int32_t jn = j + 64;
+          hpn = pl[ps + jn];
+          fpn = pl[ps + LS + jn];
+          opn = pl[ps + 2 * LS + jn];
+          rcn = seq[jn - 1];
+        }
+        const int32_t hpm = wave_shr1(hp, cHp, lane);
+        const int32_t mc = rc == nb ? P.m : P.n;
+        const int32_t F = c0 ? F0 : imax(hp + P.g, fp + P.e);
+        const int32_t O = c0 ? O0 : imax(hp + P.q, op + P.c);
+        const int32_t Hpre = c0 ? H0 : imax(hpm + mc, imax(F, O));
+
+        const int32_t prevHpre = wave_shr1(Hpre, cHpre, lane);
+        int32_t x = inner ? prevHpre + P.q - j * P.c : SVS_VNEG;
+        x = imax(wave_prefix_max(x), run1);
+        run1 = readlane63(x);
+        const int32_t Q = inner ? x + j * P.c : SVS_NEG_INF;
+        const int32_t prevQ = wave_shr1(Q, cQ, lane);
+        int32_t y = inner ? imax(prevHpre, prevQ) + P.g - j * P.e : SVS_VNEG;
+        y = imax(wave_prefix_max(y), run2);
+        run2 = readlane63(y);
+        const int32_t E = inner ? y + j * P.e : SVS_NEG_INF;
+        const int32_t H = inner ? imax(Hpre, imax(E, Q)) : H0;
+        const int32_t prevE = wave_shr1(E, cE, lane);
+        const int32_t prevH = wave_shr1(H, cH, lane);
+
+        const bool dg = inner && H == hpm + mc;
+        const bool ua = H == fp + P.e, ub = H == hp + P.g, uc = H == op + P.c, ud = H == hp + P.q;
+        const bool va = F == hp + P.g, vb = F == fp + P.e, vc = O == hp + P.q, vd = O == op + P.c;
+        const bool vm = np != 0 && (va || vb || vc || vd);
+        const bool la = inner && H == prevE + P.e, lb = inner && H == prevH + P.g;
+        const bool lc = inner && H == prevQ + P.c, ld = inner && H == prevH + P.q;
+        const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
+        const uint32_t code =
+            assemble_code(dg ? 0u : 31u, (ua || ub || uc || ud) ? 0u : 31u, (ua || (!ub && uc)) ? 1u : 0u,
+                          la || lb || lc || ld, la || (!lb && lc), lbit, vm ? 0u : 31u,
+                          (vm && (va || (!vb && vc))) ? 1u : 0u);
+        if (valid) tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+        pl[so + j] = H;
+        pl[so + LS + j] = F;
+        pl[so + 2 * LS + j] = O;
+        if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
+        cHp = readlane63(hp);
+        cHpre = readlane63(Hpre);
+        cQ = readlane63(Q);
+        cE = readlane63(E);
+        cH = readlane63(H);
+        hp = hpn; fp = fpn; op = opn; rc = rcn;
+      }
+      continue;
+    }
+
+    // ---- general path: two or more in-edges ----
     for (int32_t s = 0; s < nstrips; ++s) {
       const int32_t j = (s << 6) + lane;
       const bool valid = j <= L;
@@ -142,32 +204,22 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
       const bool inner = valid && !c0;
       const int32_t mc = (inner && seq[j - 1] == nb) ? P.m : P.n;
 
-      // ---- pass 1: vertical (F, O) and diagonal terms over all in-edges ----
       int32_t F = SVS_VNEG, O = SVS_VNEG, Hd = SVS_VNEG;
       int32_t hpm0 = 0, hp0 = 0, fp0 = 0, op0 = 0;  // first in-edge kept in registers
-      if (inner) {
-        for (uint32_t k = 0; k < npass; ++k) {
-          const uint64_t ps = np == 0 ? 0 : static_cast<uint64_t>(pslot[p0 + k]) * 3 * LS;
-          const int32_t hpm = pl[ps + j - 1];
-          const int32_t hp = pl[ps + j];
-          const int32_t fp = pl[ps + LS + j];
-          const int32_t op = pl[ps + 2 * LS + j];
-          if (k == 0) { hpm0 = hpm; hp0 = hp; fp0 = fp; op0 = op; }
-          F = imax(F, imax(hp + P.g, fp + P.e));
-          O = imax(O, imax(hp + P.q, op + P.c));
-          Hd = imax(Hd, hpm + mc);
-        }
-      } else if (c0) {
-        const uint64_t ps = np == 0 ? 0 : static_cast<uint64_t>(pslot[p0]) * 3 * LS;
-        hp0 = pl[ps];
-        fp0 = pl[ps + LS];
-        op0 = pl[ps + 2 * LS];
-        F = F0;
-        O = O0;
+      for (uint32_t k = 0; k < np; ++k) {
+        const uint64_t ps = static_cast<uint64_t>(pslot[p0 + k]) * 3 * LS;
+        const int32_t hpm = c0 ? 0 : pl[ps + j - 1];
+        const int32_t hp = pl[ps + j];
+        const int32_t fp = pl[ps + LS + j];
+        const int32_t op = pl[ps + 2 * LS + j];
+        if (k == 0) { hpm0 = hpm; hp0 = hp; fp0 = fp; op0 = op; }
+        F = imax(F, imax(hp + P.g, fp + P.e));
+        O = imax(O, imax(hp + P.q, op + P.c));
+        Hd = imax(Hd, hpm + mc);
       }
+      if (c0) { F = F0; O = O0; }
       const int32_t Hpre = c0 ? H0 : imax(Hd, imax(F, O));
 
-      // ---- horizontal gaps as two prefix-max scans ----
       const int32_t prevHpre = wave_shr1(Hpre, cHpre, lane);
       int32_t x = inner ? prevHpre + P.q - j * P.c : SVS_VNEG;
       x = imax(wave_prefix_max(x), run1);
@@ -182,50 +234,38 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
       const int32_t prevE = wave_shr1(E, cE, lane);
       const int32_t prevH = wave_shr1(H, cH, lane);
 
-      // ---- traceback code: replay of spoa's backtrack comparisons ----
-      if (valid) {
-        uint32_t diag_k = 31, up_k = 31, up_ext = 0, uc_k = 31, uc_stop = 0;
-        for (uint32_t k = 0; k < npass; ++k) {
-          int32_t hpm, hp, fp, op;
-          if (k == 0) {
-            hpm = hpm0; hp = hp0; fp = fp0; op = op0;
-          } else {
-            const uint64_t ps = static_cast<uint64_t>(pslot[p0 + k]) * 3 * LS;
-            hpm = inner ? pl[ps + j - 1] : 0;
-            hp = pl[ps + j];
-            fp = pl[ps + LS + j];
-            op = pl[ps + 2 * LS + j];
-          }
-          if (inner && diag_k == 31 && H == hpm + mc) diag_k = k;
-          if (up_k == 31) {
-            const bool a = H == fp + P.e, b = H == hp + P.g, c = H == op + P.c, d = H == hp + P.q;
-            if (a || b || c || d) { up_k = k; up_ext = (a || (!b && c)) ? 1u : 0u; }
-          }
-          if (np != 0 && uc_k == 31) {
-            const bool a = F == hp + P.g, b = F == fp + P.e, c = O == hp + P.q, d = O == op + P.c;
-            if (a || b || c || d) { uc_k = k; uc_stop = (a || (!b && c)) ? 1u : 0u; }
-          }
-        }
-        uint32_t code;
-        if (diag_k != 31) {
-          code = 0u | (diag_k << 3);
-        } else if (up_k != 31) {
-          code = 1u | (up_ext << 2) | (up_k << 3);
+      uint32_t diag_k = 31, up_k = 31, up_ext = 0, uc_k = 31, uc_stop = 0;
+      for (uint32_t k = 0; k < np; ++k) {
+        int32_t hpm, hp, fp, op;
+        if (k == 0) {
+          hpm = hpm0; hp = hp0; fp = fp0; op = op0;
         } else {
-          const bool a = inner && H == prevE + P.e, b = inner && H == prevH + P.g;
-          const bool c = inner && H == prevQ + P.c, d = inner && H == prevH + P.q;
-          code = (a || b || c || d) ? (2u | ((a || (!b && c)) ? 4u : 0u)) : 3u;
+          const uint64_t ps = static_cast<uint64_t>(pslot[p0 + k]) * 3 * LS;
+          hpm = c0 ? 0 : pl[ps + j - 1];
+          hp = pl[ps + j];
+          fp = pl[ps + LS + j];
+          op = pl[ps + 2 * LS + j];
         }
-        const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
-        code |= (lbit ? 1u : 0u) << 8;
-        code |= uc_stop << 9;
-        code |= uc_k << 10;
-        tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
-        pl[so + j] = H;
-        pl[so + LS + j] = c0 ? F0 : F;
-        pl[so + 2 * LS + j] = c0 ? O0 : O;
-        if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
+        if (inner && diag_k == 31 && H == hpm + mc) diag_k = k;
+        if (up_k == 31) {
+          const bool a = H == fp + P.e, b = H == hp + P.g, c = H == op + P.c, d = H == hp + P.q;
+          if (a || b || c || d) { up_k = k; up_ext = (a || (!b && c)) ? 1u : 0u; }
+        }
+        if (uc_k == 31) {
+          const bool a = F == hp + P.g, b = F == fp + P.e, c = O == hp + P.q, d = O == op + P.c;
+          if (a || b || c || d) { uc_k = k; uc_stop = (a || (!b && c)) ? 1u : 0u; }
+        }
       }
+      const bool la = inner && H == prevE + P.e, lb = inner && H == prevH + P.g;
+      const bool lc = inner && H == prevQ + P.c, ld = inner && H == prevH + P.q;
+      const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
+      const uint32_t code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k,
+                                          uc_stop);
+      if (valid) tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+      pl[so + j] = H;
+      pl[so + LS + j] = F;
+      pl[so + 2 * LS + j] = O;
+      if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
       cHpre = readlane63(Hpre);
       cQ = readlane63(Q);
       cE = readlane63(E);
@@ -318,7 +358,7 @@ hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream) {
   const int blocks = (a.n_jobs + waves_per_block - 1) / waves_per_block;
   hipLaunchKernelGGL(poa_nw_convex_kernel, dim3(blocks), dim3(64 * waves_per_block), 0, stream,
                      a.jobs, a.n_jobs, a.score, a.row_info, a.row_slot, a.row_pstart, a.pred_row,
-                     a.pred_slot, a.seqs, a.tb, a.pool, a.aln, a.aln_len);
+                     a.pred_slot, a.col0, a.seqs, a.tb, a.pool, a.aln, a.aln_len);
   return hipGetLastError();
 }
 

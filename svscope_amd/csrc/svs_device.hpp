@@ -18,7 +18,7 @@ struct PoaJob {
   uint32_t row_off;   // into row_info / row_slot
   uint32_t pstart_off;  // into row_pstart (n_rows + 1 entries)
   uint32_t pred_off;  // base of this job's pred_row / pred_slot entries
-  uint32_t seq_off;   // into seqs (bytes)
+  uint32_t seq_off;   // into seqs (bytes, padded to ls per job)
   uint32_t n_rows;    // graph nodes
   uint32_t len;       // read length
   uint32_t ls;        // row stride (>= len + 1, multiple of 64)
@@ -34,6 +34,7 @@ struct PoaLaunch {
   const uint32_t* row_pstart;
   const uint32_t* pred_row;
   const uint32_t* pred_slot;
+  const int32_t* col0;
   const uint8_t* seqs;
   uint16_t* tb;
   int32_t* pool;

@@ -79,7 +79,10 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
       if (needs[i]) need.push_back(static_cast<uint32_t>(i));
     if (need.empty()) continue;
     tables.resize(need.size());
-    ctx->pool->parallel_for(need.size(), [&](size_t k) { tasks[need[k]].graph.export_rows(&tables[k]); });
+    ctx->pool->parallel_for(need.size(), [&](size_t k) {
+      tasks[need[k]].graph.export_rows(&tables[k]);
+      fill_col0(&tables[k], cfg.g, cfg.e, cfg.q, cfg.c);
+    });
     host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
 
     // Split into launches that fit the device budget.
@@ -121,7 +124,7 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
         n_rows += J.n_rows;
         n_pstart += J.n_rows + 1;
         n_pred += tt.pred_row.size();
-        n_seq += round_up(J.len, 4);
+        n_seq += J.ls;  // padded: the kernel prefetches one strip past the read end
         n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
         n_pool += static_cast<uint64_t>(J.n_slots) * 3 * J.ls;
         n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
@@ -140,6 +143,7 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
       };
       const Section s_jobs = sec(nj * sizeof(PoaJob));
       const Section s_info = sec(n_rows * 4), s_slot = sec(n_rows * 4), s_ps = sec(n_pstart * 4);
+      const Section s_col0 = sec(n_rows * 12);
       const Section s_prow = sec(n_pred * 4), s_pslot = sec(n_pred * 4), s_seq = sec(n_seq);
       ctx->h_stage.ensure(off);
       char* hs = ctx->h_stage.as<char>();
@@ -150,12 +154,14 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
         std::memcpy(hs + s_info.off + 4ull * J.row_off, tt.info.data(), 4ull * J.n_rows);
         std::memcpy(hs + s_slot.off + 4ull * J.row_off, tt.slot.data(), 4ull * J.n_rows);
         std::memcpy(hs + s_ps.off + 4ull * J.pstart_off, tt.pstart.data(), 4ull * (J.n_rows + 1));
+        std::memcpy(hs + s_col0.off + 12ull * J.row_off, tt.col0.data(), 12ull * J.n_rows);
         if (!tt.pred_row.empty()) {
           std::memcpy(hs + s_prow.off + 4ull * J.pred_off, tt.pred_row.data(), 4 * tt.pred_row.size());
           std::memcpy(hs + s_pslot.off + 4ull * J.pred_off, tt.pred_slot.data(), 4 * tt.pred_slot.size());
         }
         const std::string& s = tasks[need[first + k]].seqs[step];
         std::memcpy(hs + s_seq.off + J.seq_off, s.data(), s.size());
+        std::memset(hs + s_seq.off + J.seq_off + s.size(), 0, J.ls - s.size());
       });
       host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
 
@@ -178,6 +184,7 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
       la.row_pstart = reinterpret_cast<const uint32_t*>(dg + s_ps.off);
       la.pred_row = reinterpret_cast<const uint32_t*>(dg + s_prow.off);
       la.pred_slot = reinterpret_cast<const uint32_t*>(dg + s_pslot.off);
+      la.col0 = reinterpret_cast<const int32_t*>(dg + s_col0.off);
       la.seqs = reinterpret_cast<const uint8_t*>(dg + s_seq.off);
       la.tb = ctx->d_tb.as<uint16_t>();
       la.pool = ctx->d_pool.as<int32_t>();

@@ -42,17 +42,7 @@ std::vector<int32_t> emu_align(const svs::RowTables& T, const std::string& seq, 
     const bool sink = (T.info[r] >> 8) & 1;
     const uint64_t so = static_cast<uint64_t>(T.slot[r]) * 3 * LS;
     const uint32_t p0 = T.pstart[r], np = T.pstart[r + 1] - p0, npass = np ? np : 1;
-    int32_t F0, O0;
-    if (np == 0) { F0 = P.g; O0 = P.q; }
-    else {
-      F0 = O0 = NEG_INF;
-      for (uint32_t k = 0; k < np; ++k) {
-        const uint64_t ps = static_cast<uint64_t>(T.pred_slot[p0 + k]) * 3 * LS;
-        F0 = std::max(F0, pl[ps + LS]);
-        O0 = std::max(O0, pl[ps + 2 * LS]);
-      }
-      F0 += P.e; O0 += P.c;
-    }
+    const int32_t F0 = T.col0[3 * r + 1], O0 = T.col0[3 * r + 2];
     const int32_t H0 = std::max(F0, O0);
     int32_t run1 = VNEG, run2 = VNEG, cHpre = H0, cQ = NEG_INF, cE = NEG_INF, cH = H0;
     for (int32_t s = 0; s < nstrips; ++s) {
@@ -212,6 +202,7 @@ void* emu_poa(int n, const char* const* seqs, const int* lens, int m, int mis, i
       if (seq.empty()) continue;
       if (graph.empty()) { graph.add_alignment_nodes({}, seq); continue; }
       graph.export_rows(&T);
+      svs::fill_col0(&T, P.g, P.e, P.q, P.c);
       r->max_slots = std::max(r->max_slots, T.n_slots);
       graph.add_alignment_ranks(emu_align(T, seq, P), seq);
     }
