@@ -54,10 +54,9 @@ __device__ __forceinline__ int32_t wave_prefix_max(int32_t x) {
   return x;
 }
 
-// lane l <- x[l-1]; lane 0 <- fill (wave-uniform)
-__device__ __forceinline__ int32_t wave_shr1(int32_t x, int32_t fill, int lane) {
-  const int32_t y = __shfl_up(x, 1, 64);
-  return lane == 0 ? fill : y;
+// lane l <- x[l-1]; lane 0 <- fill (wave-uniform).  DPP wave_shr:1.
+__device__ __forceinline__ int32_t wave_shr1(int32_t x, int32_t fill, int /*lane*/) {
+  return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xF, 0xF, false);
 }
 
 __device__ __forceinline__ int32_t readlane63(int32_t x) {
@@ -69,6 +68,49 @@ __device__ __forceinline__ int32_t row0_e(const PoaScore& P, int32_t j) { return
 __device__ __forceinline__ int32_t row0_q(const PoaScore& P, int32_t j) { return j == 0 ? 0 : P.q + (j - 1) * P.c; }
 __device__ __forceinline__ int32_t row0_h(const PoaScore& P, int32_t j) {
   return j == 0 ? 0 : imax(row0_q(P, j), row0_e(P, j));
+}
+
+// Cross-strip state of one row sweep (all wave-uniform scalars).
+struct StripCarry {
+  int32_t run1, run2;  // running maxima of the Q / E scan terms over earlier columns
+  int32_t cHpre, cQ, cE, cH;  // Hpre, Q, E, H at the previous strip's last column
+};
+
+// Horizontal-gap scans of one 64-column strip.  Both prefix scans depend only
+// on this strip's Hpre (not on earlier strips), so the long DPP chains of
+// strip s+1 can overlap strip s; earlier strips enter through a few scalar
+// maxima (exact for e <= c, checked on host):
+//   P1[j] = max_{j0<=k<=j} (Hpre[k-1] + q - k c)
+//   Q[j]  = j c + max(P1[j], run1)
+//   P2[j] = max_{j0<=k<=j} (max(Hpre[k-1], Qloc[k-1]) + g - k e),  Qloc[k-1] = (k-1) c + P1[k-1]
+//   E[j]  = j e + max(P2[j], run2, cQ + g - j0 e, run1 + (j-1) c + g - j e)
+__device__ __forceinline__ void strip_gaps(const PoaScore& P, int lane, int32_t j, int32_t j0, bool inner,
+                                           int32_t Hpre, int32_t H0, StripCarry& cr, int32_t& Q, int32_t& E,
+                                           int32_t& H, int32_t& prevQ, int32_t& prevE, int32_t& prevH) {
+  const int32_t pH = wave_shr1(Hpre, cr.cHpre, lane);
+  int32_t p1 = inner ? pH + P.q - j * P.c : SVS_VNEG;
+  p1 = wave_prefix_max(p1);
+  const int32_t p1m = wave_shr1(p1, SVS_VNEG, lane);
+  int32_t p2 = inner ? imax(pH, p1m + (j - 1) * P.c) + P.g - j * P.e : SVS_VNEG;
+  p2 = wave_prefix_max(p2);
+  const int32_t T1 = j0 > 0 ? cr.cQ + P.g - j0 * P.e : SVS_VNEG;
+  const int32_t T2 = lane > 0 ? cr.run1 + (j - 1) * P.c + P.g - j * P.e : SVS_VNEG;
+  Q = inner ? j * P.c + imax(p1, cr.run1) : SVS_NEG_INF;
+  E = inner ? j * P.e + imax(imax(p2, cr.run2), imax(T1, T2)) : SVS_NEG_INF;
+  H = inner ? imax(Hpre, imax(E, Q)) : H0;
+  prevQ = wave_shr1(Q, cr.cQ, lane);
+  prevE = wave_shr1(E, cr.cE, lane);
+  prevH = wave_shr1(H, cr.cH, lane);
+  // carries for the next strip, from carry-free lane-63 values
+  const int32_t jl = j0 + 63;
+  const int32_t p1l = readlane63(p1), p2l = readlane63(p2), hl = readlane63(Hpre);
+  const int32_t T2l = cr.run1 + (jl - 1) * P.c + P.g - jl * P.e;
+  cr.run2 = imax(imax(cr.run2, p2l), imax(T1, T2l));
+  cr.run1 = imax(cr.run1, p1l);
+  cr.cQ = jl * P.c + cr.run1;
+  cr.cE = jl * P.e + cr.run2;
+  cr.cHpre = hl;
+  cr.cH = imax(hl, imax(cr.cE, cr.cQ));
 }
 
 // Traceback-code assembly shared by both row paths.
@@ -125,8 +167,7 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
     const uint32_t np = rps[r + 1] - p0;
     const int32_t H0 = rc0[3 * r], F0 = rc0[3 * r + 1], O0 = rc0[3 * r + 2];
 
-    int32_t run1 = SVS_VNEG, run2 = SVS_VNEG;  // scan carries across strips
-    int32_t cHpre = H0, cQ = SVS_NEG_INF, cE = SVS_NEG_INF, cH = H0;
+    StripCarry cr{SVS_VNEG, SVS_VNEG, H0, SVS_NEG_INF, SVS_NEG_INF, H0};
 
     if (np <= 1) {
       // ---- fast path: zero or one in-edge (the common POA row) ----
@@ -156,19 +197,8 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
         const int32_t O = c0 ? O0 : imax(hp + P.q, op + P.c);
         const int32_t Hpre = c0 ? H0 : imax(hpm + mc, imax(F, O));
 
-        const int32_t prevHpre = wave_shr1(Hpre, cHpre, lane);
-        int32_t x = inner ? prevHpre + P.q - j * P.c : SVS_VNEG;
-        x = imax(wave_prefix_max(x), run1);
-        run1 = readlane63(x);
-        const int32_t Q = inner ? x + j * P.c : SVS_NEG_INF;
-        const int32_t prevQ = wave_shr1(Q, cQ, lane);
-        int32_t y = inner ? imax(prevHpre, prevQ) + P.g - j * P.e : SVS_VNEG;
-        y = imax(wave_prefix_max(y), run2);
-        run2 = readlane63(y);
-        const int32_t E = inner ? y + j * P.e : SVS_NEG_INF;
-        const int32_t H = inner ? imax(Hpre, imax(E, Q)) : H0;
-        const int32_t prevE = wave_shr1(E, cE, lane);
-        const int32_t prevH = wave_shr1(H, cH, lane);
+        int32_t Q, E, H, prevQ, prevE, prevH;
+        strip_gaps(P, lane, j, s << 6, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
 
         const bool dg = inner && H == hpm + mc;
         const bool ua = H == fp + P.e, ub = H == hp + P.g, uc = H == op + P.c, ud = H == hp + P.q;
@@ -187,10 +217,6 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
         pl[so + 2 * LS + j] = O;
         if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
         cHp = readlane63(hp);
-        cHpre = readlane63(Hpre);
-        cQ = readlane63(Q);
-        cE = readlane63(E);
-        cH = readlane63(H);
         hp = hpn; fp = fpn; op = opn; rc = rcn;
       }
       continue;
@@ -220,19 +246,8 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
       if (c0) { F = F0; O = O0; }
       const int32_t Hpre = c0 ? H0 : imax(Hd, imax(F, O));
 
-      const int32_t prevHpre = wave_shr1(Hpre, cHpre, lane);
-      int32_t x = inner ? prevHpre + P.q - j * P.c : SVS_VNEG;
-      x = imax(wave_prefix_max(x), run1);
-      run1 = readlane63(x);
-      const int32_t Q = inner ? x + j * P.c : SVS_NEG_INF;
-      const int32_t prevQ = wave_shr1(Q, cQ, lane);
-      int32_t y = inner ? imax(prevHpre, prevQ) + P.g - j * P.e : SVS_VNEG;
-      y = imax(wave_prefix_max(y), run2);
-      run2 = readlane63(y);
-      const int32_t E = inner ? y + j * P.e : SVS_NEG_INF;
-      const int32_t H = inner ? imax(Hpre, imax(E, Q)) : H0;
-      const int32_t prevE = wave_shr1(E, cE, lane);
-      const int32_t prevH = wave_shr1(H, cH, lane);
+      int32_t Q, E, H, prevQ, prevE, prevH;
+      strip_gaps(P, lane, j, s << 6, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
 
       uint32_t diag_k = 31, up_k = 31, up_ext = 0, uc_k = 31, uc_stop = 0;
       for (uint32_t k = 0; k < np; ++k) {
@@ -266,10 +281,6 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
       pl[so + LS + j] = F;
       pl[so + 2 * LS + j] = O;
       if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
-      cHpre = readlane63(Hpre);
-      cQ = readlane63(Q);
-      cE = readlane63(E);
-      cH = readlane63(H);
     }
   }
 

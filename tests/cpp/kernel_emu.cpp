@@ -65,31 +65,37 @@ std::vector<int32_t> emu_align(const svs::RowTables& T, const std::string& seq, 
         Fv[l] = F; Ov[l] = O;
         Hpre[l] = c0 ? H0 : std::max(Hd, std::max(F, O));
       }
+      // carry-independent scans (kernel v3 formulation)
+      int32_t P1[64], P2[64];
       for (int l = 0; l < 64; ++l) pHpre[l] = l == 0 ? cHpre : Hpre[l - 1];
       for (int l = 0; l < 64; ++l) {
         const int32_t j = s * 64 + l; const bool inner = j <= L && j != 0;
-        x[l] = inner ? pHpre[l] + P.q - j * P.c : VNEG;
+        P1[l] = inner ? pHpre[l] + P.q - j * P.c : VNEG;
       }
-      for (int l = 1; l < 64; ++l) x[l] = std::max(x[l], x[l - 1]);
-      for (int l = 0; l < 64; ++l) x[l] = std::max(x[l], run1);
-      run1 = x[63];
+      for (int l = 1; l < 64; ++l) P1[l] = std::max(P1[l], P1[l - 1]);
       for (int l = 0; l < 64; ++l) {
         const int32_t j = s * 64 + l; const bool inner = j <= L && j != 0;
-        Q[l] = inner ? x[l] + j * P.c : NEG_INF;
+        const int32_t qloc = l > 0 ? P1[l - 1] + (j - 1) * P.c : VNEG;
+        P2[l] = inner ? std::max(pHpre[l], qloc) + P.g - j * P.e : VNEG;
       }
-      for (int l = 0; l < 64; ++l) pQ[l] = l == 0 ? cQ : Q[l - 1];
+      for (int l = 1; l < 64; ++l) P2[l] = std::max(P2[l], P2[l - 1]);
+      const int32_t j0 = s * 64;
+      const int32_t T1 = s > 0 ? cQ + P.g - j0 * P.e : VNEG;
       for (int l = 0; l < 64; ++l) {
         const int32_t j = s * 64 + l; const bool inner = j <= L && j != 0;
-        y[l] = inner ? std::max(pHpre[l], pQ[l]) + P.g - j * P.e : VNEG;
-      }
-      for (int l = 1; l < 64; ++l) y[l] = std::max(y[l], y[l - 1]);
-      for (int l = 0; l < 64; ++l) y[l] = std::max(y[l], run2);
-      run2 = y[63];
-      for (int l = 0; l < 64; ++l) {
-        const int32_t j = s * 64 + l; const bool inner = j <= L && j != 0;
-        E[l] = inner ? y[l] + j * P.e : NEG_INF;
+        const int32_t T2 = l > 0 ? run1 + (j - 1) * P.c + P.g - j * P.e : VNEG;
+        pQ[l] = 0;
+        Q[l] = inner ? j * P.c + std::max(P1[l], run1) : NEG_INF;
+        E[l] = inner ? j * P.e + std::max(std::max(P2[l], run2), std::max(T1, T2)) : NEG_INF;
         H[l] = inner ? std::max(Hpre[l], std::max(E[l], Q[l])) : H0;
       }
+      {
+        const int32_t jl = j0 + 63;
+        const int32_t T2l = run1 + (jl - 1) * P.c + P.g - jl * P.e;
+        run2 = std::max(std::max(run2, P2[63]), std::max(T1, T2l));
+        run1 = std::max(run1, P1[63]);
+      }
+      for (int l = 0; l < 64; ++l) pQ[l] = l == 0 ? cQ : Q[l - 1];
       for (int l = 0; l < 64; ++l) { pE[l] = l == 0 ? cE : E[l - 1]; pH[l] = l == 0 ? cH : H[l - 1]; }
       for (int l = 0; l < 64; ++l) {
         const int32_t j = s * 64 + l;
