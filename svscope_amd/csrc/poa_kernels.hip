@@ -174,25 +174,33 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
       // Next strip's predecessor values are loaded before this strip's stores;
       // H_p[j-1] comes from a wave shift of H_p[j] with a scalar carry.
       const uint64_t ps = np == 0 ? 0 : static_cast<uint64_t>(pslot[p0]) * 3 * LS;
-      int32_t hp = pl[ps + lane], fp = pl[ps + LS + lane], op = pl[ps + 2 * LS + lane];
-      uint8_t rc = seq[lane == 0 ? 0 : lane - 1];
+      // Three register sets, statically named (loop unrolled x3): set k holds
+      // strip s and is reloaded with strip s+3 right after its last use, so no
+      // register copies wait on loads in flight.  Loads are unconditional; the
+      // pool and read arenas are padded past their last row.
+      const int32_t* __restrict__ qh = pl + ps + lane;
+      const uint8_t* __restrict__ qs = seq + lane;
+      struct Ld { int32_t hp, fp, op; uint8_t rc; };
+      auto load = [&](Ld& d, int32_t st) {
+        const int32_t o = st << 6;
+        d.hp = qh[o];
+        d.fp = qh[LS + o];
+        d.op = qh[2 * LS + o];
+        d.rc = (st == 0 && lane == 0) ? uint8_t(0) : qs[o - 1];
+      };
+      Ld A, B, C;
+      load(A, 0);
+      load(B, 1);
+      load(C, 2);
       int32_t cHp = 0;
-      for (int32_t s = 0; s < nstrips; ++s) {
+      auto step = [&](int32_t s, Ld& d) {
         const int32_t j = (s << 6) + lane;
         const bool valid = j <= L;
         const bool c0 = j == 0;
         const bool inner = valid && !c0;
-        int32_t hpn = 0, fpn = 0, opn = 0;
-        uint8_t rcn = 0;
-        if (s + 1 < nstrips) {
-          const int32_t jn = j + 64;
-          hpn = pl[ps + jn];
-          fpn = pl[ps + LS + jn];
-          opn = pl[ps + 2 * LS + jn];
-          rcn = seq[jn - 1];
-        }
+        const int32_t hp = d.hp, fp = d.fp, op = d.op;
         const int32_t hpm = wave_shr1(hp, cHp, lane);
-        const int32_t mc = rc == nb ? P.m : P.n;
+        const int32_t mc = d.rc == nb ? P.m : P.n;
         const int32_t F = c0 ? F0 : imax(hp + P.g, fp + P.e);
         const int32_t O = c0 ? O0 : imax(hp + P.q, op + P.c);
         const int32_t Hpre = c0 ? H0 : imax(hpm + mc, imax(F, O));
@@ -211,13 +219,21 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
             assemble_code(dg ? 0u : 31u, (ua || ub || uc || ud) ? 0u : 31u, (ua || (!ub && uc)) ? 1u : 0u,
                           la || lb || lc || ld, la || (!lb && lc), lbit, vm ? 0u : 31u,
                           (vm && (va || (!vb && vc))) ? 1u : 0u);
-        if (valid) tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+        cHp = readlane63(hp);
+        load(d, s + 3);
+        // columns past L are row padding (never read back)
+        tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
         pl[so + j] = H;
         pl[so + LS + j] = F;
         pl[so + 2 * LS + j] = O;
         if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
-        cHp = readlane63(hp);
-        hp = hpn; fp = fpn; op = opn; rc = rcn;
+      };
+      for (int32_t s = 0; s < nstrips; s += 3) {
+        step(s, A);
+        if (s + 1 >= nstrips) break;
+        step(s + 1, B);
+        if (s + 2 >= nstrips) break;
+        step(s + 2, C);
       }
       continue;
     }

@@ -144,7 +144,8 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
       const Section s_jobs = sec(nj * sizeof(PoaJob));
       const Section s_info = sec(n_rows * 4), s_slot = sec(n_rows * 4), s_ps = sec(n_pstart * 4);
       const Section s_col0 = sec(n_rows * 12);
-      const Section s_prow = sec(n_pred * 4), s_pslot = sec(n_pred * 4), s_seq = sec(n_seq);
+      // the kernel's load pipeline reads up to two strips (128 columns) past a row end
+      const Section s_prow = sec(n_pred * 4), s_pslot = sec(n_pred * 4), s_seq = sec(n_seq + 256);
       ctx->h_stage.ensure(off);
       char* hs = ctx->h_stage.as<char>();
       std::memcpy(hs + s_jobs.off, jobs.data(), s_jobs.bytes);
@@ -167,8 +168,8 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
 
       // ---- device ----
       ctx->d_row_info.ensure(off);  // one arena holds every input section
-      ctx->d_tb.ensure(n_tb * 2);
-      ctx->d_pool.ensure(n_pool * 4);
+      ctx->d_tb.ensure(n_tb * 2 + 4096);
+      ctx->d_pool.ensure(n_pool * 4 + 4096);
       ctx->d_aln.ensure(n_aln * 8);
       ctx->d_aln_len.ensure(nj * 4);
       ctx->h_aln.ensure(n_aln * 8);
