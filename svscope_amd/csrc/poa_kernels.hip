@@ -32,6 +32,7 @@
 //   bits 10-14 in-edge index continuing an up-gap run (31 = none)
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 
 #include "svs_device.hpp"
 
@@ -45,12 +46,24 @@ __device__ __forceinline__ int32_t imax(int32_t a, int32_t b) { return a > b ? a
 // Inclusive prefix max over the 64 lanes of a wave (DPP: row_shr 1/2/4/8,
 // then row_bcast15 / row_bcast31).  Lanes with no source keep the identity.
 __device__ __forceinline__ int32_t wave_prefix_max(int32_t x) {
-  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x111, 0xF, 0xF, false));
-  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x112, 0xF, 0xF, false));
-  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x114, 0xF, 0xF, false));
-  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x118, 0xF, 0xF, false));
-  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x142, 0xA, 0xF, false));
-  x = imax(x, __builtin_amdgcn_update_dpp(SVS_VNEG, x, 0x143, 0xC, 0xF, false));
+  // v_max_i32_dpp x, x[src lane], x: lanes whose DPP source is out of range
+  // (BOUND_CTRL=0) or whose row is masked off are not written and keep x.
+  // Each step reads the previous step's VALU result: 2 wait states (s_nop 1),
+  // which hipcc does not insert inside asm.
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+      : "+v"(x));
   return x;
 }
 
@@ -113,13 +126,13 @@ __device__ __forceinline__ void strip_gaps(const PoaScore& P, int lane, int32_t 
   cr.cH = imax(hl, imax(cr.cE, cr.cQ));
 }
 
-// Traceback-code assembly shared by both row paths.
+// Traceback-code assembly shared by both row paths (branch-free selects).
 __device__ __forceinline__ uint32_t assemble_code(uint32_t diag_k, uint32_t up_k, uint32_t up_ext, bool left_ok,
                                                   bool left_ext, bool lbit, uint32_t uc_k, uint32_t uc_stop) {
-  uint32_t code;
-  if (diag_k != 31) code = diag_k << 3;
-  else if (up_k != 31) code = 1u | (up_ext << 2) | (up_k << 3);
-  else code = left_ok ? (2u | (left_ext ? 4u : 0u)) : 3u;
+  const uint32_t left = left_ok ? (2u | (left_ext ? 4u : 0u)) : 3u;
+  const uint32_t up = 1u | (up_ext << 2) | (up_k << 3);
+  uint32_t code = up_k != 31 ? up : left;
+  code = diag_k != 31 ? (diag_k << 3) : code;
   return code | ((lbit ? 1u : 0u) << 8) | (uc_stop << 9) | (uc_k << 10);
 }
 
@@ -147,6 +160,14 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
   const uint32_t* __restrict__ prow = pred_row + J.pred_off;
   const uint32_t* __restrict__ pslot = pred_slot + J.pred_off;
   const int32_t nstrips = static_cast<int32_t>(LS >> 6);  // LS = 64 * ceil((L+1)/64)
+  // per-job buffer resources (all inputs wave-uniform: J is a scalar load)
+  const __amdgpu_buffer_rsrc_t pool_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(pl, 0, static_cast<int32_t>(J.n_slots * 3u * J.ls * 4u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t tb_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      tbj, 0, static_cast<int32_t>(static_cast<uint64_t>(V) * J.ls * 2u), 0x00020000);
+  // seq_rsrc byte offset b addresses seq[b - 1] (the zero pad byte precedes the read)
+  const __amdgpu_buffer_rsrc_t seq_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(seq) - 1, 0, static_cast<int32_t>(J.ls + 1), 0x00020000);
 
   // virtual row 0 -> slot 0 (planes H, F, O at offsets 0, LS, 2LS), full row width
   for (int32_t j = lane; j < static_cast<int32_t>(LS); j += 64) {
@@ -178,35 +199,48 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
       // strip s and is reloaded with strip s+3 right after its last use, so no
       // register copies wait on loads in flight.  Loads are unconditional; the
       // pool and read arenas are padded past their last row.
-      const int32_t* __restrict__ qh = pl + ps + lane;
-      const uint8_t* __restrict__ qs = seq + lane;
+      // Buffer descriptors (uniform, per job): 32-bit byte offsets, no 64-bit
+      // lane address math; reads past a buffer end return 0 (range-checked).
       struct Ld { int32_t hp, fp, op; uint8_t rc; };
+      const uint32_t lane4 = static_cast<uint32_t>(lane) * 4u;
+      const uint32_t ps4 = static_cast<uint32_t>(ps) * 4u, LS4 = static_cast<uint32_t>(LS) * 4u;
       auto load = [&](Ld& d, int32_t st) {
-        const int32_t o = st << 6;
-        d.hp = qh[o];
-        d.fp = qh[LS + o];
-        d.op = qh[2 * LS + o];
-        d.rc = (st == 0 && lane == 0) ? uint8_t(0) : qs[o - 1];
+        const uint32_t o4 = static_cast<uint32_t>(st) << 8;  // strip offset in bytes (int32 planes)
+        d.hp = __builtin_amdgcn_raw_buffer_load_b32(pool_rsrc, lane4, ps4 + o4, 0);
+        d.fp = __builtin_amdgcn_raw_buffer_load_b32(pool_rsrc, lane4, ps4 + LS4 + o4, 0);
+        d.op = __builtin_amdgcn_raw_buffer_load_b32(pool_rsrc, lane4, ps4 + 2 * LS4 + o4, 0);
+        d.rc = __builtin_amdgcn_raw_buffer_load_b8(seq_rsrc, static_cast<uint32_t>(lane),
+                                                   static_cast<uint32_t>(st) << 6, 0);
       };
       Ld A, B, C;
       load(A, 0);
       load(B, 1);
       load(C, 2);
       int32_t cHp = 0;
-      auto step = [&](int32_t s, Ld& d) {
-        const int32_t j = (s << 6) + lane;
-        const bool valid = j <= L;
-        const bool c0 = j == 0;
-        const bool inner = valid && !c0;
+      const uint32_t so4 = static_cast<uint32_t>(so) * 4u;
+      const uint32_t tro2 = static_cast<uint32_t>(r) * static_cast<uint32_t>(LS) * 2u;
+      const uint32_t lane2 = static_cast<uint32_t>(lane) * 2u;
+      auto step = [&](auto first_tag, int32_t s, Ld& d) {
+        constexpr bool FIRST = decltype(first_tag)::value;
+        const int32_t j0 = s << 6;
+        const int32_t j = j0 + lane;
+        // strips >= 1 need no masks: lanes past L compute row padding that
+        // no valid column ever reads (scans only propagate towards higher j)
+        const bool c0 = FIRST && lane == 0;
+        const bool inner = FIRST ? (lane != 0 && j <= L) : true;
         const int32_t hp = d.hp, fp = d.fp, op = d.op;
         const int32_t hpm = wave_shr1(hp, cHp, lane);
         const int32_t mc = d.rc == nb ? P.m : P.n;
-        const int32_t F = c0 ? F0 : imax(hp + P.g, fp + P.e);
-        const int32_t O = c0 ? O0 : imax(hp + P.q, op + P.c);
-        const int32_t Hpre = c0 ? H0 : imax(hpm + mc, imax(F, O));
-
+        int32_t F = imax(hp + P.g, fp + P.e);
+        int32_t O = imax(hp + P.q, op + P.c);
+        int32_t Hpre = imax(hpm + mc, imax(F, O));
+        if (FIRST) {
+          F = c0 ? F0 : F;
+          O = c0 ? O0 : O;
+          Hpre = c0 ? H0 : Hpre;
+        }
         int32_t Q, E, H, prevQ, prevE, prevH;
-        strip_gaps(P, lane, j, s << 6, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
+        strip_gaps(P, lane, j, j0, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
 
         const bool dg = inner && H == hpm + mc;
         const bool ua = H == fp + P.e, ub = H == hp + P.g, uc = H == op + P.c, ud = H == hp + P.q;
@@ -221,19 +255,23 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
                           (vm && (va || (!vb && vc))) ? 1u : 0u);
         cHp = readlane63(hp);
         load(d, s + 3);
-        // columns past L are row padding (never read back)
-        tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
-        pl[so + j] = H;
-        pl[so + LS + j] = F;
-        pl[so + 2 * LS + j] = O;
+        const uint32_t j04 = static_cast<uint32_t>(j0) * 4u;
+        __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(code), tb_rsrc, lane2,
+                                              tro2 + static_cast<uint32_t>(j0) * 2u, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(H, pool_rsrc, lane4, so4 + j04, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(F, pool_rsrc, lane4, so4 + LS4 + j04, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(O, pool_rsrc, lane4, so4 + 2 * LS4 + j04, 0);
         if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
       };
-      for (int32_t s = 0; s < nstrips; s += 3) {
-        step(s, A);
+      using TrueT = std::integral_constant<bool, true>;
+      using FalseT = std::integral_constant<bool, false>;
+      step(TrueT{}, 0, A);
+      for (int32_t s = 1; s < nstrips; s += 3) {
+        step(FalseT{}, s, B);
         if (s + 1 >= nstrips) break;
-        step(s + 1, B);
+        step(FalseT{}, s + 1, C);
         if (s + 2 >= nstrips) break;
-        step(s + 2, C);
+        step(FalseT{}, s + 2, A);
       }
       continue;
     }

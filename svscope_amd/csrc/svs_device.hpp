@@ -18,7 +18,7 @@ struct PoaJob {
   uint32_t row_off;   // into row_info / row_slot
   uint32_t pstart_off;  // into row_pstart (n_rows + 1 entries)
   uint32_t pred_off;  // base of this job's pred_row / pred_slot entries
-  uint32_t seq_off;   // into seqs (bytes, padded to ls per job)
+  uint32_t seq_off;   // into seqs: read start; seqs[seq_off-1] is a zero pad byte, region ls+64 bytes
   uint32_t n_rows;    // graph nodes
   uint32_t len;       // read length
   uint32_t ls;        // row stride (>= len + 1, multiple of 64)

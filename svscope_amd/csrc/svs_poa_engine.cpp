@@ -117,14 +117,14 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
         J.row_off = static_cast<uint32_t>(n_rows);
         J.pstart_off = static_cast<uint32_t>(n_pstart);
         J.pred_off = static_cast<uint32_t>(n_pred);
-        J.seq_off = static_cast<uint32_t>(n_seq);
+        J.seq_off = static_cast<uint32_t>(n_seq + 1);  // one zero pad byte precedes each read
         J.tb_off = n_tb;
         J.pool_off = n_pool;
         J.aln_off = n_aln;
         n_rows += J.n_rows;
         n_pstart += J.n_rows + 1;
         n_pred += tt.pred_row.size();
-        n_seq += J.ls;  // padded: the kernel prefetches one strip past the read end
+        n_seq += J.ls + 64;  // pad byte + read + tail pad (the kernel prefetches past the read end)
         n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
         n_pool += static_cast<uint64_t>(J.n_slots) * 3 * J.ls;
         n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
@@ -161,8 +161,8 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
           std::memcpy(hs + s_pslot.off + 4ull * J.pred_off, tt.pred_slot.data(), 4 * tt.pred_slot.size());
         }
         const std::string& s = tasks[need[first + k]].seqs[step];
+        std::memset(hs + s_seq.off + J.seq_off - 1, 0, J.ls + 64);
         std::memcpy(hs + s_seq.off + J.seq_off, s.data(), s.size());
-        std::memset(hs + s_seq.off + J.seq_off + s.size(), 0, J.ls - s.size());
       });
       host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
 
