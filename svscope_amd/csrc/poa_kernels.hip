@@ -136,6 +136,42 @@ __device__ __forceinline__ uint32_t assemble_code(uint32_t diag_k, uint32_t up_k
   return code | ((lbit ? 1u : 0u) << 8) | (uc_stop << 9) | (uc_k << 10);
 }
 
+constexpr int kRing = 8;        // carry ring depth between column-chunk waves
+constexpr int kMaxSlots = 64;   // row-pool slots tracked in LDS (host checks)
+constexpr long kSpinLimit = 1l << 26;
+
+// Per-job LDS state when WPJ waves share one job (WPJ > 1).
+struct JobLds {
+  StripCarry ring[3][kRing];   // wave w -> w+1: carries after w's chunk, per row
+  int32_t done[4];             // rows whose carry wave w has published
+  int32_t cons[4];             // rows whose carry wave w has consumed
+  int32_t bnd[4][kMaxSlots];   // per pool slot: H at column 64*sb(w) - 1 (owned by wave w-1)
+  int32_t best[4], best_row[4];
+  int32_t err;
+};
+
+__device__ __forceinline__ int32_t lds_acquire(int32_t* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void lds_release(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Bounded wait until *p >= target; sets *err and gives up after kSpinLimit polls.
+__device__ __forceinline__ void lds_wait_ge(int32_t* p, int32_t target, int32_t* err) {
+  long n = 0;
+  while (lds_acquire(p) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++n > kSpinLimit) { __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); return; }
+  }
+}
+
+// One job = one read against one graph, swept by WPJ waves of a 256-thread
+// block: wave `sub` owns strips [sb, se) of every row.  Row r of wave sub
+// starts once wave sub-1 has published its carries for row r, so the waves of
+// a job run as a row-skewed pipeline; pool columns and traceback codes are
+// private to their wave, and the one value read across a chunk boundary,
+// H[pred][64*sb-1], is kept per pool slot in LDS.
+template <int WPJ>
 __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore P,
     const uint32_t* __restrict__ row_info, const uint32_t* __restrict__ row_slot,
@@ -143,14 +179,20 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
     const uint32_t* __restrict__ pred_slot, const int32_t* __restrict__ col0,
     const uint8_t* __restrict__ seqs, uint16_t* __restrict__ tb, int32_t* __restrict__ pool,
     int32_t* __restrict__ aln, int32_t* __restrict__ aln_len) {
+  constexpr int JPB = 4 / WPJ;  // jobs per block
+  __shared__ JobLds lds_all[WPJ > 1 ? JPB : 1];
   const int lane = threadIdx.x & 63;
-  const int job_id = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  if (job_id >= n_jobs) return;
-  const PoaJob J = jobs[job_id];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int sub = wave % WPJ;
+  JobLds& S = lds_all[WPJ > 1 ? wave / WPJ : 0];
+  const int job_id = __builtin_amdgcn_readfirstlane(blockIdx.x * JPB + wave / WPJ);
+  const bool active = job_id < n_jobs;
+  PoaJob J{};
+  if (active) J = jobs[job_id];
   const int32_t L = static_cast<int32_t>(J.len);
   const uint64_t LS = J.ls;
   const uint32_t V = J.n_rows;
-  const uint8_t* __restrict__ seq = seqs + J.seq_off;  // padded to LS bytes
+  const uint8_t* __restrict__ seq = seqs + J.seq_off;
   int32_t* __restrict__ pl = pool + J.pool_off;
   uint16_t* __restrict__ tbj = tb + J.tb_off;
   const uint32_t* __restrict__ rinfo = row_info + J.row_off;
@@ -160,7 +202,8 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
   const uint32_t* __restrict__ prow = pred_row + J.pred_off;
   const uint32_t* __restrict__ pslot = pred_slot + J.pred_off;
   const int32_t nstrips = static_cast<int32_t>(LS >> 6);  // LS = 64 * ceil((L+1)/64)
-  // per-job buffer resources (all inputs wave-uniform: J is a scalar load)
+  const int32_t chunk = (nstrips + WPJ - 1) / WPJ;
+  const int32_t sb = min(nstrips, sub * chunk), se = min(nstrips, sb + chunk);
   const __amdgpu_buffer_rsrc_t pool_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(pl, 0, static_cast<int32_t>(J.n_slots * 3u * J.ls * 4u), 0x00020000);
   const __amdgpu_buffer_rsrc_t tb_rsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -168,58 +211,86 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
   // seq_rsrc byte offset b addresses seq[b - 1] (the zero pad byte precedes the read)
   const __amdgpu_buffer_rsrc_t seq_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(seq) - 1, 0, static_cast<int32_t>(J.ls + 1), 0x00020000);
+  const uint32_t lane4 = static_cast<uint32_t>(lane) * 4u, lane2 = static_cast<uint32_t>(lane) * 2u;
+  const uint32_t LS4 = static_cast<uint32_t>(LS) * 4u;
 
-  // virtual row 0 -> slot 0 (planes H, F, O at offsets 0, LS, 2LS), full row width
-  for (int32_t j = lane; j < static_cast<int32_t>(LS); j += 64) {
-    pl[j] = row0_h(P, j);
-    pl[LS + j] = j == 0 ? 0 : SVS_NEG_INF;
-    pl[2 * LS + j] = j == 0 ? 0 : SVS_NEG_INF;
+  if (active) {
+    // virtual row 0 -> slot 0 (planes H, F, O at offsets 0, LS, 2LS), own columns
+    for (int32_t j = sb * 64 + lane; j < se * 64; j += 64) {
+      pl[j] = row0_h(P, j);
+      pl[LS + j] = j == 0 ? 0 : SVS_NEG_INF;
+      pl[2 * LS + j] = j == 0 ? 0 : SVS_NEG_INF;
+    }
+  }
+  if (WPJ > 1) {
+    if (lane == 0) {
+      S.done[sub] = 0;
+      S.cons[sub] = 0;
+      if (sub > 0) S.bnd[sub][0] = row0_h(P, sb * 64 - 1);
+      if (sub == 0) S.err = 0;
+      S.best[sub] = SVS_NEG_INF;
+      S.best_row[sub] = 0;
+    }
+    __syncthreads();
   }
 
   int32_t best = SVS_NEG_INF;  // meaningful on the lane owning column L
   int32_t best_row = 0;
 
-  for (uint32_t r = 0; r < V; ++r) {
+  for (uint32_t r = 0; active && r < V; ++r) {
     const uint32_t info = rinfo[r];
     const uint8_t nb = static_cast<uint8_t>(info & 0xFF);
     const bool sink = (info >> 8) & 1;
-    const uint64_t so = static_cast<uint64_t>(rslot[r]) * 3 * LS;
+    const uint32_t rs = rslot[r];
+    const uint64_t so = static_cast<uint64_t>(rs) * 3 * LS;
     const uint32_t p0 = rps[r];
     const uint32_t np = rps[r + 1] - p0;
     const int32_t H0 = rc0[3 * r], F0 = rc0[3 * r + 1], O0 = rc0[3 * r + 2];
 
     StripCarry cr{SVS_VNEG, SVS_VNEG, H0, SVS_NEG_INF, SVS_NEG_INF, H0};
+    if (WPJ > 1 && sub > 0) {
+      lds_wait_ge(&S.done[sub - 1], static_cast<int32_t>(r) + 1, &S.err);
+      const StripCarry& in = S.ring[sub - 1][r % kRing];
+      cr.run1 = __builtin_amdgcn_readfirstlane(in.run1);
+      cr.run2 = __builtin_amdgcn_readfirstlane(in.run2);
+      cr.cHpre = __builtin_amdgcn_readfirstlane(in.cHpre);
+      cr.cQ = __builtin_amdgcn_readfirstlane(in.cQ);
+      cr.cE = __builtin_amdgcn_readfirstlane(in.cE);
+      cr.cH = __builtin_amdgcn_readfirstlane(in.cH);
+      if (lane == 0) {
+        lds_release(&S.cons[sub], static_cast<int32_t>(r) + 1);
+        S.bnd[sub][rs] = cr.cH;  // H[r][64*sb - 1] for later successors of r
+      }
+    }
 
-    if (np <= 1) {
+    if (np <= 1 && sb < se) {
       // ---- fast path: zero or one in-edge (the common POA row) ----
-      // Next strip's predecessor values are loaded before this strip's stores;
-      // H_p[j-1] comes from a wave shift of H_p[j] with a scalar carry.
-      const uint64_t ps = np == 0 ? 0 : static_cast<uint64_t>(pslot[p0]) * 3 * LS;
-      // Three register sets, statically named (loop unrolled x3): set k holds
-      // strip s and is reloaded with strip s+3 right after its last use, so no
-      // register copies wait on loads in flight.  Loads are unconditional; the
-      // pool and read arenas are padded past their last row.
-      // Buffer descriptors (uniform, per job): 32-bit byte offsets, no 64-bit
-      // lane address math; reads past a buffer end return 0 (range-checked).
+      // Three statically named load sets (loop unrolled x3): set k holds strip
+      // s and is reloaded with strip s+3 right after its last use, so no waits
+      // on loads in flight.  Buffer loads past a buffer end return 0.
+      const uint32_t ps = np == 0 ? 0u : pslot[p0];
+      const uint32_t ps4 = ps * 3u * static_cast<uint32_t>(LS) * 4u;
       struct Ld { int32_t hp, fp, op; uint8_t rc; };
-      const uint32_t lane4 = static_cast<uint32_t>(lane) * 4u;
-      const uint32_t ps4 = static_cast<uint32_t>(ps) * 4u, LS4 = static_cast<uint32_t>(LS) * 4u;
       auto load = [&](Ld& d, int32_t st) {
-        const uint32_t o4 = static_cast<uint32_t>(st) << 8;  // strip offset in bytes (int32 planes)
+        const uint32_t o4 = static_cast<uint32_t>(st) << 8;
         d.hp = __builtin_amdgcn_raw_buffer_load_b32(pool_rsrc, lane4, ps4 + o4, 0);
         d.fp = __builtin_amdgcn_raw_buffer_load_b32(pool_rsrc, lane4, ps4 + LS4 + o4, 0);
         d.op = __builtin_amdgcn_raw_buffer_load_b32(pool_rsrc, lane4, ps4 + 2 * LS4 + o4, 0);
         d.rc = __builtin_amdgcn_raw_buffer_load_b8(seq_rsrc, static_cast<uint32_t>(lane),
                                                    static_cast<uint32_t>(st) << 6, 0);
       };
-      Ld A, B, C;
-      load(A, 0);
-      load(B, 1);
-      load(C, 2);
-      int32_t cHp = 0;
+      // chunk starting at strip 0: strip 0 (masks for column 0 / validity) runs
+      // first from its own load set Z; the unrolled loop then always starts at A
+      const int32_t s1 = sb == 0 ? 1 : sb;
+      Ld Z, A, B, C;
+      if (sb == 0) load(Z, 0);
+      load(A, s1);
+      load(B, s1 + 1);
+      load(C, s1 + 2);
+      int32_t cHp = (WPJ > 1 && sub > 0) ? S.bnd[sub][ps] : 0;
+      if (WPJ > 1) cHp = __builtin_amdgcn_readfirstlane(cHp);
       const uint32_t so4 = static_cast<uint32_t>(so) * 4u;
-      const uint32_t tro2 = static_cast<uint32_t>(r) * static_cast<uint32_t>(LS) * 2u;
-      const uint32_t lane2 = static_cast<uint32_t>(lane) * 2u;
+      const uint32_t tro2 = r * static_cast<uint32_t>(LS) * 2u;
       auto step = [&](auto first_tag, int32_t s, Ld& d) {
         constexpr bool FIRST = decltype(first_tag)::value;
         const int32_t j0 = s << 6;
@@ -265,86 +336,121 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
       };
       using TrueT = std::integral_constant<bool, true>;
       using FalseT = std::integral_constant<bool, false>;
-      step(TrueT{}, 0, A);
-      for (int32_t s = 1; s < nstrips; s += 3) {
-        step(FalseT{}, s, B);
-        if (s + 1 >= nstrips) break;
-        step(FalseT{}, s + 1, C);
-        if (s + 2 >= nstrips) break;
-        step(FalseT{}, s + 2, A);
+      if (sb == 0) step(TrueT{}, 0, Z);
+      for (int32_t s = s1; s < se; s += 3) {
+        step(FalseT{}, s, A);
+        if (s + 1 >= se) break;
+        step(FalseT{}, s + 1, B);
+        if (s + 2 >= se) break;
+        step(FalseT{}, s + 2, C);
       }
-      continue;
+    } else if (sb < se) {
+      // ---- general path: two or more in-edges ----
+      for (int32_t s = sb; s < se; ++s) {
+        const int32_t j = (s << 6) + lane;
+        const bool valid = j <= L;
+        const bool c0 = j == 0;
+        const bool inner = valid && !c0;
+        const bool edge = WPJ > 1 && s == sb && sb > 0 && lane == 0;  // H[p][j-1] owned by wave sub-1
+        const int32_t mc = (inner && seq[j - 1] == nb) ? P.m : P.n;
+
+        int32_t F = SVS_VNEG, O = SVS_VNEG, Hd = SVS_VNEG;
+        int32_t hpm0 = 0, hp0 = 0, fp0 = 0, op0 = 0;  // first in-edge kept in registers
+        for (uint32_t k = 0; k < np; ++k) {
+          const uint32_t psk = pslot[p0 + k];
+          const uint64_t ps = static_cast<uint64_t>(psk) * 3 * LS;
+          const int32_t hpm = c0 ? 0 : (edge ? S.bnd[sub][psk] : pl[ps + j - 1]);
+          const int32_t hp = pl[ps + j];
+          const int32_t fp = pl[ps + LS + j];
+          const int32_t op = pl[ps + 2 * LS + j];
+          if (k == 0) { hpm0 = hpm; hp0 = hp; fp0 = fp; op0 = op; }
+          F = imax(F, imax(hp + P.g, fp + P.e));
+          O = imax(O, imax(hp + P.q, op + P.c));
+          Hd = imax(Hd, hpm + mc);
+        }
+        if (c0) { F = F0; O = O0; }
+        const int32_t Hpre = c0 ? H0 : imax(Hd, imax(F, O));
+        int32_t Q, E, H, prevQ, prevE, prevH;
+        strip_gaps(P, lane, j, s << 6, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
+
+        uint32_t diag_k = 31, up_k = 31, up_ext = 0, uc_k = 31, uc_stop = 0;
+        for (uint32_t k = 0; k < np; ++k) {
+          int32_t hpm, hp, fp, op;
+          if (k == 0) {
+            hpm = hpm0; hp = hp0; fp = fp0; op = op0;
+          } else {
+            const uint32_t psk = pslot[p0 + k];
+            const uint64_t ps = static_cast<uint64_t>(psk) * 3 * LS;
+            hpm = c0 ? 0 : (edge ? S.bnd[sub][psk] : pl[ps + j - 1]);
+            hp = pl[ps + j];
+            fp = pl[ps + LS + j];
+            op = pl[ps + 2 * LS + j];
+          }
+          if (inner && diag_k == 31 && H == hpm + mc) diag_k = k;
+          if (up_k == 31) {
+            const bool a = H == fp + P.e, b = H == hp + P.g, c = H == op + P.c, d = H == hp + P.q;
+            if (a || b || c || d) { up_k = k; up_ext = (a || (!b && c)) ? 1u : 0u; }
+          }
+          if (uc_k == 31) {
+            const bool a = F == hp + P.g, b = F == fp + P.e, c = O == hp + P.q, d = O == op + P.c;
+            if (a || b || c || d) { uc_k = k; uc_stop = (a || (!b && c)) ? 1u : 0u; }
+          }
+        }
+        const bool la = inner && H == prevE + P.e, lb = inner && H == prevH + P.g;
+        const bool lc = inner && H == prevQ + P.c, ld = inner && H == prevH + P.q;
+        const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
+        const uint32_t code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k,
+                                            uc_stop);
+        if (valid) tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+        pl[so + j] = H;
+        pl[so + LS + j] = F;
+        pl[so + 2 * LS + j] = O;
+        if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
+      }
     }
 
-    // ---- general path: two or more in-edges ----
-    for (int32_t s = 0; s < nstrips; ++s) {
-      const int32_t j = (s << 6) + lane;
-      const bool valid = j <= L;
-      const bool c0 = j == 0;
-      const bool inner = valid && !c0;
-      const int32_t mc = (inner && seq[j - 1] == nb) ? P.m : P.n;
-
-      int32_t F = SVS_VNEG, O = SVS_VNEG, Hd = SVS_VNEG;
-      int32_t hpm0 = 0, hp0 = 0, fp0 = 0, op0 = 0;  // first in-edge kept in registers
-      for (uint32_t k = 0; k < np; ++k) {
-        const uint64_t ps = static_cast<uint64_t>(pslot[p0 + k]) * 3 * LS;
-        const int32_t hpm = c0 ? 0 : pl[ps + j - 1];
-        const int32_t hp = pl[ps + j];
-        const int32_t fp = pl[ps + LS + j];
-        const int32_t op = pl[ps + 2 * LS + j];
-        if (k == 0) { hpm0 = hpm; hp0 = hp; fp0 = fp; op0 = op; }
-        F = imax(F, imax(hp + P.g, fp + P.e));
-        O = imax(O, imax(hp + P.q, op + P.c));
-        Hd = imax(Hd, hpm + mc);
+    if (WPJ > 1 && sub < WPJ - 1) {
+      // publish this row's carries once the consumer has freed the ring slot
+      lds_wait_ge(&S.cons[sub + 1], static_cast<int32_t>(r) + 1 - kRing, &S.err);
+      if (lane == 0) {
+        StripCarry& out = S.ring[sub][r % kRing];
+        out = cr;
+        lds_release(&S.done[sub], static_cast<int32_t>(r) + 1);
       }
-      if (c0) { F = F0; O = O0; }
-      const int32_t Hpre = c0 ? H0 : imax(Hd, imax(F, O));
-
-      int32_t Q, E, H, prevQ, prevE, prevH;
-      strip_gaps(P, lane, j, s << 6, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
-
-      uint32_t diag_k = 31, up_k = 31, up_ext = 0, uc_k = 31, uc_stop = 0;
-      for (uint32_t k = 0; k < np; ++k) {
-        int32_t hpm, hp, fp, op;
-        if (k == 0) {
-          hpm = hpm0; hp = hp0; fp = fp0; op = op0;
-        } else {
-          const uint64_t ps = static_cast<uint64_t>(pslot[p0 + k]) * 3 * LS;
-          hpm = c0 ? 0 : pl[ps + j - 1];
-          hp = pl[ps + j];
-          fp = pl[ps + LS + j];
-          op = pl[ps + 2 * LS + j];
-        }
-        if (inner && diag_k == 31 && H == hpm + mc) diag_k = k;
-        if (up_k == 31) {
-          const bool a = H == fp + P.e, b = H == hp + P.g, c = H == op + P.c, d = H == hp + P.q;
-          if (a || b || c || d) { up_k = k; up_ext = (a || (!b && c)) ? 1u : 0u; }
-        }
-        if (uc_k == 31) {
-          const bool a = F == hp + P.g, b = F == fp + P.e, c = O == hp + P.q, d = O == op + P.c;
-          if (a || b || c || d) { uc_k = k; uc_stop = (a || (!b && c)) ? 1u : 0u; }
-        }
-      }
-      const bool la = inner && H == prevE + P.e, lb = inner && H == prevH + P.g;
-      const bool lc = inner && H == prevQ + P.c, ld = inner && H == prevH + P.q;
-      const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
-      const uint32_t code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k,
-                                          uc_stop);
-      if (valid) tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
-      pl[so + j] = H;
-      pl[so + LS + j] = F;
-      pl[so + 2 * LS + j] = O;
-      if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
     }
   }
 
-  // Make the wave's traceback-code stores visible to its own lane 0.
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  if (WPJ > 1) {
+    // gather the sink maximum (lane owning column L of the owning wave) and
+    // make every wave's traceback codes visible to wave 0
+    const int owner_lane = L & 63;
+    const int32_t b = __shfl(best, owner_lane, 64), br = __shfl(best_row, owner_lane, 64);
+    if (lane == 0 && sb * 64 <= L && L < se * 64) {
+      S.best[sub] = b;
+      S.best_row[sub] = br;
+    }
+    __syncthreads();
+    if (!active || sub != 0) return;
+    int32_t bb = SVS_NEG_INF, bbr = 0;
+    for (int w = 0; w < WPJ; ++w)
+      if (S.best_row[w] != 0) { bb = S.best[w]; bbr = S.best_row[w]; }
+    (void)bb;
+    best_row = bbr;
+    if (S.err) {
+      if (lane == 0) aln_len[job_id] = -1;
+      return;
+    }
+  } else {
+    if (!active) return;
+  }
 
-  const int owner = L & 63;
-  best_row = __shfl(best_row, owner, 64);
+  if (WPJ == 1) {
+    // Make the wave's traceback-code stores visible to its own lane 0.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    best_row = __shfl(best_row, L & 63, 64);
+  }
   if (lane != 0) return;
 
   // ---- traceback (spoa backtrack order), lane 0 ----
@@ -419,11 +525,17 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
 
 hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream) {
   if (a.n_jobs <= 0) return hipSuccess;
-  const int waves_per_block = 4;
-  const int blocks = (a.n_jobs + waves_per_block - 1) / waves_per_block;
-  hipLaunchKernelGGL(poa_nw_convex_kernel, dim3(blocks), dim3(64 * waves_per_block), 0, stream,
-                     a.jobs, a.n_jobs, a.score, a.row_info, a.row_slot, a.row_pstart, a.pred_row,
-                     a.pred_slot, a.col0, a.seqs, a.tb, a.pool, a.aln, a.aln_len);
+  const int wpj = a.waves_per_job;
+  const int jpb = 4 / wpj;
+  const int blocks = (a.n_jobs + jpb - 1) / jpb;
+#define SVS_LAUNCH(W)                                                                                     \
+  hipLaunchKernelGGL(poa_nw_convex_kernel<W>, dim3(blocks), dim3(256), 0, stream, a.jobs, a.n_jobs, a.score, \
+                     a.row_info, a.row_slot, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb,     \
+                     a.pool, a.aln, a.aln_len)
+  if (wpj == 4) SVS_LAUNCH(4);
+  else if (wpj == 2) SVS_LAUNCH(2);
+  else SVS_LAUNCH(1);
+#undef SVS_LAUNCH
   return hipGetLastError();
 }
 

@@ -40,7 +40,10 @@ struct PoaLaunch {
   int32_t* pool;
   int32_t* aln;
   int32_t* aln_len;
+  int waves_per_job;  // 1, 2 or 4 (column-chunk waves per job)
 };
+
+constexpr uint32_t kPoaMaxSlotsMultiWave = 64;
 
 hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream);
 hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -37,6 +38,28 @@ void check_poa_config(const svs_poa_config& c) {
 }
 
 namespace {
+
+// Waves per job: enough column-chunk waves to put ~4 waves on each SIMD
+// (1024 SIMDs on MI355X), only for jobs wide enough to split (>= 8 strips per
+// wave) and pools small enough for the LDS boundary table.
+int choose_waves_per_job(const std::vector<PoaJob>& jobs, size_t nj) {
+  if (const char* e = std::getenv("SVS_POA_WPJ")) {
+    const int w = std::atoi(e);
+    if (w == 1 || w == 2 || w == 4) {
+      for (size_t k = 0; k < nj; ++k)
+        if (w > 1 && jobs[k].n_slots > kPoaMaxSlotsMultiWave) return 1;
+      return w;
+    }
+  }
+  uint32_t min_strips = 0xFFFFFFFFu;
+  for (size_t k = 0; k < nj; ++k) {
+    if (jobs[k].n_slots > kPoaMaxSlotsMultiWave) return 1;
+    min_strips = std::min(min_strips, jobs[k].ls / 64);
+  }
+  int w = 1;
+  while (w < 4 && static_cast<size_t>(w) * nj < 4096 && min_strips >= static_cast<uint32_t>(16 * w)) w *= 2;
+  return w;
+}
 
 struct JobSizes {
   uint64_t tb, pool, aln;
@@ -191,6 +214,7 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
       la.pool = ctx->d_pool.as<int32_t>();
       la.aln = ctx->d_aln.as<int32_t>();
       la.aln_len = ctx->d_aln_len.as<int32_t>();
+      la.waves_per_job = choose_waves_per_job(jobs, nj);
       SVS_HIP(hipEventRecord(ctx->ev_start, ctx->stream));
       SVS_HIP(launch_poa_nw_convex(la, ctx->stream));
       SVS_HIP(hipEventRecord(ctx->ev_stop, ctx->stream));
