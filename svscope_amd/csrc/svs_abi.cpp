@@ -104,13 +104,9 @@ void svs_release(svs_context* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  for (svs::DeviceBuf* b : {&ctx->d_jobs, &ctx->d_row_info, &ctx->d_row_slot, &ctx->d_row_pstart,
-                            &ctx->d_pred_row, &ctx->d_pred_slot, &ctx->d_seqs, &ctx->d_tb, &ctx->d_pool,
-                            &ctx->d_aln, &ctx->d_aln_len, &ctx->d_em_in, &ctx->d_em_ws, &ctx->d_em_out,
-                            &ctx->d_rng})
-    b->release();
-  for (svs::PinnedBuf* b : {&ctx->h_stage, &ctx->h_aln, &ctx->h_aln_len, &ctx->h_em_in, &ctx->h_em_out})
-    b->release();
+  ctx->poa_arenas.clear();
+  for (svs::DeviceBuf* b : {&ctx->d_em_in, &ctx->d_em_ws, &ctx->d_em_out, &ctx->d_rng}) b->release();
+  for (svs::PinnedBuf* b : {&ctx->h_em_in, &ctx->h_em_out}) b->release();
   if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
   if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

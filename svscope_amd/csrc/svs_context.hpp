@@ -5,6 +5,8 @@
 
 #include "threadpool.hpp"
 
+#include <memory>
+
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -74,6 +76,30 @@ struct PinnedBuf {
   }
 };
 
+// Device + pinned buffers and a stream for one in-flight POA launch.
+struct PoaArena {
+  DeviceBuf d_in, d_tb, d_pool, d_aln, d_alen;
+  PinnedBuf h_in, h_aln, h_alen;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  explicit PoaArena(int device) {
+    SVS_HIP(hipSetDevice(device));
+    SVS_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    SVS_HIP(hipEventCreate(&ev0));
+    SVS_HIP(hipEventCreate(&ev1));
+  }
+  ~PoaArena() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (DeviceBuf* b : {&d_in, &d_tb, &d_pool, &d_aln, &d_alen}) b->release();
+    for (PinnedBuf* b : {&h_in, &h_aln, &h_alen}) b->release();
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  PoaArena(const PoaArena&) = delete;
+  PoaArena& operator=(const PoaArena&) = delete;
+};
+
 }  // namespace svs
 
 struct svs_context {
@@ -82,10 +108,8 @@ struct svs_context {
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
   svs::ThreadPool* pool = nullptr;
   size_t device_budget = 0;  // bytes usable for traceback + row pool per launch
-  // POA arenas
-  svs::DeviceBuf d_jobs, d_row_info, d_row_slot, d_row_pstart, d_pred_row, d_pred_slot, d_seqs;
-  svs::DeviceBuf d_tb, d_pool, d_aln, d_aln_len;
-  svs::PinnedBuf h_stage, h_aln, h_aln_len;
+  // POA arenas, one per concurrently in-flight task group
+  std::vector<std::unique_ptr<svs::PoaArena>> poa_arenas;
   // EM arenas
   svs::DeviceBuf d_em_in, d_em_ws, d_em_out, d_rng;
   svs::PinnedBuf h_em_in, h_em_out;
