@@ -172,7 +172,9 @@ void PoaGraph::export_rows(RowTables* t) const {
   t->pred_row.clear();
   t->pred_slot.clear();
   t->max_preds = 0;
-  std::vector<uint32_t> last_use(V);
+  static thread_local std::vector<uint32_t> last_use, free_slots;
+  last_use.resize(V);
+  free_slots.clear();
   uint32_t np = 0;
   for (uint32_t r = 0; r < V; ++r) {
     const uint32_t node = rank_to_node_[r];
@@ -191,7 +193,6 @@ void PoaGraph::export_rows(RowTables* t) const {
   t->pred_slot.resize(np);
   // Row-pool slot assignment: a row lives from its computation until its last
   // successor has been computed; slot 0 holds the virtual row 0 for the whole job.
-  std::vector<uint32_t> free_slots;
   uint32_t next = 1;
   for (uint32_t r = 0; r < V; ++r) {
     uint32_t s;

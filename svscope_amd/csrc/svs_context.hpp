@@ -80,13 +80,13 @@ struct PinnedBuf {
 struct PoaArena {
   DeviceBuf d_in, d_tb, d_pool, d_aln, d_alen;
   PinnedBuf h_in, h_aln, h_alen;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  explicit PoaArena(int device) {
+  hipStream_t stream = nullptr;  // shared, in-order: groups alternate on the GPU
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+  PoaArena(int device, hipStream_t s) : stream(s) {
     SVS_HIP(hipSetDevice(device));
-    SVS_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     SVS_HIP(hipEventCreate(&ev0));
     SVS_HIP(hipEventCreate(&ev1));
+    SVS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
   }
   ~PoaArena() {
     if (stream) (void)hipStreamSynchronize(stream);
@@ -94,7 +94,7 @@ struct PoaArena {
     for (PinnedBuf* b : {&h_in, &h_aln, &h_alen}) b->release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
-    if (stream) (void)hipStreamDestroy(stream);
+    if (done) (void)hipEventDestroy(done);
   }
   PoaArena(const PoaArena&) = delete;
   PoaArena& operator=(const PoaArena&) = delete;

@@ -11,6 +11,7 @@ namespace svs {
 struct PoaTask {
   std::vector<std::string> seqs;
   PoaGraph graph;
+  RowTables rows;  // exported row tables of the current step (capacity reused across steps)
   std::string consensus;
   std::vector<std::string> msa;
 };

@@ -72,8 +72,7 @@ double ms_since(Clock::time_point t0) {
 
 // One launch in flight: the jobs of one task group at one step.
 struct Launch {
-  std::vector<uint32_t> ids;       // task indices, one job each
-  std::vector<RowTables> tables;   // exported row tables, same order
+  std::vector<uint32_t> ids;       // task indices, one job each (tables in PoaTask::rows)
   std::vector<PoaJob> jobs;
   size_t step = 0;
   size_t n_aln = 0;
@@ -95,7 +94,7 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, 
   uint64_t n_rows = 0, n_pstart = 0, n_pred = 0, n_seq = 0, n_tb = 0, n_pool = 0, n_aln = 0;
   uint32_t max_preds = 0;
   for (size_t k = 0; k < nj; ++k) {
-    const auto& tt = la.tables[k];
+    const auto& tt = tasks[la.ids[k]].rows;
     const std::string& s = tasks[la.ids[k]].seqs[la.step];
     PoaJob& J = la.jobs[k];
     J.n_rows = static_cast<uint32_t>(tt.info.size());
@@ -139,7 +138,7 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, 
   char* hs = A.h_in.as<char>();
   std::memcpy(hs + s_jobs, la.jobs.data(), nj * sizeof(PoaJob));
   ctx->pool->parallel_for(nj, [&](size_t k) {
-    const auto& tt = la.tables[k];
+    const auto& tt = tasks[la.ids[k]].rows;
     const PoaJob& J = la.jobs[k];
     std::memcpy(hs + s_info + 4ull * J.row_off, tt.info.data(), 4ull * J.n_rows);
     std::memcpy(hs + s_slot + 4ull * J.row_off, tt.slot.data(), 4ull * J.n_rows);
@@ -185,6 +184,7 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, 
   SVS_HIP(hipEventRecord(A.ev1, A.stream));
   SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 4, hipMemcpyDeviceToHost, A.stream));
   SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, pl.aln, n_aln * 8, hipMemcpyDeviceToHost, A.stream));
+  SVS_HIP(hipEventRecord(A.done, A.stream));
   st.launches += 1;
   st.alignments += nj;
   st.tb_bytes += n_tb * 2;
@@ -196,7 +196,7 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, 
 // Waits for the launch and folds its alignments back into the graphs.
 void finish(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, svs_poa_stats& st, double& host_ms) {
   PoaArena& A = *la.arena;
-  SVS_HIP(hipStreamSynchronize(A.stream));
+  SVS_HIP(hipEventSynchronize(A.done));  // the other group's launch may still be queued behind it
   float ms = 0.f;
   SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
   st.kernel_ms += ms;
@@ -218,8 +218,9 @@ void finish(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, svs_poa_s
   host_ms += ms_since(th0);
 }
 
-// Task group: a disjoint subset of the jobs that advances step by step on its
-// own stream/arena, so its host work overlaps the other group's kernel.
+// Task group: a disjoint subset of the jobs that advances step by step with its
+// own arena.  Groups alternate on one in-order stream, so while the GPU runs
+// group B's step the host folds group A's alignments and enqueues A's next step.
 struct Group {
   std::vector<uint32_t> members;
   size_t step = 0, max_steps = 0;
@@ -249,17 +250,16 @@ bool advance(svs_context* ctx, Group& g, PoaArena* arena, std::vector<PoaTask>& 
       if (needs[i]) ids.push_back(g.members[i]);
     ++g.step;
     if (ids.empty()) { host_ms += ms_since(th0); continue; }
-    std::vector<RowTables> tables(ids.size());
     ctx->pool->parallel_for(ids.size(), [&](size_t k) {
-      tasks[ids[k]].graph.export_rows(&tables[k]);
-      fill_col0(&tables[k], cfg.g, cfg.e, cfg.q, cfg.c);
+      auto& t = tasks[ids[k]];
+      t.graph.export_rows(&t.rows);
+      fill_col0(&t.rows, cfg.g, cfg.e, cfg.q, cfg.c);
     });
     host_ms += ms_since(th0);
     uint64_t total = 0;
-    for (size_t k = 0; k < ids.size(); ++k) total += job_bytes(tables[k], tasks[ids[k]].seqs[step].size());
+    for (size_t k = 0; k < ids.size(); ++k) total += job_bytes(tasks[ids[k]].rows, tasks[ids[k]].seqs[step].size());
     if (total <= budget) {
       g.la.ids = std::move(ids);
-      g.la.tables = std::move(tables);
       g.la.step = step;
       g.la.arena = arena;
       pack_and_launch(ctx, g.la, tasks, score, st, host_ms);
@@ -272,14 +272,13 @@ bool advance(svs_context* ctx, Group& g, PoaArena* arena, std::vector<PoaTask>& 
       size_t last = first;
       uint64_t bytes = 0;
       while (last < ids.size()) {
-        const uint64_t b = job_bytes(tables[last], tasks[ids[last]].seqs[step].size());
+        const uint64_t b = job_bytes(tasks[ids[last]].rows, tasks[ids[last]].seqs[step].size());
         if (last > first && bytes + b > budget) break;
         bytes += b;
         ++last;
       }
       Launch sub;
       sub.ids.assign(ids.begin() + first, ids.begin() + last);
-      sub.tables.assign(std::make_move_iterator(tables.begin() + first), std::make_move_iterator(tables.begin() + last));
       sub.step = step;
       sub.arena = arena;
       pack_and_launch(ctx, sub, tasks, score, st, host_ms);
@@ -300,7 +299,7 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
   const PoaScore score{cfg.m, cfg.n, cfg.g, cfg.e, cfg.q, cfg.c};
   // Two groups once there are enough jobs to keep the GPU busy with half of them.
   const size_t n_groups = tasks.size() >= 64 ? 2 : 1;
-  while (ctx->poa_arenas.size() < n_groups) ctx->poa_arenas.emplace_back(new PoaArena(ctx->device));
+  while (ctx->poa_arenas.size() < n_groups) ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
   std::vector<Group> groups(n_groups);
   for (size_t i = 0; i < tasks.size(); ++i) {
     Group& g = groups[i % n_groups];

@@ -4,6 +4,7 @@
 // recurrence, traceback codes and code-driven traceback against the oracle
 // without a GPU.  Not part of the product library.
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cstdint>
 #include <cstring>
@@ -193,7 +194,7 @@ std::vector<int32_t> emu_align(const svs::RowTables& T, const std::string& seq, 
   return fwd;
 }
 
-struct EmuResult { std::string consensus, error; std::vector<std::string> msa; uint32_t max_slots = 0; };
+struct EmuResult { std::string consensus, error; std::vector<std::string> msa; uint32_t max_slots = 0; double graph_ms = 0, dp_ms = 0; };
 }  // namespace
 
 extern "C" {
@@ -207,10 +208,17 @@ void* emu_poa(int n, const char* const* seqs, const int* lens, int m, int mis, i
       std::string seq(seqs[s], static_cast<size_t>(lens[s]));
       if (seq.empty()) continue;
       if (graph.empty()) { graph.add_alignment_nodes({}, seq); continue; }
+      auto t0 = std::chrono::steady_clock::now();
       graph.export_rows(&T);
       svs::fill_col0(&T, P.g, P.e, P.q, P.c);
+      auto t1 = std::chrono::steady_clock::now();
       r->max_slots = std::max(r->max_slots, T.n_slots);
-      graph.add_alignment_ranks(emu_align(T, seq, P), seq);
+      auto aln = emu_align(T, seq, P);
+      auto t2 = std::chrono::steady_clock::now();
+      graph.add_alignment_ranks(aln, seq);
+      auto t3 = std::chrono::steady_clock::now();
+      r->graph_ms += std::chrono::duration<double, std::milli>((t1 - t0) + (t3 - t2)).count();
+      r->dp_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
     }
     r->consensus = graph.consensus(-1);
     r->msa = graph.msa();
@@ -223,4 +231,5 @@ int emu_msa_rows(void* h) { return static_cast<int>(static_cast<EmuResult*>(h)->
 const char* emu_msa_row(void* h, int i) { return static_cast<EmuResult*>(h)->msa[i].c_str(); }
 int emu_max_slots(void* h) { return static_cast<int>(static_cast<EmuResult*>(h)->max_slots); }
 void emu_free(void* h) { delete static_cast<EmuResult*>(h); }
+double emu_graph_ms(void* h) { return static_cast<EmuResult*>(h)->graph_ms; }
 }
