@@ -131,10 +131,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    cells = sum(st["dp_cells"] for _, st in stats)
-    kms = sum(st["kernel_ms"] for _, st in stats)
-    launches = sum(st["launches"] for _, st in stats)
-    host_ms = sum(st["host_graph_ms"] for _, st in stats)
+    poa_stats = [st for name, st in stats if name in ("msa_poa", "consensus_poa")]
+    cells = sum(st["dp_cells"] for st in poa_stats)
+    kms = sum(st["kernel_ms"] for st in poa_stats)
+    launches = sum(st["launches"] for st in poa_stats)
+    host_ms = sum(st["host_graph_ms"] for st in poa_stats)
+    phases = {}
+    for name, st in stats:
+        if name == "phases":
+            for k, v in st.items():
+                phases[k] = round(phases.get(k, 0.0) + v, 3)
     achieved = cells * BYTES_PER_CELL / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     total_windows = B * K * world
 
@@ -175,6 +181,7 @@ def main():
             "breakdown": {"poa_cells": cells, "poa_kernel_ms": round(kms, 2), "poa_launches": launches,
                           "gcups": round(cells / (kms * 1e-3) / 1e9, 3) if kms else None,
                           "host_graph_ms": round(host_ms, 1), "em_output_windows": n_em,
+                          "phases_s": phases,
                           "em_dtype": "f64"},
         }
         print(json.dumps(out), flush=True)

@@ -114,6 +114,18 @@ int svs_similarity_batch(svs_context* ctx, int32_t n_windows, const svs_em_windo
                          const int64_t* s_off, double* S);
 int svs_em_batch(svs_context* ctx, int32_t n_windows, const svs_em_window* wins, const uint8_t* X,
                  const int32_t* labels, const svs_em_config* cfg, svs_em_result** out);
+/* scipy linkage(S, 'ward') + fcluster(Z, K, 'maxclust') for K = 1..kmax-1,
+ * kmax = min(max_c + 1, n_reads) (ReadsCluster.py:243 linkage, :94 fcluster;
+ * third-party scipy 1.15 restated on the host, parity-tested against it).
+ * S: n_reads x n_reads per window at S + s_off[w]; labels written at
+ * labels + wins[w].label_off, (kmax-1) rows of n_reads.  Host-only: no context. */
+int svs_ward_maxclust_batch(int32_t n_windows, const svs_em_window* wins, const double* S, const int64_t* s_off,
+                            int32_t max_c, int32_t* labels);
+/* Whole EMCluster (ReadsCluster.py:221-277) for a batch: similarity kernel ->
+ * ward/maxclust initial labels on the host thread pool -> EM kernel.
+ * wins[w].label_off is ignored (labels are internal). */
+int svs_em_cluster_batch(svs_context* ctx, int32_t n_windows, const svs_em_window* wins, const uint8_t* X,
+                         const svs_em_config* cfg, svs_em_result** out);
 int svs_em_result_get(const svs_em_result* r, int32_t window, int32_t field, const void** data, int64_t* count);
 void svs_em_result_free(svs_em_result* r);
 /* Host-only: numpy legacy RandomState(seed).standard_exponential(n), bitwise. */

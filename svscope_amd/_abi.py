@@ -98,6 +98,11 @@ def _declare_em(lib):
     lib.svs_em_batch.argtypes = [P, I32, ctypes.POINTER(EmWindow), P, P, ctypes.POINTER(EmConfig),
                                  ctypes.POINTER(ctypes.c_void_p)]
     lib.svs_em_batch.restype = ctypes.c_int
+    lib.svs_ward_maxclust_batch.argtypes = [I32, ctypes.POINTER(EmWindow), P, P, I32, P]
+    lib.svs_ward_maxclust_batch.restype = ctypes.c_int
+    lib.svs_em_cluster_batch.argtypes = [P, I32, ctypes.POINTER(EmWindow), P, ctypes.POINTER(EmConfig),
+                                         ctypes.POINTER(ctypes.c_void_p)]
+    lib.svs_em_cluster_batch.restype = ctypes.c_int
     lib.svs_em_result_get.argtypes = [P, I32, I32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64)]
     lib.svs_em_result_get.restype = ctypes.c_int
     lib.svs_em_result_free.argtypes = [P]

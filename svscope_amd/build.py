@@ -25,6 +25,7 @@ SOURCES = [
     "em_kernels.hip",
     "poa_graph.cpp",
     "svs_threadpool.cpp",
+    "ward.cpp",
     "svs_poa_engine.cpp",
     "svs_em_engine.cpp",
     "svs_abi.cpp",

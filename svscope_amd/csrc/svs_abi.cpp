@@ -13,6 +13,7 @@
 #include "svs_context.hpp"
 #include "svs_device.hpp"
 #include "svs_internal.hpp"
+#include "ward.hpp"
 
 struct svs_poa_result {
   std::vector<std::string> consensus;
@@ -209,6 +210,40 @@ int svs_em_batch(svs_context* ctx, int32_t n_windows, const svs_em_window* wins,
   const int rc = guarded([&] {
     SVS_HIP(hipSetDevice(ctx->device));
     res = svs::run_em(ctx, n_windows, wins, X, labels, *cfg);
+  });
+  if (rc == SVS_OK) *out = res;
+  return rc;
+}
+
+int svs_ward_maxclust_batch(int32_t n_windows, const svs_em_window* wins, const double* S, const int64_t* s_off,
+                            int32_t max_c, int32_t* labels) {
+  if (n_windows < 0 || (n_windows > 0 && (!wins || !S || !s_off || !labels)) || max_c < 1)
+    return fail(SVS_E_INVALID, "svs_ward_maxclust_batch: invalid argument");
+  for (int32_t w = 0; w < n_windows; ++w)
+    if (wins[w].n_reads < 1 || s_off[w] < 0 || wins[w].label_off < 0)
+      return fail(SVS_E_INVALID, "svs_ward_maxclust_batch: window " + std::to_string(w) + " is malformed");
+  return guarded([&] {
+    std::vector<svs::WardMerge> Z;
+    for (int32_t w = 0; w < n_windows; ++w) {
+      const int n = wins[w].n_reads;
+      svs::ward_linkage(S + s_off[w], n, &Z);
+      svs::maxclust_labels(Z, n, std::min(max_c + 1, n), labels + wins[w].label_off);
+    }
+  });
+}
+
+int svs_em_cluster_batch(svs_context* ctx, int32_t n_windows, const svs_em_window* wins, const uint8_t* X,
+                         const svs_em_config* cfg, svs_em_result** out) {
+  if (!ctx || !cfg || !out) return fail(SVS_E_INVALID, "svs_em_cluster_batch: invalid argument");
+  *out = nullptr;
+  std::string err;
+  const int v = svs::em_validate(n_windows, wins, X, &err);
+  if (v != SVS_OK) return fail(v, "svs_em_cluster_batch: " + err);
+  if (cfg->max_c < 1) return fail(SVS_E_INVALID, "svs_em_cluster_batch: max_c must be >= 1");
+  svs_em_result* res = nullptr;
+  const int rc = guarded([&] {
+    SVS_HIP(hipSetDevice(ctx->device));
+    res = svs::run_em_cluster(ctx, n_windows, wins, X, *cfg);
   });
   if (rc == SVS_OK) *out = res;
   return rc;

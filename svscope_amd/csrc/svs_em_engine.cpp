@@ -18,6 +18,9 @@
 #include "../../include/svscope.h"
 #include "svs_context.hpp"
 #include "svs_em_device.hpp"
+#include "svs_internal.hpp"
+#include "threadpool.hpp"
+#include "ward.hpp"
 
 struct svs_em_result {
   struct Win {
@@ -279,3 +282,32 @@ int svs_em_result_get(const svs_em_result* r, int32_t window, int32_t field, con
 void svs_em_result_free(svs_em_result* r) { delete r; }
 
 }  // extern "C"
+
+namespace svs {
+
+svs_em_result* run_em_cluster(svs_context* ctx, int32_t n, const svs_em_window* wins, const uint8_t* X,
+                              const svs_em_config& cfg) {
+  std::vector<svs_em_window> W(wins, wins + n);
+  std::vector<int64_t> s_off(n);
+  int64_t s_tot = 0, l_tot = 0;
+  for (int32_t w = 0; w < n; ++w) {
+    const int64_t r = W[w].n_reads;
+    s_off[w] = s_tot;
+    s_tot += r * r;
+    W[w].label_off = l_tot;
+    l_tot += (std::min<int64_t>(cfg.max_c + 1, r) - 1) * r;
+  }
+  std::vector<double> S(static_cast<size_t>(std::max<int64_t>(1, s_tot)));
+  std::vector<int32_t> labels(static_cast<size_t>(std::max<int64_t>(1, l_tot)));
+  if (n > 0) run_similarity(ctx, n, W.data(), X, S.data(), s_off.data());
+  // ward + maxclust per window on the pool (ReadsCluster.py:243, :94)
+  ctx->pool->parallel_for(static_cast<size_t>(n), [&](size_t w) {
+    thread_local std::vector<WardMerge> Z;
+    const int r = W[w].n_reads;
+    ward_linkage(S.data() + s_off[w], r, &Z);
+    maxclust_labels(Z, r, std::min(cfg.max_c + 1, r), labels.data() + W[w].label_off);
+  });
+  return run_em(ctx, n, W.data(), X, labels.data(), cfg);
+}
+
+}  // namespace svs

@@ -25,5 +25,7 @@ void run_similarity(svs_context* ctx, int32_t n, const svs_em_window* wins, cons
                     const int64_t* s_off);
 svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, const uint8_t* X,
                       const int32_t* labels, const svs_em_config& cfg);
+svs_em_result* run_em_cluster(svs_context* ctx, int32_t n, const svs_em_window* wins, const uint8_t* X,
+                              const svs_em_config& cfg);
 
 }  // namespace svs

@@ -11,6 +11,8 @@ signature, gate, labelling and record format of
 batched GPU POA for all window MSAs, one batched GPU EM, and one batched GPU
 POA for all cluster consensus sequences.
 """
+import time
+
 import numpy as np
 
 from .data_scanner import SeqDecoder, msa_feature_selection_batch
@@ -25,6 +27,8 @@ def _tag(read_id):
 def DecisionBatch(windows, Tlabel="tumor", readcutoff=3, hcutoff=3, scutoff=0.05, context=None, stats=None):
     """windows: list of (TDRecord, sequenceList, ReadIDs, flank_5, flank_3[, windowFlag]).
     Returns the list of 10-field records, in input order."""
+    t_start = time.perf_counter()
+    phase = {}
     records = []
     gated = []
     for w, win in enumerate(windows):
@@ -40,10 +44,15 @@ def DecisionBatch(windows, Tlabel="tumor", readcutoff=3, hcutoff=3, scutoff=0.05
             gated.append(w)
     if not gated:
         return records
+    t0 = time.perf_counter()
     feats = msa_feature_selection_batch([(windows[w][1], windows[w][3], windows[w][4], np.asarray(windows[w][2]))
                                          for w in gated], hcutoff, scutoff, context=context, stats=stats)
+    phase["msa_and_features_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
     em_idx = [k for k, (_, feat, _) in enumerate(feats) if feat.shape[0] != 0 and feat.shape[1] >= 10]
-    ems = em_cluster_batch([feats[k][1] for k in em_idx], context=context) if em_idx else []
+    ems = em_cluster_batch([feats[k][1] for k in em_idx], context=context, timing=phase) if em_idx else []
+    phase["em_total_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
     # cluster labelling (ascending label order, DecisionMaker.py:145-154)
     plans = []
     jobs = []
@@ -69,6 +78,8 @@ def DecisionBatch(windows, Tlabel="tumor", readcutoff=3, hcutoff=3, scutoff=0.05
                 else:
                     entry[kind + "_job"].append(None)
         plans.append(entry)
+    phase["labelling_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
     cons = []
     if jobs:
         res = poa_batch(jobs, algorithm=1, genmsa=False, context=context, return_stats=stats is not None)
@@ -76,6 +87,7 @@ def DecisionBatch(windows, Tlabel="tumor", readcutoff=3, hcutoff=3, scutoff=0.05
             res, st = res
             stats.append(("consensus_poa", st))
         cons = [c for c, _ in res]
+    phase["consensus_s"] = time.perf_counter() - t0
     for p in plans:
         som_seq = [cons[j] if j is not None else "-" for j in p["som_job"]]
         germ_seq = [cons[j] if j is not None else "-" for j in p["germ_job"]]
@@ -88,6 +100,9 @@ def DecisionBatch(windows, Tlabel="tumor", readcutoff=3, hcutoff=3, scutoff=0.05
             r[7] = ";".join(",".join(list(p["ids"][i])) for i in p["germ"])
             r[8] = len(germ_seq)
             r[9] = r[9] + "|EMOutput"
+    if stats is not None:
+        phase["decision_total_s"] = time.perf_counter() - t_start
+        stats.append(("phases", phase))
     return records
 
 

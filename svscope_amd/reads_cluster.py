@@ -6,17 +6,18 @@
 
 Pipeline per batch of windows:
   1. read similarity S (pariwiseDistance, :52-59)           -> HIP kernel
-  2. scipy ward linkage(S) + fcluster(K, 'maxclust') (:243, :94) -> host
-     (third-party scipy, kept exactly as the reference uses it)
+  2. scipy ward linkage(S) + fcluster(K, 'maxclust') (:243, :94) -> host C++
+     restatement on the engine thread pool (csrc/ward.cpp; bit-exact vs scipy,
+     tests/test_ward_host.py)
   3. EM for K = 1..Kmax-1, BIC, K=1->2 rule, argmax (:246-277) -> HIP kernel
 Only ``initselection=1`` (the value the reference uses) is implemented.
 RNG contract: each window starts from numpy's RandomState(2023) stream
 (SURVEY.md §8(a15)); the per-window stream offset consumed is reported.
 """
 import ctypes
+import time
 
 import numpy as np
-from scipy.cluster.hierarchy import fcluster, linkage
 
 from . import _abi
 
@@ -64,13 +65,7 @@ def similarity_batch(mats, context=None):
     return [S[s_off[w]:s_off[w] + X.shape[0] ** 2].reshape(X.shape[0], X.shape[0]) for w, X in enumerate(mats)]
 
 
-def ward_labels(S, kmax):
-    """fcluster(linkage(S, 'ward'), K, 'maxclust') for K = 1..kmax-1 (ReadsCluster.py:243, :94)."""
-    Z = linkage(S, "ward")
-    return np.stack([fcluster(Z, K, criterion="maxclust") for K in range(1, kmax)]).astype(np.int32)
-
-
-def em_cluster_batch(mats, max_C=9, n_step=20, seed=2023, want_params=False, context=None):
+def em_cluster_batch(mats, max_C=9, n_step=20, seed=2023, want_params=False, context=None, timing=None):
     """Batched EMCluster.  Returns one dict per matrix:
     K, Rclust, BICList, lik (+ gamma, pi, theta when want_params)."""
     ctx = context or _abi.default_context()
@@ -82,25 +77,14 @@ def em_cluster_batch(mats, max_C=9, n_step=20, seed=2023, want_params=False, con
             raise ValueError("seqdatamx symbols must be 0..4 (DataScanner.SeqEncoder)")
     if not mats:
         return []
-    sims = similarity_batch(mats, context=ctx)
-    labels = []
-    label_off = []
-    off = 0
-    for X, S in zip(mats, sims):
-        kmax = min(max_C + 1, X.shape[0])
-        lab = ward_labels(S, kmax)
-        labels.append(lab.reshape(-1))
-        label_off.append(off)
-        off += lab.size
-    lab_blob = np.concatenate(labels).astype(np.int32)
+    t0 = time.perf_counter()
     wins, blob = _pack_matrices(mats)
-    for w in range(len(mats)):
-        wins[w].label_off = label_off[w]
     cfg = EmConfigStruct(int(max_C), int(n_step), int(seed), 1 if want_params else 0, 1e-10)
     res = ctypes.c_void_p()
-    _abi.check(ctx.lib.svs_em_batch(ctx.handle, len(mats), wins,
-                                    blob.ctypes.data_as(ctypes.c_void_p), lab_blob.ctypes.data_as(ctypes.c_void_p),
-                                    ctypes.byref(cfg), ctypes.byref(res)), "svs_em_batch")
+    _abi.check(ctx.lib.svs_em_cluster_batch(ctx.handle, len(mats), wins, blob.ctypes.data_as(ctypes.c_void_p),
+                                            ctypes.byref(cfg), ctypes.byref(res)), "svs_em_cluster_batch")
+    if timing is not None:
+        timing["em_cluster_call_s"] = time.perf_counter() - t0
     out = []
     try:
         ptr = ctypes.c_void_p()

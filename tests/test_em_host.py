@@ -17,9 +17,9 @@ def test_rng_table_is_numpy_legacy_bitwise():
 
 
 def test_ward_labels_shape():
-    from svscope_amd.reads_cluster import ward_labels
+    from test_ward_host import engine_labels
     from oracle.em_oracle import similarity
     rs = np.random.RandomState(0)
     X = rs.randint(0, 5, size=(12, 30))
-    lab = ward_labels(similarity(X), 10)
+    lab = engine_labels([similarity(X)])[0]
     assert lab.shape == (9, 12) and lab.min() >= 1 and (lab[0] == 1).all()
