@@ -131,7 +131,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    poa_stats = [st for name, st in stats if name in ("msa_poa", "consensus_poa")]
+    poa_stats = [st for name, st in stats if name in ("msa_poa", "consensus_poa", "decision_poa")]
     cells = sum(st["dp_cells"] for st in poa_stats)
     kms = sum(st["kernel_ms"] for st in poa_stats)
     launches = sum(st["launches"] for st in poa_stats)

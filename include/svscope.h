@@ -131,6 +131,75 @@ void svs_em_result_free(svs_em_result* r);
 /* Host-only: numpy legacy RandomState(seed).standard_exponential(n), bitwise. */
 int svs_rng_exponential_table(uint32_t seed, int64_t n, double* out);
 
+/* ---------------------------------------------------------------- Decision
+ * The whole per-window decision (DecisionMaker.Decision, DecisionMaker.py:134-191)
+ * for a batch of gated windows, pipelined on one device:
+ *   window MSA POA (DataScanner.py:206/213) -> MSAFeatureSelection (:181-220,
+ *   host) -> EMCluster (ReadsCluster.py:221-277, GPU, in batches on its own
+ *   stream) -> cluster labelling (DecisionMaker.py:145-154, host) -> consensus
+ *   POA per reported cluster (:155-176).
+ * The POA stages share one continuous-batching scheduler, so consensus jobs of
+ * early windows fill the GPU next to MSA jobs of later ones.  The caller does
+ * the gate (:134) and formats the record (:178-190) from the returned read-id
+ * indices and consensus strings. */
+typedef struct svs_decision_window {
+  int32_t n_seqs;      /* len(sequenceList): reference window sequence + reads */
+  int32_t n_ids;       /* len(ReadIDs) */
+  int64_t seq_start;   /* index of sequenceList[0] in seq_byte_start */
+  int64_t flank5_off;  /* flank_5 = text[flank5_off : flank5_off + flank5_len] */
+  int64_t flank3_off;
+  int32_t flank5_len;
+  int32_t flank3_len;
+  int64_t tag_off;     /* is_tlabel[tag_off + i] = 1 iff ReadIDs[i]'s tag == Tlabel */
+} svs_decision_window;
+
+typedef struct svs_decision_config {
+  int32_t readcutoff;  /* 3 */
+  int32_t hcutoff;     /* 3 */
+  double scutoff;      /* 0.05 */
+  svs_poa_config poa;  /* poa(seqs, 1) defaults; genmsa ignored */
+  svs_em_config em;    /* EMCluster defaults: max_c 9, n_step 20, seed 2023 */
+  int32_t em_batch;    /* windows per EM launch while MSAs are still running (0: 512) */
+  int32_t reserved;
+} svs_decision_config;
+
+typedef struct svs_decision_stats {
+  svs_poa_stats poa;   /* MSA + consensus POA together */
+  double wall_ms, features_ms, labelling_ms, em_wall_ms, em_kernel_ms;
+  int64_t msa_tasks, consensus_tasks, em_windows, em_launches;
+} svs_decision_stats;
+
+typedef struct svs_decision_result svs_decision_result;
+
+/* Window status values */
+#define SVS_DEC_NO_EM 0       /* seqdatamx has < 10 feature columns: default record */
+#define SVS_DEC_EM 1          /* EM ran, no somatic + germline pair: default record */
+#define SVS_DEC_EMOUTPUT 2    /* record with clusters, flag + "|EMOutput" */
+#define SVS_DEC_INDEX_ERROR 3 /* a label row has no read id: the reference raises IndexError */
+
+int svs_decision_batch(svs_context* ctx, int32_t n_windows, const svs_decision_window* wins,
+                       const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
+                       const uint8_t* is_tlabel, const svs_decision_config* cfg, svs_decision_result** out);
+int svs_decision_result_window(const svs_decision_result* r, int32_t window, int32_t* status, int32_t* K,
+                               int32_t* n_som, int32_t* n_germ);
+/* cluster c of a window: somatic clusters first (c < n_som), then germline;
+ * ids = ReadIDs indices of the cluster's reads, cons = its consensus ("-" when
+ * every read of the cluster is empty). */
+int svs_decision_result_cluster(const svs_decision_result* r, int32_t window, int32_t cluster,
+                                const int32_t** ids, int32_t* n_ids, const char** cons, int64_t* cons_len);
+int svs_decision_result_stats(const svs_decision_result* r, svs_decision_stats* out);
+void svs_decision_result_free(svs_decision_result* r);
+
+/* Host-only MSAFeatureSelection after the MSA (DataScanner.py:181-220) for
+ * tests: msa = n_rows x width bytes; read_lens = len(sequenceList[1:]).
+ * Writes seqdatamx (rows x n_feat) into feat (capacity feat_cap bytes) and the
+ * returned readIDList as ReadIDs indices into id_map (capacity id_cap).
+ * On SVS_E_INVALID with *rows >= 0 the capacities were too small. */
+int svs_msa_features(int32_t n_rows, int32_t width, const char* msa, const char* flank5, int32_t flank5_len,
+                     const char* flank3, int32_t flank3_len, int32_t n_reads, const int32_t* read_lens,
+                     int32_t n_ids, int32_t hcutoff, double scutoff, int32_t* rows, int32_t* n_feat,
+                     uint8_t* feat, int64_t feat_cap, int32_t* id_map, int32_t* n_map, int64_t id_cap);
+
 /* Wave-primitive self test (GPU tests): per 64-lane wave, inclusive prefix max
  * and shift-right-by-one (lane 0 <- -7). */
 int svs_wave_selftest(svs_context* ctx, const int32_t* in, int32_t* scan, int32_t* shift,

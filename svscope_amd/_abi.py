@@ -45,6 +45,31 @@ class PoaStats(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class DecisionWindow(ctypes.Structure):
+    _fields_ = [("n_seqs", ctypes.c_int32), ("n_ids", ctypes.c_int32), ("seq_start", ctypes.c_int64),
+                ("flank5_off", ctypes.c_int64), ("flank3_off", ctypes.c_int64), ("flank5_len", ctypes.c_int32),
+                ("flank3_len", ctypes.c_int32), ("tag_off", ctypes.c_int64)]
+
+
+class DecisionConfig(ctypes.Structure):
+    _fields_ = [("readcutoff", ctypes.c_int32), ("hcutoff", ctypes.c_int32), ("scutoff", ctypes.c_double),
+                ("poa", PoaConfig), ("em", EmConfig), ("em_batch", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class DecisionStats(ctypes.Structure):
+    _fields_ = [("poa", PoaStats), ("wall_ms", ctypes.c_double), ("features_ms", ctypes.c_double),
+                ("labelling_ms", ctypes.c_double), ("em_wall_ms", ctypes.c_double), ("em_kernel_ms", ctypes.c_double),
+                ("msa_tasks", ctypes.c_int64), ("consensus_tasks", ctypes.c_int64), ("em_windows", ctypes.c_int64),
+                ("em_launches", ctypes.c_int64)]
+
+    def as_dict(self):
+        d = {name: getattr(self, name) for name, _ in self._fields_ if name != "poa"}
+        d["poa"] = self.poa.as_dict()
+        return d
+
+
+DEC_NO_EM, DEC_EM, DEC_EMOUTPUT, DEC_INDEX_ERROR = 0, 1, 2, 3
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -103,6 +128,22 @@ def _declare_em(lib):
     lib.svs_em_cluster_batch.argtypes = [P, I32, ctypes.POINTER(EmWindow), P, ctypes.POINTER(EmConfig),
                                          ctypes.POINTER(ctypes.c_void_p)]
     lib.svs_em_cluster_batch.restype = ctypes.c_int
+    lib.svs_decision_batch.argtypes = [P, I32, ctypes.POINTER(DecisionWindow), P, P, P, P,
+                                       ctypes.POINTER(DecisionConfig), ctypes.POINTER(ctypes.c_void_p)]
+    lib.svs_decision_batch.restype = ctypes.c_int
+    PI32 = ctypes.POINTER(ctypes.c_int32)
+    lib.svs_decision_result_window.argtypes = [P, I32, PI32, PI32, PI32, PI32]
+    lib.svs_decision_result_window.restype = ctypes.c_int
+    lib.svs_decision_result_cluster.argtypes = [P, I32, I32, ctypes.POINTER(PI32), PI32,
+                                                ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64)]
+    lib.svs_decision_result_cluster.restype = ctypes.c_int
+    lib.svs_decision_result_stats.argtypes = [P, ctypes.POINTER(DecisionStats)]
+    lib.svs_decision_result_stats.restype = ctypes.c_int
+    lib.svs_decision_result_free.argtypes = [P]
+    lib.svs_decision_result_free.restype = None
+    lib.svs_msa_features.argtypes = [I32, I32, P, P, I32, P, I32, I32, P, I32, I32, ctypes.c_double, PI32, PI32,
+                                     P, ctypes.c_int64, P, PI32, ctypes.c_int64]
+    lib.svs_msa_features.restype = ctypes.c_int
     lib.svs_em_result_get.argtypes = [P, I32, I32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64)]
     lib.svs_em_result_get.restype = ctypes.c_int
     lib.svs_em_result_free.argtypes = [P]

@@ -22,10 +22,13 @@ ARCH = os.environ.get("SVS_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [
     "poa_kernels.hip",
+    "poa_strip.hip",
     "em_kernels.hip",
     "poa_graph.cpp",
     "svs_threadpool.cpp",
     "ward.cpp",
+    "features.cpp",
+    "svs_decision.cpp",
     "svs_poa_engine.cpp",
     "svs_em_engine.cpp",
     "svs_abi.cpp",

@@ -216,8 +216,68 @@ void PoaGraph::export_rows(RowTables* t) const {
   t->n_slots = next;
 }
 
+void PoaGraph::export_strip_rows(RowTables* t) const {
+  const uint32_t V = num_nodes();
+  t->info.clear();
+  t->slot.clear();
+  t->pstart.resize(V + 1);
+  t->pred_row.clear();
+  t->max_preds = 0;
+  t->rec.assign(static_cast<size_t>(V) * kRecWords, 0);
+  static thread_local std::vector<uint32_t> lds_last, slot;
+  static thread_local std::vector<uint32_t> free_slots;
+  lds_last.assign(V, 0);
+  slot.assign(V, kNoSlot);
+  free_slots.clear();
+  uint32_t np_total = 0;
+  for (uint32_t r = 0; r < V; ++r) {
+    const uint32_t node = rank_to_node_[r];
+    t->pstart[r] = np_total;
+    for (uint32_t e : in_[node]) {
+      const uint32_t pr = node_to_rank_[e_tail_[e]];
+      t->pred_row.push_back(pr + 1);
+      if (pr + 1 != r) lds_last[pr] = std::max(lds_last[pr], r + 1);  // read through the pool
+      ++np_total;
+    }
+    t->max_preds = std::max<uint32_t>(t->max_preds, static_cast<uint32_t>(in_[node].size()));
+  }
+  t->pstart[V] = np_total;
+  t->pred_slot.assign(np_total, kNoSlot);
+  uint32_t next = 1;  // slot 0: virtual row 0
+  for (uint32_t r = 0; r < V; ++r) {
+    const uint32_t node = rank_to_node_[r];
+    const bool store = lds_last[r] != 0;
+    if (store) {
+      if (free_slots.empty()) {
+        slot[r] = next++;
+      } else {
+        slot[r] = free_slots.back();
+        free_slots.pop_back();
+      }
+    }
+    const uint32_t a = t->pstart[r], b = t->pstart[r + 1];
+    uint32_t* w = t->rec.data() + static_cast<size_t>(r) * kRecWords;
+    w[0] = static_cast<uint8_t>(base_[node]) | (out_[node].empty() ? 0x100u : 0u) | (store ? 0x200u : 0u) |
+           ((b - a) << 10);
+    w[1] = store ? slot[r] : kNoSlot;
+    if (a == b) w[2] = 0;  // source: in-edge from the virtual row 0 (slot 0)
+    for (uint32_t k = a; k < b; ++k) {
+      const uint32_t pr = t->pred_row[k] - 1;
+      const uint32_t ps = (pr + 1 == r) ? kNoSlot : slot[pr];
+      t->pred_slot[k] = ps;
+      const uint32_t i = k - a;
+      if (i < kInlinePreds) w[2 + i / 2] |= ps << (16 * (i & 1));
+    }
+    for (uint32_t k = a; k < b; ++k) {
+      const uint32_t pr = t->pred_row[k] - 1;
+      if (pr + 1 != r && lds_last[pr] == r + 1) free_slots.push_back(slot[pr]);
+    }
+  }
+  t->n_slots = next;
+}
+
 void fill_col0(RowTables* t, int32_t g, int32_t e, int32_t q, int32_t c) {
-  const size_t V = t->info.size();
+  const size_t V = t->pstart.empty() ? 0 : t->pstart.size() - 1;
   t->col0.resize(3 * V);
   for (size_t r = 0; r < V; ++r) {
     int32_t F0, O0;

@@ -25,7 +25,18 @@ struct RowTables {
   std::vector<int32_t> col0;        // per rank row: H, F, O of DP column 0 (fill_col0)
   uint32_t n_slots = 1;
   uint32_t max_preds = 0;
+  // Strip-kernel tables (export_strip_rows): kRecWords words per row
+  //   w0: base | sink << 8 | store << 9 | np << 10
+  //   w1: own pool slot (kNoSlot: not stored)
+  //   w2, w3: 16-bit pool slots of the first kInlinePreds in-edges, kNoSlot =
+  //         "the row just above" (kept in registers); further in-edges are in
+  //         pred_slot[pstart[r] + k]
+  std::vector<uint32_t> rec;
 };
+
+constexpr uint32_t kRecWords = 4;
+constexpr uint32_t kInlinePreds = 4;
+constexpr uint32_t kNoSlot = 0xFFFF;
 
 // Column 0 of the NW matrix depends only on the graph (gap runs down the
 // in-edges, spoa Initialize): F0 = max_p F0[p] + e (g for sources), O0 likewise
@@ -46,6 +57,11 @@ class PoaGraph {
                            const std::string& seq);
 
   void export_rows(RowTables* t) const;
+  // Tables for the strip-major kernel: a row is stored in the pool only if a
+  // successor other than the next row reads it; an in-edge from the row just
+  // above is served from registers.  Fills rec, pstart, pred_row, pred_slot,
+  // n_slots, max_preds (info/slot are left empty).
+  void export_strip_rows(RowTables* t) const;
   std::vector<std::string> msa() const;
   std::string consensus(int32_t min_coverage);
 

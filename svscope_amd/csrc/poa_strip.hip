@@ -1,0 +1,296 @@
+// MI355X (gfx950) POA alignment kernel, strip-major: Needleman-Wunsch of one
+// read against a partial-order graph with spoa's convex gap model, plus the
+// traceback, for a batch of independent (graph, read) jobs.
+//
+// Replaces the DP + backtrack of spoa's SisdAlignmentEngine (kNW, convex)
+// reached by the reference through `poa(seqs, 1)` at
+// /root/reference/src/DataScanner.py:206,213 and DecisionMaker.py:160,171.
+//
+// Mapping (one 64-lane wave = one job = one workgroup):
+//  * the DP matrix is swept strip by strip: strip s = columns 64s .. 64s+63,
+//    lane l owning column 64s + l; within a strip all graph rows are visited in
+//    rank order;
+//  * the row pool (H, F, O of rows that a later, non-adjacent row still reads)
+//    only spans the current strip, so it lives in LDS: n_slots x 768 B per
+//    wave (config-3 windows need <= 13 slots); an in-edge from the row just
+//    above is served from registers and that row is not stored at all when no
+//    other row reads it (export_strip_rows plans slots and liveness);
+//  * the only state carried from strip s-1 to strip s is per row: the two
+//    scan carries, Hpre and H at the strip's last column (16 B), written once
+//    by lane 0 and read back as a uniform load one strip later, prefetched two
+//    rows ahead; row records (32 B) are prefetched the same way;
+//  * per cell only the 16-bit traceback code goes to HBM (coalesced 128 B per
+//    strip row); the backtrack is the same lane-0 replay of spoa's order as in
+//    the row-major kernel (poa_wave.hpp).
+// HBM traffic per DP cell: 2 B traceback + ~0.5 B carries (vs ~25 B for the
+// row-major kernel's global pool), and no global load on the row-to-row
+// dependency chain.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <type_traits>
+
+#include "poa_graph.hpp"
+#include "poa_wave.hpp"
+#include "svs_device.hpp"
+
+namespace svs {
+
+namespace {
+
+constexpr int kSlotInts = 3 * 64;  // H, F, O planes of one pool slot
+
+// Prefetched inputs of one row: its record and its carries into this strip
+// (strip 0: column-0 values H0, F0, O0 from fill_col0).
+struct RowIn {
+  uint32_t w0, w1, w2, w3;
+  int32_t b0, b1, b2, b3;
+};
+
+__device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, const uint32_t* __restrict__ spill) {
+  if (k >= kInlinePreds) return spill[k];
+  const uint32_t w = k < 2 ? d.w2 : d.w3;
+  return (w >> (16 * (k & 1))) & 0xFFFFu;
+}
+
+}  // namespace
+
+template <bool LDSP>
+__global__ __launch_bounds__(64) void poa_strip_kernel(
+    const PoaJob* __restrict__ jobs, int n_jobs, PoaScore P, const uint32_t* __restrict__ rec_all,
+    const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
+    const uint32_t* __restrict__ pred_slot, const int32_t* __restrict__ col0, const uint8_t* __restrict__ seqs,
+    uint16_t* __restrict__ tb, int32_t* __restrict__ bnd_all, int32_t* __restrict__ gpool,
+    int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
+  extern __shared__ int32_t lds[];
+  const int lane = threadIdx.x;
+  const int job_id = blockIdx.x;
+  if (job_id >= n_jobs) return;
+  const PoaJob J = jobs[job_id];
+  const int32_t L = static_cast<int32_t>(J.len);
+  const uint32_t LS = J.ls;
+  const uint32_t V = J.n_rows;
+  const int32_t nstrips = static_cast<int32_t>(LS >> 6);
+  int32_t* __restrict__ pool;
+  if constexpr (LDSP) pool = lds;
+  else pool = gpool + J.pool_off;
+  int32_t* __restrict__ slot_ch = pool + (LDSP ? lds_slots : J.n_slots) * kSlotInts;  // per slot: H at column j0-1
+  uint16_t* __restrict__ tbj = tb + J.tb_off;
+  const uint32_t* __restrict__ rec = rec_all + static_cast<uint64_t>(J.rec_off) * kRecWords;
+  const uint32_t* __restrict__ rps = row_pstart + J.pstart_off;
+  const uint32_t* __restrict__ prow = pred_row + J.pred_off;
+  const uint32_t* __restrict__ pslot = pred_slot + J.pred_off;
+  const int32_t* __restrict__ rc0 = col0 + 3ull * J.row_off;
+  const uint8_t* __restrict__ seq = seqs + J.seq_off;
+  int32_t* __restrict__ bnd = bnd_all + J.bnd_off;
+
+  int32_t best = SVS_NEG_INF;  // meaningful on the lane owning column L
+  int32_t best_row = 0;
+
+  auto sweep = [&](auto first_tag, int32_t s) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    const int32_t j0 = s << 6;
+    const int32_t j = j0 + lane;
+    const uint8_t rc = seq[j - 1];  // seqs[seq_off - 1] is a zero pad byte (column 0)
+    const int32_t* __restrict__ bin = bnd + static_cast<uint64_t>((s + 1) & 1) * V * 4;
+    int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s & 1) * V * 4;
+    const bool write_bnd = s + 1 < nstrips;
+    // virtual row 0 in slot 0
+    pool[lane] = row0_h(P, j);
+    pool[64 + lane] = j == 0 ? 0 : SVS_NEG_INF;
+    pool[128 + lane] = j == 0 ? 0 : SVS_NEG_INF;
+    if (lane == 0) slot_ch[0] = FIRST ? 0 : row0_h(P, j0 - 1);
+    __builtin_amdgcn_wave_barrier();
+
+    auto fetch = [&](RowIn& d, uint32_t r) {
+      const uint32_t rr = r < V ? r : V - 1;
+      const uint32_t* w = rec + static_cast<uint64_t>(rr) * kRecWords;
+      d.w0 = w[0]; d.w1 = w[1]; d.w2 = w[2]; d.w3 = w[3];
+      if (FIRST) {
+        d.b0 = rc0[3 * rr];
+        d.b1 = rc0[3 * rr + 1];
+        d.b2 = rc0[3 * rr + 2];
+        d.b3 = 0;
+      } else {
+        const int4 v = *reinterpret_cast<const int4*>(bin + 4ull * rr);
+        d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
+      }
+    };
+
+    int32_t pH = 0, pF = 0, pO = 0, pcH = 0;  // the row just above (registers)
+    auto step = [&](uint32_t r, const RowIn& d) {
+      const uint32_t w0 = __builtin_amdgcn_readfirstlane(d.w0);
+      const uint32_t nb = w0 & 0xFFu;
+      const bool sink = (w0 >> 8) & 1u;
+      const bool store = (w0 >> 9) & 1u;
+      const uint32_t np = (w0 >> 10) & 31u;
+      const uint32_t own = __builtin_amdgcn_readfirstlane(d.w1) & 0xFFFFu;
+      int32_t H0 = 0, F0 = 0, O0 = 0;
+      StripCarry cr;
+      if (FIRST) {
+        H0 = __builtin_amdgcn_readfirstlane(d.b0);
+        F0 = __builtin_amdgcn_readfirstlane(d.b1);
+        O0 = __builtin_amdgcn_readfirstlane(d.b2);
+        cr = StripCarry{SVS_VNEG, SVS_VNEG, H0, SVS_NEG_INF, SVS_NEG_INF, H0};
+      } else {
+        const int32_t jl = j0 - 1;
+        cr.run1 = __builtin_amdgcn_readfirstlane(d.b0);
+        cr.run2 = __builtin_amdgcn_readfirstlane(d.b1);
+        cr.cHpre = __builtin_amdgcn_readfirstlane(d.b2);
+        cr.cH = __builtin_amdgcn_readfirstlane(d.b3);
+        cr.cQ = jl * P.c + cr.run1;
+        cr.cE = jl * P.e + cr.run2;
+      }
+      const int32_t cH_in = cr.cH;  // H[r][j0 - 1]: the diagonal fill successors need
+      const bool c0 = FIRST && lane == 0;
+      const bool inner = FIRST ? (lane != 0 && j <= L) : true;
+      const int32_t mc = rc == nb ? P.m : P.n;
+      // in-edge k: (H, F, O) at this strip and H at column j0-1
+      // (pool reads are nontemporal loads so that the compiler cannot merge them
+      // with the register case into a select of pointers, which would force the
+      // registers into scratch and every pool read onto the flat path)
+      auto pred_vals = [&](uint32_t ps, int32_t& hp, int32_t& fp, int32_t& op, int32_t& fill) {
+        const bool reg = ps == kNoSlot;
+        const int32_t fl = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(slot_ch + (reg ? 0u : ps)));
+        fill = reg ? pcH : fl;
+        if (reg) {
+          hp = pH; fp = pF; op = pO;
+        } else {
+          const int32_t* q = pool + ps * kSlotInts;
+          hp = __builtin_nontemporal_load(q + lane);
+          fp = __builtin_nontemporal_load(q + 64 + lane);
+          op = __builtin_nontemporal_load(q + 128 + lane);
+        }
+      };
+      int32_t H, F, O, Q, E, prevQ, prevE, prevH;
+      uint32_t code;
+      if (np <= 1) {
+        const uint32_t ps = __builtin_amdgcn_readfirstlane(d.w2) & 0xFFFFu;  // np == 0: slot 0 (virtual row)
+        int32_t hp, fp, op, fill;
+        pred_vals(ps, hp, fp, op, fill);
+        const int32_t hpm = wave_shr1(hp, fill, lane);
+        F = imax(hp + P.g, fp + P.e);
+        O = imax(hp + P.q, op + P.c);
+        int32_t Hpre = imax(hpm + mc, imax(F, O));
+        if (FIRST) {
+          F = c0 ? F0 : F;
+          O = c0 ? O0 : O;
+          Hpre = c0 ? H0 : Hpre;
+        }
+        strip_gaps(P, lane, j, j0, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
+        const bool dg = inner && H == hpm + mc;
+        const bool ua = H == fp + P.e, ub = H == hp + P.g, uc = H == op + P.c, ud = H == hp + P.q;
+        const bool va = F == hp + P.g, vb = F == fp + P.e, vc = O == hp + P.q, vd = O == op + P.c;
+        const bool vm = np != 0 && (va || vb || vc || vd);
+        const bool la = inner && H == prevE + P.e, lb = inner && H == prevH + P.g;
+        const bool lc = inner && H == prevQ + P.c, ld = inner && H == prevH + P.q;
+        const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
+        code = assemble_code(dg ? 0u : 31u, (ua || ub || uc || ud) ? 0u : 31u, (ua || (!ub && uc)) ? 1u : 0u,
+                             la || lb || lc || ld, la || (!lb && lc), lbit, vm ? 0u : 31u,
+                             (vm && (va || (!vb && vc))) ? 1u : 0u);
+      } else {
+        const uint32_t* __restrict__ spill = pslot + rps[r];
+        F = SVS_VNEG;
+        O = SVS_VNEG;
+        int32_t Hd = SVS_VNEG;
+        for (uint32_t k = 0; k < np; ++k) {
+          int32_t hp, fp, op, fill;
+          pred_vals(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hp, fp, op, fill);
+          const int32_t hpm = c0 ? 0 : wave_shr1(hp, fill, lane);
+          F = imax(F, imax(hp + P.g, fp + P.e));
+          O = imax(O, imax(hp + P.q, op + P.c));
+          Hd = imax(Hd, hpm + mc);
+        }
+        if (c0) { F = F0; O = O0; }
+        const int32_t Hpre = c0 ? H0 : imax(Hd, imax(F, O));
+        strip_gaps(P, lane, j, j0, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
+        uint32_t diag_k = 31, up_k = 31, up_ext = 0, uc_k = 31, uc_stop = 0;
+        for (uint32_t k = 0; k < np; ++k) {
+          int32_t hp, fp, op, fill;
+          pred_vals(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hp, fp, op, fill);
+          const int32_t hpm = c0 ? 0 : wave_shr1(hp, fill, lane);
+          if (inner && diag_k == 31 && H == hpm + mc) diag_k = k;
+          if (up_k == 31) {
+            const bool a = H == fp + P.e, b = H == hp + P.g, c = H == op + P.c, dd = H == hp + P.q;
+            if (a || b || c || dd) { up_k = k; up_ext = (a || (!b && c)) ? 1u : 0u; }
+          }
+          if (uc_k == 31) {
+            const bool a = F == hp + P.g, b = F == fp + P.e, c = O == hp + P.q, dd = O == op + P.c;
+            if (a || b || c || dd) { uc_k = k; uc_stop = (a || (!b && c)) ? 1u : 0u; }
+          }
+        }
+        const bool la = inner && H == prevE + P.e, lb = inner && H == prevH + P.g;
+        const bool lc = inner && H == prevQ + P.c, ld = inner && H == prevH + P.q;
+        const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
+        code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k, uc_stop);
+      }
+      tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+      if (store) {
+        int32_t* q = pool + own * kSlotInts;
+        q[lane] = H;
+        q[64 + lane] = F;
+        q[128 + lane] = O;
+        if (lane == 0) slot_ch[own] = cH_in;
+      }
+      pH = H;
+      pF = F;
+      pO = O;
+      pcH = cH_in;
+      if (write_bnd && lane == 0)
+        *reinterpret_cast<int4*>(bout + 4ull * r) = make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH);
+      if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
+    };
+
+    // rows in pairs with two statically named prefetch sets (no waits on
+    // loads still in flight when a set is refilled)
+    RowIn A, B;
+    fetch(A, 0);
+    fetch(B, 1);
+    for (uint32_t r = 0; r < V; r += 2) {
+      step(r, A);
+      fetch(A, r + 2);
+      if (r + 1 >= V) break;
+      step(r + 1, B);
+      fetch(B, r + 3);
+    }
+    // this strip's boundary stores must land before the next strip reads them
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  if (V > 0) {
+    using TrueT = std::integral_constant<bool, true>;
+    using FalseT = std::integral_constant<bool, false>;
+    sweep(TrueT{}, 0);
+    for (int32_t s = 1; s < nstrips; ++s) sweep(FalseT{}, s);
+  }
+
+  // make the wave's traceback-code stores visible to its own lane 0
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  best_row = __shfl(best_row, L & 63, 64);
+  if (lane != 0) return;
+  auto tbc = [&](int32_t row, int32_t col) -> uint32_t { return tbj[static_cast<uint64_t>(row - 1) * LS + col]; };
+  auto pred_of = [&](int32_t row, uint32_t k) -> int32_t {
+    const uint32_t a = rps[row - 1], b = rps[row];
+    return (b == a) ? 0 : static_cast<int32_t>(prow[a + k]);
+  };
+  aln_len[job_id] = poa_traceback(P, V, L, best_row, tbc, pred_of, aln + 2 * J.aln_off);
+}
+
+hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
+  if (a.n_jobs <= 0) return hipSuccess;
+  if (a.lds_slots > 0) {
+    const size_t lds = static_cast<size_t>(a.lds_slots) * (kStripSlotBytes + 4);
+    hipLaunchKernelGGL(poa_strip_kernel<true>, dim3(a.n_jobs), dim3(64), lds, stream, a.jobs, a.n_jobs, a.score,
+                       a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.pool, a.aln,
+                       a.aln_len, a.lds_slots);
+  } else {
+    hipLaunchKernelGGL(poa_strip_kernel<false>, dim3(a.n_jobs), dim3(64), 0, stream, a.jobs, a.n_jobs, a.score,
+                       a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.pool, a.aln,
+                       a.aln_len, 0u);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace svs

@@ -81,6 +81,7 @@ int svs_init(int device_ordinal, svs_context** out) {
     ctx = new svs_context();
     ctx->device = device_ordinal;
     SVS_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    SVS_HIP(hipStreamCreateWithFlags(&ctx->em_stream, hipStreamNonBlocking));
     SVS_HIP(hipEventCreate(&ctx->ev_start));
     SVS_HIP(hipEventCreate(&ctx->ev_stop));
     size_t free_b = 0, total_b = 0;
@@ -105,12 +106,14 @@ void svs_release(svs_context* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->em_stream) (void)hipStreamSynchronize(ctx->em_stream);
   ctx->poa_arenas.clear();
   for (svs::DeviceBuf* b : {&ctx->d_em_in, &ctx->d_em_ws, &ctx->d_em_out, &ctx->d_rng}) b->release();
   for (svs::PinnedBuf* b : {&ctx->h_em_in, &ctx->h_em_out}) b->release();
   if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
   if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->em_stream) (void)hipStreamDestroy(ctx->em_stream);
   delete ctx->pool;
   delete ctx;
 }
@@ -243,10 +246,96 @@ int svs_em_cluster_batch(svs_context* ctx, int32_t n_windows, const svs_em_windo
   svs_em_result* res = nullptr;
   const int rc = guarded([&] {
     SVS_HIP(hipSetDevice(ctx->device));
-    res = svs::run_em_cluster(ctx, n_windows, wins, X, *cfg);
+    res = svs::run_em_cluster(ctx, n_windows, wins, X, *cfg, ctx->pool);
   });
   if (rc == SVS_OK) *out = res;
   return rc;
+}
+
+int svs_decision_batch(svs_context* ctx, int32_t n_windows, const svs_decision_window* wins,
+                       const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
+                       const uint8_t* is_tlabel, const svs_decision_config* cfg, svs_decision_result** out) {
+  if (!ctx || !cfg || !out || n_windows < 0 || (n_windows > 0 && (!wins || !seq_byte_start)))
+    return fail(SVS_E_INVALID, "svs_decision_batch: invalid argument");
+  *out = nullptr;
+  for (int32_t w = 0; w < n_windows; ++w) {
+    const svs_decision_window& W = wins[w];
+    if (W.n_seqs < 1 || W.n_ids < 0 || W.seq_start < 0 || W.flank5_len < 0 || W.flank3_len < 0 || W.tag_off < 0 ||
+        ((W.flank5_len || W.flank3_len) && !text) || (W.n_ids && !is_tlabel))
+      return fail(SVS_E_INVALID, "svs_decision_batch: window " + std::to_string(w) + " is malformed");
+  }
+  if (cfg->readcutoff < 0 || cfg->em.max_c < 1 || cfg->em.n_step < 1)
+    return fail(SVS_E_INVALID, "svs_decision_batch: invalid config");
+  svs_decision_result* res = nullptr;
+  const int rc = guarded([&] {
+    SVS_HIP(hipSetDevice(ctx->device));
+    svs::check_poa_config(cfg->poa);
+    res = svs::run_decision(ctx, n_windows, wins, seq_byte_start, seq_bytes, text, is_tlabel, *cfg);
+  });
+  if (rc == SVS_OK) *out = res;
+  return rc;
+}
+
+int svs_decision_result_window(const svs_decision_result* r, int32_t window, int32_t* status, int32_t* K,
+                               int32_t* n_som, int32_t* n_germ) {
+  if (!r || window < 0 || window >= static_cast<int32_t>(r->w.size()) || !status || !K || !n_som || !n_germ)
+    return fail(SVS_E_INVALID, "svs_decision_result_window: invalid argument");
+  const auto& w = r->w[window];
+  *status = w.status;
+  *K = w.K;
+  *n_som = static_cast<int32_t>(w.som.size());
+  *n_germ = static_cast<int32_t>(w.germ.size());
+  return SVS_OK;
+}
+
+int svs_decision_result_cluster(const svs_decision_result* r, int32_t window, int32_t cluster,
+                                const int32_t** ids, int32_t* n_ids, const char** cons, int64_t* cons_len) {
+  if (!r || window < 0 || window >= static_cast<int32_t>(r->w.size()) || !ids || !n_ids || !cons || !cons_len)
+    return fail(SVS_E_INVALID, "svs_decision_result_cluster: invalid argument");
+  const auto& w = r->w[window];
+  const int32_t ns = static_cast<int32_t>(w.som.size()), ng = static_cast<int32_t>(w.germ.size());
+  if (cluster < 0 || cluster >= ns + ng) return fail(SVS_E_INVALID, "svs_decision_result_cluster: bad cluster");
+  const svs::ClusterPlan& p = cluster < ns ? w.som[cluster] : w.germ[cluster - ns];
+  *ids = p.ids.data();
+  *n_ids = static_cast<int32_t>(p.ids.size());
+  *cons = p.consensus.data();
+  *cons_len = static_cast<int64_t>(p.consensus.size());
+  return SVS_OK;
+}
+
+int svs_decision_result_stats(const svs_decision_result* r, svs_decision_stats* out) {
+  if (!r || !out) return fail(SVS_E_INVALID, "svs_decision_result_stats: invalid argument");
+  *out = r->st;
+  return SVS_OK;
+}
+
+void svs_decision_result_free(svs_decision_result* r) { delete r; }
+
+int svs_msa_features(int32_t n_rows, int32_t width, const char* msa, const char* flank5, int32_t flank5_len,
+                     const char* flank3, int32_t flank3_len, int32_t n_reads, const int32_t* read_lens,
+                     int32_t n_ids, int32_t hcutoff, double scutoff, int32_t* rows, int32_t* n_feat,
+                     uint8_t* feat, int64_t feat_cap, int32_t* id_map, int32_t* n_map, int64_t id_cap) {
+  if (n_rows < 0 || width < 0 || n_reads < 0 || n_ids < 0 || !rows || !n_feat || !n_map ||
+      (n_rows * static_cast<int64_t>(width) > 0 && !msa) || (n_reads > 0 && !read_lens) ||
+      (flank5_len > 0 && !flank5) || (flank3_len > 0 && !flank3))
+    return fail(SVS_E_INVALID, "svs_msa_features: invalid argument");
+  *rows = -1;
+  return guarded([&] {
+    std::vector<std::string> m(n_rows);
+    for (int32_t r = 0; r < n_rows; ++r) m[r].assign(msa + static_cast<int64_t>(r) * width, width);
+    std::vector<int32_t> lens(read_lens, read_lens + n_reads);
+    svs::WindowFeatures f;
+    svs::msa_feature_select(m, std::string(flank5 ? flank5 : "", flank5_len),
+                            std::string(flank3 ? flank3 : "", flank3_len), lens, n_ids, hcutoff, scutoff, &f);
+    *rows = f.rows;
+    *n_feat = f.n_feat;
+    *n_map = static_cast<int32_t>(f.id_map.size());
+    if (static_cast<int64_t>(f.feat.size()) > feat_cap || static_cast<int64_t>(f.id_map.size()) > id_cap ||
+        (!f.feat.empty() && !feat) || (!f.id_map.empty() && !id_map))
+      throw svs::SvsError(SVS_E_INVALID, "svs_msa_features: output capacity too small");
+    if (!f.feat.empty()) std::memcpy(feat, f.feat.data(), f.feat.size());
+    if (!f.id_map.empty()) std::memcpy(id_map, f.id_map.data(), 4 * f.id_map.size());
+  });
 }
 
 int svs_wave_selftest(svs_context* ctx, const int32_t* in, int32_t* scan, int32_t* shift, int32_t n_waves) {

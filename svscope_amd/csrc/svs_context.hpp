@@ -104,7 +104,8 @@ struct PoaArena {
 
 struct svs_context {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;     // POA launches (task groups alternate on it)
+  hipStream_t em_stream = nullptr;  // similarity + EM kernels, concurrent with POA
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
   svs::ThreadPool* pool = nullptr;
   size_t device_budget = 0;  // bytes usable for traceback + row pool per launch

@@ -23,6 +23,9 @@ struct PoaJob {
   uint32_t len;       // read length
   uint32_t ls;        // row stride (>= len + 1, multiple of 64)
   uint32_t n_slots;   // pool slots (slot 0 = virtual row 0)
+  uint64_t bnd_off;   // strip kernel: int32 strip-boundary carries, 2 x n_rows x 4
+  uint32_t rec_off;   // strip kernel: row records (kRecWords uint32 per row), in rows
+  uint32_t pad_;
 };
 
 struct PoaLaunch {
@@ -41,11 +44,21 @@ struct PoaLaunch {
   int32_t* aln;
   int32_t* aln_len;
   int waves_per_job;  // 1, 2 or 4 (column-chunk waves per job)
+  // strip-major kernel
+  const uint32_t* rec;   // row records (export_strip_rows)
+  int32_t* bnd;          // strip-boundary carries
+  uint32_t lds_slots;    // pool slots per wave held in LDS (max n_slots of the launch)
 };
+
+// Strip-major kernel: LDS bytes per pool slot (H, F, O planes of 64 lanes + the
+// slot's boundary H) and the largest pool kept in LDS.
+constexpr uint32_t kStripSlotBytes = 3 * 64 * 4;
+constexpr uint32_t kStripMaxLdsSlots = 80;
 
 constexpr uint32_t kPoaMaxSlotsMultiWave = 64;
 
 hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream);
+hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream);
 hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
                                 hipStream_t stream);
 

@@ -22,17 +22,6 @@
 #include "threadpool.hpp"
 #include "ward.hpp"
 
-struct svs_em_result {
-  struct Win {
-    int32_t K = 0;
-    int64_t rng_used = 0;
-    std::vector<int32_t> rclust;
-    std::vector<double> bic, lik, gamma, pi, theta;
-  };
-  std::vector<Win> w;
-  double kernel_ms = 0.0;
-};
-
 namespace svs {
 
 void legacy_exponentials(uint32_t seed, uint64_t n, double* out) {
@@ -137,13 +126,13 @@ void run_similarity(svs_context* ctx, int32_t n, const svs_em_window* wins, cons
   ctx->d_em_in.ensure(total);
   ctx->d_em_out.ensure(sdoubles * sizeof(double) + 8);
   char* d = ctx->d_em_in.as<char>();
-  SVS_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, ctx->stream));
+  SVS_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, ctx->em_stream));
   SVS_HIP(launch_similarity(reinterpret_cast<const EmWindow*>(d + off_w), n, reinterpret_cast<const uint8_t*>(d + off_x),
-                            reinterpret_cast<const int64_t*>(d + off_o), ctx->d_em_out.as<double>(), ctx->stream));
+                            reinterpret_cast<const int64_t*>(d + off_o), ctx->d_em_out.as<double>(), ctx->em_stream));
   ctx->h_em_out.ensure(sdoubles * sizeof(double) + 8);
   SVS_HIP(hipMemcpyAsync(ctx->h_em_out.ptr, ctx->d_em_out.ptr, sdoubles * sizeof(double), hipMemcpyDeviceToHost,
-                         ctx->stream));
-  SVS_HIP(hipStreamSynchronize(ctx->stream));
+                         ctx->em_stream));
+  SVS_HIP(hipStreamSynchronize(ctx->em_stream));
   const double* hs = ctx->h_em_out.as<double>();
   for (int32_t w = 0; w < n; ++w)
     std::memcpy(S_out + s_off_in[w], hs + s_off[w],
@@ -194,7 +183,7 @@ svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, co
   ctx->d_em_out.ensure(od_bytes + oi_bytes + par_bytes + 256);
   ctx->h_em_out.ensure(od_bytes + oi_bytes + par_bytes + 256);
   char* d = ctx->d_em_in.as<char>();
-  SVS_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, ctx->stream));
+  SVS_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, ctx->em_stream));
   double* d_outd = ctx->d_em_out.as<double>();
   int32_t* d_outi = reinterpret_cast<int32_t*>(ctx->d_em_out.as<char>() + (od_bytes + 255) / 256 * 256);
   double* d_par = reinterpret_cast<double*>(reinterpret_cast<char*>(d_outi) + oi_bytes);
@@ -204,18 +193,18 @@ svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, co
     uint64_t want = std::max<uint64_t>(ctx->rng_len, 1ull << 20);
     for (int attempt = 0;; ++attempt) {
       ensure_rng(ctx, static_cast<uint32_t>(cfg.seed), want);
-      SVS_HIP(hipEventRecord(ctx->ev_start, ctx->stream));
+      SVS_HIP(hipEventRecord(ctx->ev_start, ctx->em_stream));
       SVS_HIP(launch_em_cluster(reinterpret_cast<const EmWindow*>(d + off_w), n,
                                 reinterpret_cast<const uint8_t*>(d + off_x), reinterpret_cast<const int32_t*>(d + off_l),
                                 ctx->d_rng.as<double>(), ctx->rng_len, ec, ctx->d_em_ws.as<double>(), d_outd, d_outi,
-                                ctx->stream));
+                                ctx->em_stream));
       if (cfg.want_params)
         SVS_HIP(launch_em_gather(reinterpret_cast<const EmWindow*>(d + off_w), n, ctx->d_em_ws.as<double>(), d_outi,
-                                 d_par, ctx->stream));
-      SVS_HIP(hipEventRecord(ctx->ev_stop, ctx->stream));
+                                 d_par, ctx->em_stream));
+      SVS_HIP(hipEventRecord(ctx->ev_stop, ctx->em_stream));
       SVS_HIP(hipMemcpyAsync(ctx->h_em_out.ptr, ctx->d_em_out.ptr,
-                             (od_bytes + 255) / 256 * 256 + oi_bytes + par_bytes, hipMemcpyDeviceToHost, ctx->stream));
-      SVS_HIP(hipStreamSynchronize(ctx->stream));
+                             (od_bytes + 255) / 256 * 256 + oi_bytes + par_bytes, hipMemcpyDeviceToHost, ctx->em_stream));
+      SVS_HIP(hipStreamSynchronize(ctx->em_stream));
       float ms = 0.f;
       SVS_HIP(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
       res->kernel_ms += ms;
@@ -286,7 +275,7 @@ void svs_em_result_free(svs_em_result* r) { delete r; }
 namespace svs {
 
 svs_em_result* run_em_cluster(svs_context* ctx, int32_t n, const svs_em_window* wins, const uint8_t* X,
-                              const svs_em_config& cfg) {
+                              const svs_em_config& cfg, ThreadPool* pool) {
   std::vector<svs_em_window> W(wins, wins + n);
   std::vector<int64_t> s_off(n);
   int64_t s_tot = 0, l_tot = 0;
@@ -301,12 +290,14 @@ svs_em_result* run_em_cluster(svs_context* ctx, int32_t n, const svs_em_window* 
   std::vector<int32_t> labels(static_cast<size_t>(std::max<int64_t>(1, l_tot)));
   if (n > 0) run_similarity(ctx, n, W.data(), X, S.data(), s_off.data());
   // ward + maxclust per window on the pool (ReadsCluster.py:243, :94)
-  ctx->pool->parallel_for(static_cast<size_t>(n), [&](size_t w) {
+  auto ward = [&](size_t w) {
     thread_local std::vector<WardMerge> Z;
     const int r = W[w].n_reads;
     ward_linkage(S.data() + s_off[w], r, &Z);
     maxclust_labels(Z, r, std::min(cfg.max_c + 1, r), labels.data() + W[w].label_off);
-  });
+  };
+  if (pool) pool->parallel_for(static_cast<size_t>(n), ward);
+  else for (int32_t w = 0; w < n; ++w) ward(static_cast<size_t>(w));
   return run_em(ctx, n, W.data(), X, labels.data(), cfg);
 }
 

@@ -1,19 +1,72 @@
 // Internal declarations shared by the engine translation units.
 #pragma once
+#include <functional>
 #include <string>
 #include <vector>
 
 #include "../../include/svscope.h"
+#include "features.hpp"
 #include "poa_graph.hpp"
+
+// EM results of one batch (opaque to ABI users).
+struct svs_em_result {
+  struct Win {
+    int32_t K = 0;
+    int64_t rng_used = 0;
+    std::vector<int32_t> rclust;
+    std::vector<double> bic, lik, gamma, pi, theta;
+  };
+  std::vector<Win> w;
+  double kernel_ms = 0.0;
+};
+
+// Decision pipeline results (opaque to ABI users).
+struct svs_decision_result {
+  struct Win {
+    int32_t status = 0, K = 0;
+    std::vector<svs::ClusterPlan> som, germ;
+  };
+  std::vector<Win> w;
+  svs_decision_stats st{};
+};
 
 namespace svs {
 
 struct PoaTask {
   std::vector<std::string> seqs;
+  bool genmsa = false;  // also produce the MSA rows when the task completes
+  uint32_t tag = 0;     // caller's bookkeeping (window / cluster id)
+  size_t next = 0;      // index of the next sequence to align
   PoaGraph graph;
-  RowTables rows;  // exported row tables of the current step (capacity reused across steps)
+  RowTables rows;       // exported row tables of the current step (capacity reused across steps)
   std::string consensus;
   std::vector<std::string> msa;
+};
+
+// Continuous-batching POA driver.  Every launch aligns the next sequence of
+// each active task of one task group; two groups alternate on the in-order
+// POA stream so the host folds one group's alignments while the GPU runs the
+// other's.  Finished tasks leave their group after every step and queued tasks
+// take their place, so the GPU stays full while tasks of different lengths
+// (window MSAs, cluster consensus jobs) come and go.
+class PoaScheduler {
+ public:
+  using DoneFn = std::function<void(const std::vector<uint32_t>&)>;
+  // poll(block): called between launches; may add() tasks.  Returns true while
+  // outside work may still add tasks; with block=true it may wait for it.
+  using PollFn = std::function<bool(bool)>;
+  PoaScheduler(svs_context* ctx, const svs_poa_config& cfg, svs_poa_stats& st);
+  ~PoaScheduler();
+  uint32_t add(PoaTask&& t);
+  PoaTask& task(uint32_t id);
+  // Runs until no task is queued or active and poll() reports no outside work.
+  // done(ids) receives each batch of completed tasks (consensus / msa filled);
+  // afterwards the scheduler drops their graphs.
+  void run(const DoneFn& done, const PollFn& poll);
+
+ private:
+  struct Impl;
+  Impl* impl_;
 };
 
 void check_poa_config(const svs_poa_config& c);
@@ -25,7 +78,14 @@ void run_similarity(svs_context* ctx, int32_t n, const svs_em_window* wins, cons
                     const int64_t* s_off);
 svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, const uint8_t* X,
                       const int32_t* labels, const svs_em_config& cfg);
+class ThreadPool;
+// pool == nullptr runs the host ward/maxclust step on the calling thread (used
+// by the pipeline's EM worker, which must not share the driver's pool).
 svs_em_result* run_em_cluster(svs_context* ctx, int32_t n, const svs_em_window* wins, const uint8_t* X,
-                              const svs_em_config& cfg);
+                              const svs_em_config& cfg, ThreadPool* pool);
+
+svs_decision_result* run_decision(svs_context* ctx, int32_t n, const svs_decision_window* wins,
+                                  const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
+                                  const uint8_t* is_tlabel, const svs_decision_config& cfg);
 
 }  // namespace svs

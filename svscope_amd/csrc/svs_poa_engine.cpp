@@ -1,17 +1,20 @@
-// Batched POA engine: lockstep driver over many independent POA jobs (one job
-// = one pyspoa `poa(seqs, 1)` call of the reference: a window MSA at
-// DataScanner.py:206,213 or a cluster consensus at DecisionMaker.py:160,171).
+// Batched POA engine: continuous-batching driver over many independent POA
+// tasks (one task = one pyspoa `poa(seqs, 1)` call of the reference: a window
+// MSA at DataScanner.py:206,213 or a cluster consensus at DecisionMaker.py:160,171).
 //
-// Step s aligns the s-th sequence of every job at once: the host exports each
-// job's rank-ordered row tables, one HIP launch runs every read-vs-graph DP
-// (one wave per job) and its traceback, and the host folds the alignments back
-// into the graphs in parallel.
+// Each launch aligns the next sequence of every active task of a group: the
+// host exports each task's rank-ordered row tables, one HIP launch runs every
+// read-vs-graph DP and its traceback, and the host folds the alignments back
+// into the graphs in parallel.  Completed tasks leave after every step and
+// queued ones take their place (PoaScheduler).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -70,24 +73,158 @@ double ms_since(Clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
 }
 
-// One launch in flight: the jobs of one task group at one step.
+// One launch in flight: the jobs of one task group (each at its own next sequence).
 struct Launch {
-  std::vector<uint32_t> ids;       // task indices, one job each (tables in PoaTask::rows)
+  std::vector<uint32_t> ids;       // task ids, one job each (tables in PoaTask::rows)
   std::vector<PoaJob> jobs;
-  size_t step = 0;
   size_t n_aln = 0;
   PoaArena* arena = nullptr;
 };
 
+// Kernel selection: the strip-major kernel (poa_strip.hip) unless
+// SVS_POA_KERNEL=rows asks for the row-major one (poa_kernels.hip).
+bool use_strip_kernel() {
+  const char* e = std::getenv("SVS_POA_KERNEL");
+  return !(e && std::string(e) == "rows");
+}
+
+// SVS_POA_STRIP_GLOBAL_POOL=1 keeps the strip kernel's pool in global memory
+// even when it fits LDS (tests the path large graphs take).
+bool strip_pool_forced_global() {
+  const char* e = std::getenv("SVS_POA_STRIP_GLOBAL_POOL");
+  return e && std::string(e) == "1";
+}
+
 uint64_t job_bytes(const RowTables& tt, uint64_t L) {
-  const uint64_t ls = round_up(L + 1, 64), V = tt.info.size();
+  const uint64_t ls = round_up(L + 1, 64), V = tt.pstart.size() - 1;
+  if (use_strip_kernel()) {
+    // traceback codes + two strip-boundary carry buffers (+ a global pool when
+    // the graph needs more slots than the LDS pool holds)
+    const uint64_t pool = (tt.n_slots > kStripMaxLdsSlots || strip_pool_forced_global())
+                              ? static_cast<uint64_t>(tt.n_slots) * 193 * 4 + 256 : 0;
+    return V * ls * 2 + V * 32 + pool + 256 + (V + L + 1) * 8;
+  }
   return V * ls * 2 + static_cast<uint64_t>(tt.n_slots) * 3 * ls * 4 + (V + L + 1) * 8;
+}
+
+void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, const PoaScore& score,
+                           svs_poa_stats& st, double& host_ms) {
+  auto th0 = Clock::now();
+  const size_t nj = la.ids.size();
+  la.jobs.assign(nj, PoaJob{});
+  uint64_t n_rows = 0, n_pstart = 0, n_pred = 0, n_seq = 0, n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
+  uint32_t max_preds = 0, max_slots = 1;
+  for (size_t k = 0; k < nj; ++k) max_slots = std::max(max_slots, tasks[la.ids[k]].rows.n_slots);
+  const bool lds_pool = max_slots <= kStripMaxLdsSlots && !strip_pool_forced_global();
+  for (size_t k = 0; k < nj; ++k) {
+    const auto& tt = tasks[la.ids[k]].rows;
+    const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];
+    PoaJob& J = la.jobs[k];
+    J.n_rows = static_cast<uint32_t>(tt.pstart.size() - 1);
+    J.len = static_cast<uint32_t>(s.size());
+    J.ls = static_cast<uint32_t>(round_up(J.len + 1, 64));
+    J.n_slots = tt.n_slots;
+    J.row_off = static_cast<uint32_t>(n_rows);
+    J.rec_off = static_cast<uint32_t>(n_rows);
+    J.pstart_off = static_cast<uint32_t>(n_pstart);
+    J.pred_off = static_cast<uint32_t>(n_pred);
+    J.seq_off = static_cast<uint32_t>(n_seq + 1);  // one zero pad byte precedes each read
+    J.tb_off = n_tb;
+    J.bnd_off = n_bnd;
+    J.pool_off = n_pool;
+    J.aln_off = n_aln;
+    n_rows += J.n_rows;
+    n_pstart += J.n_rows + 1;
+    n_pred += tt.pred_row.size();
+    n_seq += J.ls + 64;
+    n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
+    n_bnd += round_up(static_cast<uint64_t>(J.n_rows) * 8, 64);
+    if (!lds_pool) n_pool += round_up(static_cast<uint64_t>(J.n_slots) * 193, 64);
+    n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
+    max_preds = std::max(max_preds, tt.max_preds);
+    st.dp_cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);
+  }
+  if (max_preds > 31)
+    throw SvsError(SVS_E_UNSUPPORTED, "a graph node has more than 31 in-edges (traceback code limit)");
+  if (n_rows * kRecWords > 0xFFFFFFFFull || n_pred > 0xFFFFFFFFull || n_seq > 0xFFFFFFFFull)
+    throw SvsError(SVS_E_UNSUPPORTED, "batch too large for 32-bit table offsets");
+  la.n_aln = n_aln;
+  size_t off = 0;
+  auto sec = [&](size_t bytes) {
+    const size_t o = off;
+    off = round_up(off + bytes, 256);
+    return o;
+  };
+  const size_t s_jobs = sec(nj * sizeof(PoaJob));
+  const size_t s_rec = sec(n_rows * kRecWords * 4), s_ps = sec(n_pstart * 4), s_col0 = sec(n_rows * 12);
+  const size_t s_prow = sec(n_pred * 4), s_pslot = sec(n_pred * 4), s_seq = sec(n_seq + 256);
+  PoaArena& A = *la.arena;
+  A.h_in.ensure(off);
+  char* hs = A.h_in.as<char>();
+  std::memcpy(hs + s_jobs, la.jobs.data(), nj * sizeof(PoaJob));
+  ctx->pool->parallel_for(nj, [&](size_t k) {
+    const auto& tt = tasks[la.ids[k]].rows;
+    const PoaJob& J = la.jobs[k];
+    std::memcpy(hs + s_rec + 4ull * kRecWords * J.rec_off, tt.rec.data(), 4ull * kRecWords * J.n_rows);
+    std::memcpy(hs + s_ps + 4ull * J.pstart_off, tt.pstart.data(), 4ull * (J.n_rows + 1));
+    std::memcpy(hs + s_col0 + 12ull * J.row_off, tt.col0.data(), 12ull * J.n_rows);
+    if (!tt.pred_row.empty()) {
+      std::memcpy(hs + s_prow + 4ull * J.pred_off, tt.pred_row.data(), 4 * tt.pred_row.size());
+      std::memcpy(hs + s_pslot + 4ull * J.pred_off, tt.pred_slot.data(), 4 * tt.pred_slot.size());
+    }
+    const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];
+    std::memset(hs + s_seq + J.seq_off - 1, 0, J.ls + 64);
+    std::memcpy(hs + s_seq + J.seq_off, s.data(), s.size());
+  });
+  host_ms += ms_since(th0);
+
+  A.d_in.ensure(off);
+  A.d_tb.ensure(n_tb * 2 + 4096);
+  A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096);
+  A.d_aln.ensure(n_aln * 8);
+  A.d_alen.ensure(nj * 4);
+  A.h_aln.ensure(n_aln * 8);
+  A.h_alen.ensure(nj * 4);
+  char* dg = A.d_in.as<char>();
+  SVS_HIP(hipMemcpyAsync(dg, hs, off, hipMemcpyHostToDevice, A.stream));
+  PoaLaunch pl{};
+  pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
+  pl.n_jobs = static_cast<int>(nj);
+  pl.score = score;
+  pl.rec = reinterpret_cast<const uint32_t*>(dg + s_rec);
+  pl.row_pstart = reinterpret_cast<const uint32_t*>(dg + s_ps);
+  pl.pred_row = reinterpret_cast<const uint32_t*>(dg + s_prow);
+  pl.pred_slot = reinterpret_cast<const uint32_t*>(dg + s_pslot);
+  pl.col0 = reinterpret_cast<const int32_t*>(dg + s_col0);
+  pl.seqs = reinterpret_cast<const uint8_t*>(dg + s_seq);
+  pl.tb = A.d_tb.as<uint16_t>();
+  pl.bnd = A.d_pool.as<int32_t>();
+  pl.pool = A.d_pool.as<int32_t>() + n_bnd;
+  pl.aln = A.d_aln.as<int32_t>();
+  pl.aln_len = A.d_alen.as<int32_t>();
+  pl.lds_slots = lds_pool ? max_slots : 0;
+  SVS_HIP(hipEventRecord(A.ev0, A.stream));
+  SVS_HIP(launch_poa_strip(pl, A.stream));
+  SVS_HIP(hipEventRecord(A.ev1, A.stream));
+  SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 4, hipMemcpyDeviceToHost, A.stream));
+  SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, pl.aln, n_aln * 8, hipMemcpyDeviceToHost, A.stream));
+  SVS_HIP(hipEventRecord(A.done, A.stream));
+  st.launches += 1;
+  st.alignments += nj;
+  st.tb_bytes += n_tb * 2;
+  st.pool_bytes += (n_bnd + n_pool) * 4;
+  st.h2d_bytes += off;
+  st.d2h_bytes += n_aln * 8 + nj * 4;
 }
 
 // Packs the launch's tables into the arena's pinned buffer and enqueues
 // H2D copy, kernel and D2H copies on the arena's stream (no host wait).
-void pack_and_launch(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, const PoaScore& score,
+void pack_and_launch(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, const PoaScore& score,
                      svs_poa_stats& st, double& host_ms) {
+  if (use_strip_kernel()) {
+    pack_and_launch_strip(ctx, la, tasks, score, st, host_ms);
+    return;
+  }
   auto th0 = Clock::now();
   const size_t nj = la.ids.size();
   la.jobs.assign(nj, PoaJob{});
@@ -95,7 +232,7 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, 
   uint32_t max_preds = 0;
   for (size_t k = 0; k < nj; ++k) {
     const auto& tt = tasks[la.ids[k]].rows;
-    const std::string& s = tasks[la.ids[k]].seqs[la.step];
+    const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];
     PoaJob& J = la.jobs[k];
     J.n_rows = static_cast<uint32_t>(tt.info.size());
     J.len = static_cast<uint32_t>(s.size());
@@ -148,7 +285,7 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, 
       std::memcpy(hs + s_prow + 4ull * J.pred_off, tt.pred_row.data(), 4 * tt.pred_row.size());
       std::memcpy(hs + s_pslot + 4ull * J.pred_off, tt.pred_slot.data(), 4 * tt.pred_slot.size());
     }
-    const std::string& s = tasks[la.ids[k]].seqs[la.step];
+    const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];
     std::memset(hs + s_seq + J.seq_off - 1, 0, J.ls + 64);
     std::memcpy(hs + s_seq + J.seq_off, s.data(), s.size());
   });
@@ -194,7 +331,7 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, 
 }
 
 // Waits for the launch and folds its alignments back into the graphs.
-void finish(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, svs_poa_stats& st, double& host_ms) {
+void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_stats& st, double& host_ms) {
   PoaArena& A = *la.arena;
   SVS_HIP(hipEventSynchronize(A.done));  // the other group's launch may still be queued behind it
   float ms = 0.f;
@@ -213,127 +350,199 @@ void finish(svs_context* ctx, Launch& la, std::vector<PoaTask>& tasks, svs_poa_s
       fwd[2 * x + 1] = p[2 * (n - 1 - x) + 1];
     }
     auto& t = tasks[la.ids[k]];
-    t.graph.add_alignment_ranks(fwd, t.seqs[la.step]);
+    t.graph.add_alignment_ranks(fwd, t.seqs[t.next]);
+    ++t.next;
   });
   host_ms += ms_since(th0);
 }
 
-// Task group: a disjoint subset of the jobs that advances step by step with its
-// own arena.  Groups alternate on one in-order stream, so while the GPU runs
-// group B's step the host folds group A's alignments and enqueues A's next step.
+// Task group: a disjoint subset of the active tasks with its own arena.
 struct Group {
-  std::vector<uint32_t> members;
-  size_t step = 0, max_steps = 0;
+  std::vector<uint32_t> active;
   Launch la;
   bool pending = false;
+  PoaArena* arena = nullptr;
 };
 
-// Prepares the group's next step with GPU work and launches it (returns false
-// when the group is finished).  Steps whose jobs exceed the group's device
-// budget run as synchronous sub-launches.
-bool advance(svs_context* ctx, Group& g, PoaArena* arena, std::vector<PoaTask>& tasks, const svs_poa_config& cfg,
-             const PoaScore& score, size_t budget, svs_poa_stats& st, double& host_ms) {
-  std::vector<uint8_t> needs(g.members.size());
-  while (g.step < g.max_steps) {
-    const size_t step = g.step;
-    auto th0 = Clock::now();
-    // sequences landing on an empty graph become a fresh chain on the host (no DP)
-    ctx->pool->parallel_for(g.members.size(), [&](size_t i) {
-      auto& t = tasks[g.members[i]];
-      needs[i] = 0;
-      if (step >= t.seqs.size() || t.seqs[step].empty()) return;
-      if (t.graph.empty()) t.graph.add_alignment_nodes({}, t.seqs[step]);
-      else needs[i] = 1;
-    });
-    std::vector<uint32_t> ids;
-    for (size_t i = 0; i < g.members.size(); ++i)
-      if (needs[i]) ids.push_back(g.members[i]);
-    ++g.step;
-    if (ids.empty()) { host_ms += ms_since(th0); continue; }
-    ctx->pool->parallel_for(ids.size(), [&](size_t k) {
-      auto& t = tasks[ids[k]];
-      t.graph.export_rows(&t.rows);
-      fill_col0(&t.rows, cfg.g, cfg.e, cfg.q, cfg.c);
-    });
-    host_ms += ms_since(th0);
-    uint64_t total = 0;
-    for (size_t k = 0; k < ids.size(); ++k) total += job_bytes(tasks[ids[k]].rows, tasks[ids[k]].seqs[step].size());
-    if (total <= budget) {
-      g.la.ids = std::move(ids);
-      g.la.step = step;
-      g.la.arena = arena;
-      pack_and_launch(ctx, g.la, tasks, score, st, host_ms);
-      g.pending = true;
-      return true;
-    }
-    // over budget: consecutive synchronous sub-launches
-    size_t first = 0;
-    while (first < ids.size()) {
-      size_t last = first;
-      uint64_t bytes = 0;
-      while (last < ids.size()) {
-        const uint64_t b = job_bytes(tasks[ids[last]].rows, tasks[ids[last]].seqs[step].size());
-        if (last > first && bytes + b > budget) break;
-        bytes += b;
-        ++last;
-      }
-      Launch sub;
-      sub.ids.assign(ids.begin() + first, ids.begin() + last);
-      sub.step = step;
-      sub.arena = arena;
-      pack_and_launch(ctx, sub, tasks, score, st, host_ms);
-      finish(ctx, sub, tasks, st, host_ms);
-      first = last;
-    }
+size_t active_jobs_per_group() {
+  if (const char* e = std::getenv("SVS_POA_ACTIVE_JOBS")) {
+    const long v = std::atol(e);
+    if (v > 0) return static_cast<size_t>(v);
   }
-  return false;
+  return 1024;  // x WPJ waves fills the 1024 SIMDs of MI355X about 4 deep
 }
 
 }  // namespace
 
-void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_config& cfg,
-                   svs_poa_stats& st) {
-  check_poa_config(cfg);
-  const auto t_wall0 = Clock::now();
+struct PoaScheduler::Impl {
+  svs_context* ctx;
+  svs_poa_config cfg;
+  PoaScore score;
+  svs_poa_stats& st;
+  std::deque<PoaTask> tasks;
+  std::deque<uint32_t> queue;
+  Group groups[2];
+  size_t cap;
+  size_t budget;
   double host_ms = 0.0;
-  const PoaScore score{cfg.m, cfg.n, cfg.g, cfg.e, cfg.q, cfg.c};
-  // Two groups once there are enough jobs to keep the GPU busy with half of them.
-  const size_t n_groups = tasks.size() >= 64 ? 2 : 1;
-  while (ctx->poa_arenas.size() < n_groups) ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
-  std::vector<Group> groups(n_groups);
-  for (size_t i = 0; i < tasks.size(); ++i) {
-    Group& g = groups[i % n_groups];
-    g.members.push_back(static_cast<uint32_t>(i));
-    g.max_steps = std::max(g.max_steps, tasks[i].seqs.size());
+
+  Impl(svs_context* c, const svs_poa_config& k, svs_poa_stats& s)
+      : ctx(c), cfg(k), score{k.m, k.n, k.g, k.e, k.q, k.c}, st(s), cap(active_jobs_per_group()),
+        budget(c->device_budget / 2) {
+    while (ctx->poa_arenas.size() < 2) ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
+    for (int g = 0; g < 2; ++g) groups[g].arena = ctx->poa_arenas[g].get();
   }
-  const size_t budget = ctx->device_budget / n_groups;
-  try {
-    for (size_t gi = 0; gi < n_groups; ++gi)
-      advance(ctx, groups[gi], ctx->poa_arenas[gi].get(), tasks, cfg, score, budget, st, host_ms);
-    bool any = true;
-    while (any) {
-      any = false;
-      for (size_t gi = 0; gi < n_groups; ++gi) {
-        Group& g = groups[gi];
+
+  // Moves queued tasks into the group: at most half of the queue (so the other
+  // group gets work too) and at most `cap` active tasks.
+  void refill(Group& g) {
+    if (queue.empty() || g.active.size() >= cap) return;
+    size_t take = std::min(cap - g.active.size(), std::max<size_t>(1, (queue.size() + 1) / 2));
+    while (take-- > 0 && !queue.empty()) {
+      g.active.push_back(queue.front());
+      queue.pop_front();
+    }
+  }
+
+  // Prepares the group's next launch (or completes its tasks) and launches it.
+  void advance(Group& g, const DoneFn& done) {
+    std::vector<uint8_t> needs;
+    for (;;) {
+      refill(g);
+      if (g.active.empty()) return;
+      auto th0 = Clock::now();
+      needs.assign(g.active.size(), 0);
+      // sequences landing on an empty graph become a fresh chain (no DP)
+      ctx->pool->parallel_for(g.active.size(), [&](size_t i) {
+        PoaTask& t = tasks[g.active[i]];
+        while (t.next < t.seqs.size()) {
+          const std::string& s = t.seqs[t.next];
+          if (s.empty()) { ++t.next; continue; }
+          if (t.graph.empty()) { t.graph.add_alignment_nodes({}, s); ++t.next; continue; }
+          break;
+        }
+        if (t.next < t.seqs.size()) {
+          needs[i] = 1;
+          if (use_strip_kernel()) t.graph.export_strip_rows(&t.rows);
+          else t.graph.export_rows(&t.rows);
+          fill_col0(&t.rows, cfg.g, cfg.e, cfg.q, cfg.c);
+        } else {
+          t.consensus = t.graph.consensus(cfg.min_coverage);
+          if (t.genmsa) t.msa = t.graph.msa();
+        }
+      });
+      std::vector<uint32_t> ids, fin;
+      for (size_t i = 0; i < g.active.size(); ++i) (needs[i] ? ids : fin).push_back(g.active[i]);
+      host_ms += ms_since(th0);
+      g.active = ids;
+      if (!fin.empty()) {
+        done(fin);
+        for (uint32_t id : fin) {
+          PoaTask& t = tasks[id];
+          t.graph = PoaGraph();
+          t.rows = RowTables();
+          std::vector<std::string>().swap(t.seqs);
+        }
+        if (ids.empty()) continue;  // refill and try again
+      }
+      uint64_t total = 0;
+      for (uint32_t id : ids) total += job_bytes(tasks[id].rows, tasks[id].seqs[tasks[id].next].size());
+      if (total <= budget) {
+        g.la.ids = std::move(ids);
+        g.la.arena = g.arena;
+        pack_and_launch(ctx, g.la, tasks, score, st, host_ms);
+        g.pending = true;
+        return;
+      }
+      // over budget: consecutive synchronous sub-launches, then prepare again
+      size_t first = 0;
+      while (first < ids.size()) {
+        size_t last = first;
+        uint64_t bytes = 0;
+        while (last < ids.size()) {
+          const uint64_t b = job_bytes(tasks[ids[last]].rows, tasks[ids[last]].seqs[tasks[ids[last]].next].size());
+          if (last > first && bytes + b > budget) break;
+          bytes += b;
+          ++last;
+        }
+        Launch sub;
+        sub.ids.assign(ids.begin() + first, ids.begin() + last);
+        sub.arena = g.arena;
+        pack_and_launch(ctx, sub, tasks, score, st, host_ms);
+        finish(ctx, sub, tasks, st, host_ms);
+        first = last;
+      }
+    }
+  }
+
+  void run(const DoneFn& done, const PollFn& poll) {
+    for (Group& g : groups) advance(g, done);
+    for (;;) {
+      bool progressed = false;
+      for (Group& g : groups) {
         if (!g.pending) continue;
         finish(ctx, g.la, tasks, st, host_ms);
         g.pending = false;
-        advance(ctx, g, ctx->poa_arenas[gi].get(), tasks, cfg, score, budget, st, host_ms);
-        any = true;
+        advance(g, done);
+        progressed = true;
       }
+      const bool outside = poll(false);
+      for (Group& g : groups)
+        if (!g.pending && !queue.empty()) advance(g, done);
+      const bool busy = groups[0].pending || groups[1].pending;
+      if (progressed || busy) continue;
+      if (outside) {
+        poll(true);
+        continue;
+      }
+      break;
     }
-  } catch (...) {
-    for (auto& a : ctx->poa_arenas) (void)hipStreamSynchronize(a->stream);
-    throw;
   }
-  auto th0 = Clock::now();
-  ctx->pool->parallel_for(tasks.size(), [&](size_t i) {
-    auto& t = tasks[i];
-    t.consensus = t.graph.consensus(cfg.min_coverage);
-    if (cfg.genmsa) t.msa = t.graph.msa();
-  });
-  host_ms += ms_since(th0);
-  st.host_graph_ms += host_ms;
+};
+
+PoaScheduler::PoaScheduler(svs_context* ctx, const svs_poa_config& cfg, svs_poa_stats& st)
+    : impl_(nullptr) {
+  check_poa_config(cfg);
+  impl_ = new Impl(ctx, cfg, st);
+}
+
+PoaScheduler::~PoaScheduler() {
+  for (auto& a : impl_->ctx->poa_arenas) (void)hipStreamSynchronize(a->stream);
+  impl_->st.host_graph_ms += impl_->host_ms;
+  delete impl_;
+}
+
+uint32_t PoaScheduler::add(PoaTask&& t) {
+  const uint32_t id = static_cast<uint32_t>(impl_->tasks.size());
+  t.next = 0;
+  impl_->tasks.push_back(std::move(t));
+  impl_->queue.push_back(id);
+  return id;
+}
+
+PoaTask& PoaScheduler::task(uint32_t id) { return impl_->tasks[id]; }
+
+void PoaScheduler::run(const DoneFn& done, const PollFn& poll) { impl_->run(done, poll); }
+
+void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_config& cfg,
+                   svs_poa_stats& st) {
+  const auto t_wall0 = Clock::now();
+  {
+    PoaScheduler sched(ctx, cfg, st);
+    for (auto& t : tasks) {
+      t.genmsa = cfg.genmsa != 0;
+      sched.add(std::move(t));
+    }
+    sched.run(
+        [&](const std::vector<uint32_t>& ids) {
+          for (uint32_t id : ids) {
+            PoaTask& t = sched.task(id);
+            tasks[id].consensus = std::move(t.consensus);
+            tasks[id].msa = std::move(t.msa);
+          }
+        },
+        [](bool) { return false; });
+  }
   st.wall_ms += ms_since(t_wall0);
 }
 

@@ -7,28 +7,71 @@ signature, gate, labelling and record format of
   gate :134 -> MSAFeatureSelection :136 -> EMCluster if >= 10 features :137-138
   -> per-cluster somatic/germline test in ascending label order :145-154
   -> POA consensus per reported cluster :155-176 -> record :178-190.
-``DecisionBatch(windows, ...)`` runs the same logic for many windows with one
-batched GPU POA for all window MSAs, one batched GPU EM, and one batched GPU
-POA for all cluster consensus sequences.
+``DecisionBatch(windows, ...)`` runs the same logic for many windows through
+one ``svs_decision_batch`` call: window MSAs, feature selection, EM and the
+cluster consensus POAs are pipelined inside the engine (include/svscope.h).
 """
+import ctypes
+import os
 import time
 
 import numpy as np
 
-from .data_scanner import SeqDecoder, msa_feature_selection_batch
-from .poa import poa_batch
-from .reads_cluster import em_cluster_batch
+from . import _abi
 
 
 def _tag(read_id):
     return read_id.split("|")[0].split("_")[-1]
 
 
+def _pack_windows(windows, gated, Tlabel):
+    """Flattens the gated windows into the svs_decision_batch input arrays."""
+    wins = (_abi.DecisionWindow * max(1, len(gated)))()
+    byte_start = [0]
+    chunks, text, tags = [], [], []
+    total = text_len = tag_len = 0
+    for k, w in enumerate(gated):
+        rec, seqs, ids, f5, f3 = windows[w][:5]
+        W = wins[k]
+        W.n_seqs = len(seqs)
+        W.n_ids = len(ids)
+        W.seq_start = len(byte_start) - 1
+        for s in seqs:
+            b = s.encode("latin-1") if isinstance(s, str) else bytes(s)
+            chunks.append(b)
+            total += len(b)
+            byte_start.append(total)
+        b5, b3 = f5.encode("latin-1"), f3.encode("latin-1")
+        W.flank5_off, W.flank5_len = text_len, len(b5)
+        W.flank3_off, W.flank3_len = text_len + len(b5), len(b3)
+        text.append(b5 + b3)
+        text_len += len(b5) + len(b3)
+        W.tag_off = tag_len
+        tags.append(np.fromiter((_tag(x) == Tlabel for x in ids), dtype=np.uint8, count=len(ids)))
+        tag_len += len(ids)
+    starts = np.asarray(byte_start, dtype=np.int64)
+    blob = b"".join(chunks) or b"\0"
+    txt = b"".join(text) or b"\0"
+    tag_arr = np.concatenate(tags) if tag_len else np.zeros(1, np.uint8)
+    return wins, starts, blob, txt, tag_arr
+
+
+def _config(readcutoff, hcutoff, scutoff):
+    cfg = _abi.DecisionConfig()
+    cfg.readcutoff, cfg.hcutoff, cfg.scutoff = int(readcutoff), int(hcutoff), float(scutoff)
+    cfg.poa = _abi.PoaConfig(1, 5, -4, -8, -6, -10, -4, -1, 1)
+    cfg.em = _abi.EmConfig(9, 20, 2023, 0, 1e-10)
+    cfg.em_batch = int(os.environ.get("SVS_EM_BATCH", "0"))
+    return cfg
+
+
 def DecisionBatch(windows, Tlabel="tumor", readcutoff=3, hcutoff=3, scutoff=0.05, context=None, stats=None):
     """windows: list of (TDRecord, sequenceList, ReadIDs, flank_5, flank_3[, windowFlag]).
-    Returns the list of 10-field records, in input order."""
+    Returns the list of 10-field records, in input order.  The gated windows go
+    through one svs_decision_batch call (MSA POA, features, EM and consensus
+    POA pipelined on the GPU); this function keeps the gate (:134) and the
+    record formatting (:178-190)."""
     t_start = time.perf_counter()
-    phase = {}
     records = []
     gated = []
     for w, win in enumerate(windows):
@@ -44,65 +87,57 @@ def DecisionBatch(windows, Tlabel="tumor", readcutoff=3, hcutoff=3, scutoff=0.05
             gated.append(w)
     if not gated:
         return records
+    ctx = context or _abi.default_context()
+    lib = ctx.lib
+    wins, starts, blob, txt, tag_arr = _pack_windows(windows, gated, Tlabel)
+    cfg = _config(readcutoff, hcutoff, scutoff)
+    res = ctypes.c_void_p()
     t0 = time.perf_counter()
-    feats = msa_feature_selection_batch([(windows[w][1], windows[w][3], windows[w][4], np.asarray(windows[w][2]))
-                                         for w in gated], hcutoff, scutoff, context=context, stats=stats)
-    phase["msa_and_features_s"] = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    em_idx = [k for k, (_, feat, _) in enumerate(feats) if feat.shape[0] != 0 and feat.shape[1] >= 10]
-    ems = em_cluster_batch([feats[k][1] for k in em_idx], context=context, timing=phase) if em_idx else []
-    phase["em_total_s"] = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    # cluster labelling (ascending label order, DecisionMaker.py:145-154)
-    plans = []
-    jobs = []
-    for k, em in zip(em_idx, ems):
-        encoded, _, ids = feats[k]
-        ids = np.asarray(ids)
-        labels = em["Rclust"]
-        som, germ = [], []
-        for L in np.unique(labels):
-            idx = np.where(labels == L)[0]
-            types = np.unique([_tag(x) for x in ids[idx]])
-            if types.shape[0] == 1 and types[0] == Tlabel and idx.shape[0] >= readcutoff:
-                som.append(idx)
-            elif idx.shape[0] >= readcutoff:
-                germ.append(idx)
-        entry = dict(w=gated[k], ids=ids, som=som, germ=germ, som_job=[], germ_job=[])
-        for kind in ("som", "germ"):
-            for idx in entry[kind]:
-                rows = [SeqDecoder(r) for r in encoded[idx + 1]]
-                if max(len(x) for x in rows) > 0:
-                    entry[kind + "_job"].append(len(jobs))
-                    jobs.append(rows)
-                else:
-                    entry[kind + "_job"].append(None)
-        plans.append(entry)
-    phase["labelling_s"] = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    cons = []
-    if jobs:
-        res = poa_batch(jobs, algorithm=1, genmsa=False, context=context, return_stats=stats is not None)
-        if stats is not None:
-            res, st = res
-            stats.append(("consensus_poa", st))
-        cons = [c for c, _ in res]
-    phase["consensus_s"] = time.perf_counter() - t0
-    for p in plans:
-        som_seq = [cons[j] if j is not None else "-" for j in p["som_job"]]
-        germ_seq = [cons[j] if j is not None else "-" for j in p["germ_job"]]
-        if len(som_seq) > 0 and len(p["germ"]) > 0:
-            r = records[p["w"]]
-            r[3] = ";".join(som_seq)
-            r[4] = ";".join(",".join(list(p["ids"][i])) for i in p["som"])
-            r[5] = len(som_seq)
-            r[6] = ";".join(germ_seq)
-            r[7] = ";".join(",".join(list(p["ids"][i])) for i in p["germ"])
-            r[8] = len(germ_seq)
+    _abi.check(lib.svs_decision_batch(ctx.handle, len(gated), wins, starts.ctypes.data_as(ctypes.c_void_p), blob, txt,
+                                      tag_arr.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cfg), ctypes.byref(res)),
+               "svs_decision_batch")
+    t1 = time.perf_counter()
+    try:
+        status, K, ns, ng = (ctypes.c_int32() for _ in range(4))
+        iptr = ctypes.POINTER(ctypes.c_int32)()
+        nid = ctypes.c_int32()
+        cptr = ctypes.c_void_p()
+        clen = ctypes.c_int64()
+        for k, w in enumerate(gated):
+            _abi.check(lib.svs_decision_result_window(res, k, ctypes.byref(status), ctypes.byref(K),
+                                                      ctypes.byref(ns), ctypes.byref(ng)))
+            if status.value == _abi.DEC_INDEX_ERROR:
+                raise IndexError(f"window {w}: an EM label row has no read id (the reference raises here)")
+            if status.value != _abi.DEC_EMOUTPUT:
+                continue
+            ids = windows[w][2]
+            seqs_out, ids_out = [], []
+            for c in range(ns.value + ng.value):
+                _abi.check(lib.svs_decision_result_cluster(res, k, c, ctypes.byref(iptr), ctypes.byref(nid),
+                                                           ctypes.byref(cptr), ctypes.byref(clen)))
+                seqs_out.append(ctypes.string_at(cptr, clen.value).decode("ascii"))
+                ids_out.append(",".join(str(ids[iptr[i]]) for i in range(nid.value)))
+            r = records[w]
+            r[3] = ";".join(seqs_out[:ns.value])
+            r[4] = ";".join(ids_out[:ns.value])
+            r[5] = ns.value
+            r[6] = ";".join(seqs_out[ns.value:])
+            r[7] = ";".join(ids_out[ns.value:])
+            r[8] = ng.value
             r[9] = r[9] + "|EMOutput"
-    if stats is not None:
-        phase["decision_total_s"] = time.perf_counter() - t_start
-        stats.append(("phases", phase))
+        if stats is not None:
+            st = _abi.DecisionStats()
+            _abi.check(lib.svs_decision_result_stats(res, ctypes.byref(st)))
+            d = st.as_dict()
+            stats.append(("decision_poa", d["poa"]))
+            stats.append(("phases", {"decision_call_s": t1 - t0, "format_s": time.perf_counter() - t1,
+                                     "decision_total_s": time.perf_counter() - t_start,
+                                     "features_s": d["features_ms"] / 1e3, "labelling_s": d["labelling_ms"] / 1e3,
+                                     "em_wall_s": d["em_wall_ms"] / 1e3, "em_kernel_s": d["em_kernel_ms"] / 1e3,
+                                     "em_launches": d["em_launches"], "em_windows": d["em_windows"],
+                                     "consensus_tasks": d["consensus_tasks"]}))
+    finally:
+        lib.svs_decision_result_free(res)
     return records
 
 

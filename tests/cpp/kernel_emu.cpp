@@ -7,6 +7,7 @@
 #include <chrono>
 #include <climits>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -22,6 +23,59 @@ struct Score { int32_t m, n, g, e, q, c; };
 int32_t r0e(const Score& P, int32_t j) { return j == 0 ? 0 : P.g + (j - 1) * P.e; }
 int32_t r0q(const Score& P, int32_t j) { return j == 0 ? 0 : P.q + (j - 1) * P.c; }
 int32_t r0h(const Score& P, int32_t j) { return j == 0 ? 0 : std::max(r0q(P, j), r0e(P, j)); }
+
+std::vector<int32_t> emu_traceback(const svs::RowTables& T, const std::vector<uint16_t>& tb, uint64_t LS, int32_t L,
+                                   int32_t best_row, const Score& P) {
+  std::vector<int32_t> out;
+  auto tbc = [&](int32_t row, int32_t col) -> uint32_t { return tb[static_cast<uint64_t>(row - 1) * LS + col]; };
+  auto pred_of = [&](int32_t row, uint32_t k) -> int32_t {
+    const uint32_t a = T.pstart[row - 1], b = T.pstart[row];
+    return b == a ? 0 : static_cast<int32_t>(T.pred_row[a + k]);
+  };
+  int32_t i = best_row, jj = L;
+  while (!(i == 0 && jj == 0)) {
+    int32_t pi = i, pj = jj;
+    bool el = false, eu = false;
+    if (i == 0) {
+      const int32_t Hij = r0h(P, jj);
+      const bool a = Hij == r0e(P, jj - 1) + P.e, b = Hij == r0h(P, jj - 1) + P.g;
+      const bool c = Hij == r0q(P, jj - 1) + P.c, d = Hij == r0h(P, jj - 1) + P.q;
+      if (!(a || b || c || d)) throw std::runtime_error("emu: row0 no move");
+      el = a || (!b && c);
+      pj = jj - 1;
+    } else {
+      const uint32_t code = tbc(i, jj), t = code & 3u, k = (code >> 3) & 31u;
+      if (t == 0) { pi = pred_of(i, k); pj = jj - 1; }
+      else if (t == 1) { pi = pred_of(i, k); eu = (code >> 2) & 1u; }
+      else if (t == 2) { pj = jj - 1; el = (code >> 2) & 1u; }
+      else throw std::runtime_error("emu: no move");
+    }
+    out.push_back(pi == i ? -1 : i - 1);
+    out.push_back(pj == jj ? -1 : jj - 1);
+    i = pi; jj = pj;
+    if (el) {
+      while (true) {
+        out.push_back(-1); out.push_back(jj - 1); --jj;
+        const bool stop = i == 0 ? (r0h(P, jj) + P.g == r0e(P, jj + 1) || r0h(P, jj) + P.q == r0q(P, jj + 1))
+                                 : ((tbc(i, jj + 1) >> 8) & 1u);
+        if (stop) break;
+      }
+    } else if (eu) {
+      while (true) {
+        const uint32_t code = tbc(i, jj), k = (code >> 10) & 31u;
+        const bool stop = (code >> 9) & 1u;
+        const int32_t nxt = k == 31u ? 0 : pred_of(i, k);
+        out.push_back(i - 1); out.push_back(-1);
+        i = nxt;
+        if (stop || i == 0) break;
+      }
+    }
+  }
+  std::vector<int32_t> fwd(out.size());
+  const size_t n = out.size() / 2;
+  for (size_t k = 0; k < n; ++k) { fwd[2 * k] = out[2 * (n - 1 - k)]; fwd[2 * k + 1] = out[2 * (n - 1 - k) + 1]; }
+  return fwd;
+}
 
 // returns forward rank pairs
 std::vector<int32_t> emu_align(const svs::RowTables& T, const std::string& seq, const Score& P) {
@@ -143,58 +197,194 @@ std::vector<int32_t> emu_align(const svs::RowTables& T, const std::string& seq, 
       cHpre = Hpre[63]; cQ = Q[63]; cE = E[63]; cH = H[63];
     }
   }
-  std::vector<int32_t> out;
-  auto tbc = [&](int32_t row, int32_t col) -> uint32_t { return tb[static_cast<uint64_t>(row - 1) * LS + col]; };
-  auto pred_of = [&](int32_t row, uint32_t k) -> int32_t {
-    const uint32_t a = T.pstart[row - 1], b = T.pstart[row];
-    return b == a ? 0 : static_cast<int32_t>(T.pred_row[a + k]);
-  };
-  int32_t i = best_row, jj = L;
-  while (!(i == 0 && jj == 0)) {
-    int32_t pi = i, pj = jj;
-    bool el = false, eu = false;
-    if (i == 0) {
-      const int32_t Hij = r0h(P, jj);
-      const bool a = Hij == r0e(P, jj - 1) + P.e, b = Hij == r0h(P, jj - 1) + P.g;
-      const bool c = Hij == r0q(P, jj - 1) + P.c, d = Hij == r0h(P, jj - 1) + P.q;
-      if (!(a || b || c || d)) throw std::runtime_error("emu: row0 no move");
-      el = a || (!b && c);
-      pj = jj - 1;
-    } else {
-      const uint32_t code = tbc(i, jj), t = code & 3u, k = (code >> 3) & 31u;
-      if (t == 0) { pi = pred_of(i, k); pj = jj - 1; }
-      else if (t == 1) { pi = pred_of(i, k); eu = (code >> 2) & 1u; }
-      else if (t == 2) { pj = jj - 1; el = (code >> 2) & 1u; }
-      else throw std::runtime_error("emu: no move");
-    }
-    out.push_back(pi == i ? -1 : i - 1);
-    out.push_back(pj == jj ? -1 : jj - 1);
-    i = pi; jj = pj;
-    if (el) {
-      while (true) {
-        out.push_back(-1); out.push_back(jj - 1); --jj;
-        const bool stop = i == 0 ? (r0h(P, jj) + P.g == r0e(P, jj + 1) || r0h(P, jj) + P.q == r0q(P, jj + 1))
-                                 : ((tbc(i, jj + 1) >> 8) & 1u);
-        if (stop) break;
-      }
-    } else if (eu) {
-      while (true) {
-        const uint32_t code = tbc(i, jj), k = (code >> 10) & 31u;
-        const bool stop = (code >> 9) & 1u;
-        const int32_t nxt = k == 31u ? 0 : pred_of(i, k);
-        out.push_back(i - 1); out.push_back(-1);
-        i = nxt;
-        if (stop || i == 0) break;
-      }
-    }
-  }
-  std::vector<int32_t> fwd(out.size());
-  const size_t n = out.size() / 2;
-  for (size_t k = 0; k < n; ++k) { fwd[2 * k] = out[2 * (n - 1 - k)]; fwd[2 * k + 1] = out[2 * (n - 1 - k) + 1]; }
-  return fwd;
+  return emu_traceback(T, tb, LS, L, best_row, P);
 }
 
-struct EmuResult { std::string consensus, error; std::vector<std::string> msa; uint32_t max_slots = 0; double graph_ms = 0, dp_ms = 0; };
+// Strip-major emulation of poa_strip.hip on the export_strip_rows tables:
+// per strip, a 64-column pool with the planner's slots, register pass-through
+// for in-edges from the row just above, per-slot boundary H, and the per-row
+// carries handed from strip to strip.
+std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string& seq, const Score& P) {
+  const int32_t L = static_cast<int32_t>(seq.size());
+  const uint64_t LS = (static_cast<uint64_t>(L) + 1 + 63) / 64 * 64;
+  const uint32_t V = static_cast<uint32_t>(T.pstart.size() - 1);
+  const int32_t nstrips = static_cast<int32_t>(LS >> 6);
+  std::vector<int32_t> pool(static_cast<size_t>(T.n_slots) * 192, 0x7eadbeef), slot_ch(T.n_slots, 0x7eadbeef);
+  std::vector<int32_t> bnd(static_cast<size_t>(V) * 4 * 2, 0);
+  std::vector<uint16_t> tb(static_cast<size_t>(V) * LS);
+  std::vector<uint8_t> written(T.n_slots, 0);
+  int32_t best = NEG_INF, best_row = 0;
+  for (int32_t s = 0; s < nstrips; ++s) {
+    const bool FIRST = s == 0;
+    const int32_t j0 = s * 64;
+    int32_t* bin = bnd.data() + static_cast<size_t>((s + 1) & 1) * V * 4;
+    int32_t* bout = bnd.data() + static_cast<size_t>(s & 1) * V * 4;
+    std::fill(written.begin(), written.end(), 0);
+    for (int l = 0; l < 64; ++l) {
+      const int32_t j = j0 + l;
+      pool[l] = r0h(P, j); pool[64 + l] = j == 0 ? 0 : NEG_INF; pool[128 + l] = j == 0 ? 0 : NEG_INF;
+    }
+    slot_ch[0] = FIRST ? 0 : r0h(P, j0 - 1);
+    written[0] = 1;
+    int32_t pHv[64], pFv[64], pOv[64], pcH = 0;
+    for (uint32_t r = 0; r < V; ++r) {
+      const uint32_t* w = T.rec.data() + static_cast<size_t>(r) * svs::kRecWords;
+      const uint32_t nb = w[0] & 0xFF, np = (w[0] >> 10) & 31;
+      const bool sink = (w[0] >> 8) & 1, store = (w[0] >> 9) & 1;
+      const uint32_t own = w[1] & 0xFFFF;
+      int32_t run1, run2, cHpre, cQ, cE, cH, H0 = 0, F0 = 0, O0 = 0;
+      if (FIRST) {
+        H0 = T.col0[3 * r]; F0 = T.col0[3 * r + 1]; O0 = T.col0[3 * r + 2];
+        run1 = VNEG; run2 = VNEG; cHpre = H0; cQ = NEG_INF; cE = NEG_INF; cH = H0;
+      } else {
+        run1 = bin[4 * r]; run2 = bin[4 * r + 1]; cHpre = bin[4 * r + 2]; cH = bin[4 * r + 3];
+        cQ = (j0 - 1) * P.c + run1; cE = (j0 - 1) * P.e + run2;
+      }
+      const int32_t cH_in = cH;
+      const uint32_t npass = np ? np : 1;
+      auto slot_of = [&](uint32_t k) -> uint32_t {
+        if (np == 0) return 0;
+        if (k < svs::kInlinePreds) return (w[2 + k / 2] >> (16 * (k & 1))) & 0xFFFF;
+        return T.pred_slot[T.pstart[r] + k];
+      };
+      auto vals = [&](uint32_t k, int l, int32_t& hp, int32_t& fp, int32_t& op, int32_t& hpm) {
+        const uint32_t ps = slot_of(k);
+        int32_t fill;
+        if (ps == svs::kNoSlot) {
+          if (r == 0) throw std::runtime_error("emu strip: register in-edge on row 0");
+          hp = pHv[l]; fp = pFv[l]; op = pOv[l]; fill = pcH;
+          hpm = l == 0 ? fill : pHv[l - 1];
+        } else {
+          if (!written[ps]) throw std::runtime_error("emu strip: read of an unwritten pool slot");
+          hp = pool[ps * 192 + l]; fp = pool[ps * 192 + 64 + l]; op = pool[ps * 192 + 128 + l]; fill = slot_ch[ps];
+          hpm = l == 0 ? fill : pool[ps * 192 + l - 1];
+        }
+      };
+      int32_t Hpre[64], Fv[64], Ov[64], Hd[64];
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = j0 + l;
+        const bool c0 = FIRST && l == 0;
+        const int32_t mc = static_cast<uint8_t>(j >= 1 && j <= L ? seq[j - 1] : 0) == nb ? P.m : P.n;
+        int32_t F = VNEG, O = VNEG, D = VNEG;
+        for (uint32_t k = 0; k < npass; ++k) {
+          int32_t hp, fp, op, hpm;
+          vals(k, l, hp, fp, op, hpm);
+          F = std::max(F, std::max(hp + P.g, fp + P.e));
+          O = std::max(O, std::max(hp + P.q, op + P.c));
+          D = std::max(D, (c0 ? 0 : hpm) + mc);
+        }
+        if (c0) { F = F0; O = O0; }
+        Fv[l] = F; Ov[l] = O; Hd[l] = D;
+        Hpre[l] = c0 ? H0 : std::max(D, std::max(F, O));
+      }
+      int32_t P1[64], P2[64], Q[64], E[64], H[64], pHp[64];
+      for (int l = 0; l < 64; ++l) pHp[l] = l == 0 ? cHpre : Hpre[l - 1];
+      auto inner_of = [&](int l) { const int32_t j = j0 + l; return FIRST ? (l != 0 && j <= L) : true; };
+      for (int l = 0; l < 64; ++l) P1[l] = inner_of(l) ? pHp[l] + P.q - (j0 + l) * P.c : VNEG;
+      for (int l = 1; l < 64; ++l) P1[l] = std::max(P1[l], P1[l - 1]);
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = j0 + l;
+        const int32_t p1m = l > 0 ? P1[l - 1] : VNEG;
+        P2[l] = inner_of(l) ? std::max(pHp[l], p1m + (j - 1) * P.c) + P.g - j * P.e : VNEG;
+      }
+      for (int l = 1; l < 64; ++l) P2[l] = std::max(P2[l], P2[l - 1]);
+      const int32_t T1 = j0 > 0 ? cQ + P.g - j0 * P.e : VNEG;
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = j0 + l;
+        const int32_t T2 = l > 0 ? run1 + (j - 1) * P.c + P.g - j * P.e : VNEG;
+        Q[l] = inner_of(l) ? j * P.c + std::max(P1[l], run1) : NEG_INF;
+        E[l] = inner_of(l) ? j * P.e + std::max(std::max(P2[l], run2), std::max(T1, T2)) : NEG_INF;
+        H[l] = inner_of(l) ? std::max(Hpre[l], std::max(E[l], Q[l])) : H0;
+      }
+      int32_t pQ[64], pE[64], pH[64];
+      for (int l = 0; l < 64; ++l) {
+        pQ[l] = l == 0 ? cQ : Q[l - 1]; pE[l] = l == 0 ? cE : E[l - 1]; pH[l] = l == 0 ? cH : H[l - 1];
+      }
+      {
+        const int32_t jl = j0 + 63;
+        const int32_t T2l = run1 + (jl - 1) * P.c + P.g - jl * P.e;
+        run2 = std::max(std::max(run2, P2[63]), std::max(T1, T2l));
+        run1 = std::max(run1, P1[63]);
+        cQ = jl * P.c + run1; cE = jl * P.e + run2; cHpre = Hpre[63];
+        cH = std::max(cHpre, std::max(cE, cQ));
+      }
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = j0 + l;
+        const bool c0 = FIRST && l == 0;
+        const bool inner = inner_of(l);
+        const int32_t mc = static_cast<uint8_t>(j >= 1 && j <= L ? seq[j - 1] : 0) == nb ? P.m : P.n;
+        uint32_t dk = 31, uk = 31, ue = 0, ck = 31, cs = 0;
+        for (uint32_t k = 0; k < npass; ++k) {
+          int32_t hp, fp, op, hpm;
+          vals(k, l, hp, fp, op, hpm);
+          if (c0) hpm = 0;
+          if (inner && dk == 31 && H[l] == hpm + mc) dk = k;
+          if (uk == 31) {
+            const bool a = H[l] == fp + P.e, b = H[l] == hp + P.g, c = H[l] == op + P.c, d = H[l] == hp + P.q;
+            if (a || b || c || d) { uk = k; ue = (a || (!b && c)) ? 1 : 0; }
+          }
+          if (np != 0 && ck == 31) {
+            const bool a = Fv[l] == hp + P.g, b = Fv[l] == fp + P.e, c = Ov[l] == hp + P.q, d = Ov[l] == op + P.c;
+            if (a || b || c || d) { ck = k; cs = (a || (!b && c)) ? 1 : 0; }
+          }
+        }
+        uint32_t code;
+        if (dk != 31) code = dk << 3;
+        else if (uk != 31) code = 1u | (ue << 2) | (uk << 3);
+        else {
+          const bool a = inner && H[l] == pE[l] + P.e, b = inner && H[l] == pH[l] + P.g;
+          const bool c = inner && H[l] == pQ[l] + P.c, d = inner && H[l] == pH[l] + P.q;
+          code = (a || b || c || d) ? (2u | ((a || (!b && c)) ? 4u : 0u)) : 3u;
+        }
+        const bool lbit = inner && (pH[l] + P.g == E[l] || pH[l] + P.q == Q[l]);
+        code |= (lbit ? 1u : 0u) << 8;
+        code |= cs << 9;
+        code |= ck << 10;
+        tb[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+        if (sink && j == L && H[l] > best) { best = H[l]; best_row = static_cast<int32_t>(r) + 1; }
+      }
+      if (store) {
+        if (own == svs::kNoSlot || own == 0 || own >= T.n_slots) throw std::runtime_error("emu strip: bad own slot");
+        for (int l = 0; l < 64; ++l) {
+          pool[own * 192 + l] = H[l]; pool[own * 192 + 64 + l] = Fv[l]; pool[own * 192 + 128 + l] = Ov[l];
+        }
+        slot_ch[own] = cH_in;
+        written[own] = 1;
+      }
+      for (int l = 0; l < 64; ++l) { pHv[l] = H[l]; pFv[l] = Fv[l]; pOv[l] = Ov[l]; }
+      pcH = cH_in;
+      bout[4 * r] = run1; bout[4 * r + 1] = run2; bout[4 * r + 2] = cHpre; bout[4 * r + 3] = cH;
+    }
+  }
+  return emu_traceback(T, tb, LS, L, best_row, P);
+}
+
+struct EmuResult {
+  std::string consensus, error;
+  std::vector<std::string> msa;
+  uint32_t max_slots = 0;
+  double graph_ms = 0, dp_ms = 0;
+  // row-structure counters over every exported table (tools/row_stats.py)
+  uint64_t rows = 0, np0 = 0, np1 = 0, np2 = 0, pred_prev = 0, must_store = 0, slot_sum = 0, tables = 0;
+};
+
+void row_stats(const svs::RowTables& T, EmuResult* r) {
+  const size_t R = T.info.size();
+  std::vector<uint8_t> store(R + 1, 0);
+  for (size_t i = 0; i < R; ++i) {
+    const uint32_t a = T.pstart[i], b = T.pstart[i + 1], np = b - a;
+    r->rows += 1;
+    if (np == 0) r->np0 += 1; else if (np == 1) r->np1 += 1; else r->np2 += 1;
+    for (uint32_t k = a; k < b; ++k) {
+      const uint32_t p = T.pred_row[k];  // 1-based
+      if (p == i) r->pred_prev += 1;     // pred is the row just above (row i is 1-based i+1)
+      else if (p >= 1) store[p] = 1;
+    }
+  }
+  for (size_t i = 1; i <= R; ++i) r->must_store += store[i];
+  r->slot_sum += T.n_slots;
+  r->tables += 1;
+}
 }  // namespace
 
 extern "C" {
@@ -209,11 +399,14 @@ void* emu_poa(int n, const char* const* seqs, const int* lens, int m, int mis, i
       if (seq.empty()) continue;
       if (graph.empty()) { graph.add_alignment_nodes({}, seq); continue; }
       auto t0 = std::chrono::steady_clock::now();
-      graph.export_rows(&T);
+      const bool strip = std::getenv("EMU_STRIP") != nullptr;
+      if (strip) graph.export_strip_rows(&T);
+      else graph.export_rows(&T);
       svs::fill_col0(&T, P.g, P.e, P.q, P.c);
       auto t1 = std::chrono::steady_clock::now();
       r->max_slots = std::max(r->max_slots, T.n_slots);
-      auto aln = emu_align(T, seq, P);
+      if (!strip) row_stats(T, r);
+      auto aln = strip ? emu_align_strip(T, seq, P) : emu_align(T, seq, P);
       auto t2 = std::chrono::steady_clock::now();
       graph.add_alignment_ranks(aln, seq);
       auto t3 = std::chrono::steady_clock::now();
@@ -230,6 +423,11 @@ const char* emu_consensus(void* h) { return static_cast<EmuResult*>(h)->consensu
 int emu_msa_rows(void* h) { return static_cast<int>(static_cast<EmuResult*>(h)->msa.size()); }
 const char* emu_msa_row(void* h, int i) { return static_cast<EmuResult*>(h)->msa[i].c_str(); }
 int emu_max_slots(void* h) { return static_cast<int>(static_cast<EmuResult*>(h)->max_slots); }
+void emu_row_stats(void* h, uint64_t* out) {
+  auto* r = static_cast<EmuResult*>(h);
+  const uint64_t v[8] = {r->rows, r->np0, r->np1, r->np2, r->pred_prev, r->must_store, r->slot_sum, r->tables};
+  for (int i = 0; i < 8; ++i) out[i] = v[i];
+}
 void emu_free(void* h) { delete static_cast<EmuResult*>(h); }
 double emu_graph_ms(void* h) { return static_cast<EmuResult*>(h)->graph_ms; }
 }

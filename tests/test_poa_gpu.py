@@ -83,3 +83,31 @@ def test_genmsa_false_and_min_coverage():
     cons, msa = poa(seqs, 1, genmsa=False)
     assert msa == [] and cons == oracle_poa(seqs, 1)[0]
     assert poa(seqs, 1, min_coverage=3) == oracle_poa(seqs, 1, min_coverage=3)
+
+
+@pytest.mark.parametrize("env", [
+    {"SVS_POA_KERNEL": "rows", "SVS_POA_WPJ": "1"},
+    {"SVS_POA_KERNEL": "rows", "SVS_POA_WPJ": "2"},
+    {"SVS_POA_KERNEL": "rows", "SVS_POA_WPJ": "4"},
+    {"SVS_POA_STRIP_GLOBAL_POOL": "1"},
+])
+def test_kernel_variants_match_oracle(env):
+    """Every POA kernel variant (row-major with 1/2/4 waves per job, and the
+    strip-major kernel with its pool in global memory) gives the oracle's result."""
+    import os
+    from svscope_amd import synth
+    from svscope_amd.poa import poa_batch
+    cases = helpers.random_cases(31, 40, max_seqs=10, max_len=260, edits=20)
+    cases += [synth.make_window(w, 12, 1500)[0] for w in range(2)]
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        got = poa_batch(cases)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    for seqs, g in zip(cases, got):
+        assert g == oracle_poa(seqs, 1)

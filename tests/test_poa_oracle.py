@@ -26,9 +26,17 @@ def test_oracle_rejects_unsupported_modes():
         oracle_poa(["ACGT", "ACGT"], 0)
 
 
-@pytest.fixture(scope="module")
-def emu():
-    return helpers.build_emu()
+@pytest.fixture(scope="module", params=["rows", "strip"])
+def emu(request):
+    """The emulator in both kernel layouts: row-major tables (poa_kernels.hip)
+    and the strip-major planner with register pass-through (poa_strip.hip)."""
+    lib = helpers.build_emu()
+    if request.param == "strip":
+        os.environ["EMU_STRIP"] = "1"
+    else:
+        os.environ.pop("EMU_STRIP", None)
+    yield lib
+    os.environ.pop("EMU_STRIP", None)
 
 
 def test_emulator_matches_oracle_random(emu):

@@ -32,22 +32,61 @@ def pmc(d, cells_json=None):
     for f in find(d, "counter_collection.csv"):
         for row in csv.DictReader(open(f)):
             name = row.get("Kernel_Name", "")
-            if "poa_nw_convex" not in name:
+            if "poa_nw_convex" not in name and "poa_strip" not in name:
                 continue
-            key = row.get("Dispatch_Id")
-            per.setdefault(key, {})[row["Counter_Name"]] = float(row["Counter_Value"])
-    fetch = sum(v.get("FETCH_SIZE", 0.0) for v in per.values())
-    write = sum(v.get("WRITE_SIZE", 0.0) for v in per.values())
-    res = {"poa_dispatches": len(per), "FETCH_SIZE_kB_sum": fetch, "WRITE_SIZE_kB_sum": write}
+            key = (f, row.get("Dispatch_Id"))
+            c = per.setdefault(key, {})
+            c[row["Counter_Name"]] = c.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+    sums = {}
+    for v in per.values():
+        for k, x in v.items():
+            sums[k] = sums.get(k, 0.0) + x
+    res = {"poa_dispatches": len(per), "counter_sums": sums}
+    if "FETCH_SIZE" in sums or "WRITE_SIZE" in sums:
+        fetch = sums.get("FETCH_SIZE", 0.0) * 1024.0
+        write = sums.get("WRITE_SIZE", 0.0) * 1024.0
+        res["fetch_bytes_raw"] = fetch
+        res["fetch_bytes_corrected"] = 2.0 * fetch   # gfx950 FETCH_SIZE 1/2 under-count
+        res["write_bytes"] = write
     if cells_json and os.path.exists(cells_json):
-        cells = json.load(open(cells_json)).get("dp_cells")
-        res["dp_cells"] = cells
+        st = None
+        for line in open(cells_json):
+            line = line.strip()
+            if line.startswith("{"):
+                st = json.loads(line)
+        if st:
+            res["dp_cells"] = st["dp_cells"]
+            res["launches"] = st["launches"]
+            if "write_bytes" in res:
+                res["hbm_bytes_per_cell"] = (res["fetch_bytes_corrected"] + res["write_bytes"]) / st["dp_cells"]
     return res
+
+
+def merge(out_json, *pmc_jsons):
+    """Combine separate FETCH / WRITE passes into profiles/pmc_poa_traffic.json."""
+    fetch = write = cells = None
+    for p in pmc_jsons:
+        d = json.load(open(p))
+        if "FETCH_SIZE" in d.get("counter_sums", {}):
+            fetch = d["fetch_bytes_corrected"] / d["dp_cells"]
+            fetch_raw = d["fetch_bytes_raw"] / d["dp_cells"]
+        if "WRITE_SIZE" in d.get("counter_sums", {}):
+            write = d["write_bytes"] / d["dp_cells"]
+        cells = d.get("dp_cells", cells)
+    res = {"kernel": "poa_strip_kernel",
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; kB x 1024; "
+                     "FETCH_SIZE doubled (gfx950 under-count, MI355X_MICROARCH.md HBM section)",
+           "fetch_bytes_per_cell": fetch, "fetch_bytes_per_cell_raw": fetch_raw, "write_bytes_per_cell": write,
+           "hbm_bytes_per_cell": fetch + write, "dp_cells_profiled": cells}
+    json.dump(res, open(out_json, "w"), indent=1)
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
     mode, d = sys.argv[1], sys.argv[2]
     if mode == "stats":
         print(json.dumps(stats(d), indent=1))
+    elif mode == "merge":
+        merge(d, *sys.argv[3:])
     else:
         print(json.dumps(pmc(d, sys.argv[3] if len(sys.argv) > 3 else None), indent=1))
