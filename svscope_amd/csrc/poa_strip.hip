@@ -6,7 +6,7 @@
 // reached by the reference through `poa(seqs, 1)` at
 // /root/reference/src/DataScanner.py:206,213 and DecisionMaker.py:160,171.
 //
-// Mapping (one 64-lane wave = one job = one workgroup):
+// Mapping (one job = one workgroup of WPJ waves, WPJ in {1, 2, 4}):
 //  * the DP matrix is swept strip by strip: strip s = columns 64s .. 64s+63,
 //    lane l owning column 64s + l; within a strip all graph rows are visited in
 //    rank order;
@@ -17,8 +17,10 @@
 //    other row reads it (export_strip_rows plans slots and liveness);
 //  * the only state carried from strip s-1 to strip s is per row: the two
 //    scan carries, Hpre and H at the strip's last column (16 B), written once
-//    by lane 0 and read back as a uniform load one strip later, prefetched two
-//    rows ahead; row records (32 B) are prefetched the same way;
+//    by lane 0 and read back as a uniform load by the wave sweeping strip s,
+//    prefetched two rows ahead; row records (16 B) are prefetched the same
+//    way.  With WPJ > 1 the waves of a job sweep consecutive strips as a
+//    row-skewed pipeline (LDS progress counters);
 //  * per cell only the 16-bit traceback code goes to HBM (coalesced 128 B per
 //    strip row); the backtrack is the same lane-0 replay of spoa's order as in
 //    the row-major kernel (poa_wave.hpp).
@@ -54,15 +56,39 @@ __device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, con
 
 }  // namespace
 
-template <bool LDSP>
-__global__ __launch_bounds__(64) void poa_strip_kernel(
+// Bounded LDS-flag wait (workgroup scope); sets *err after kStripSpinLimit polls.
+constexpr long kStripSpinLimit = 1l << 26;
+__device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, int32_t* err) {
+  long n = 0;
+  int32_t v;
+  while ((v = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++n > kStripSpinLimit) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return target;
+    }
+  }
+  return v;
+}
+
+// WPJ waves per job (one job per workgroup): wave w sweeps strips w, w+WPJ,
+// ...; strip s reads the carries wave (w-1) mod WPJ left for strip s-1, which
+// it publishes every 8 rows through an LDS progress counter (workgroup-scope
+// release / acquire), so the waves form a row-skewed pipeline over strips.
+template <bool LDSP, int WPJ>
+__global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore P, const uint32_t* __restrict__ rec_all,
     const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
     const uint32_t* __restrict__ pred_slot, const int32_t* __restrict__ col0, const uint8_t* __restrict__ seqs,
     uint16_t* __restrict__ tb, int32_t* __restrict__ bnd_all, int32_t* __restrict__ gpool,
     int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
   extern __shared__ int32_t lds[];
-  const int lane = threadIdx.x;
+  __shared__ int32_t prog[WPJ];  // per wave: strip * (V + 1) + rows done, carries published
+  __shared__ int32_t s_err;
+  __shared__ int32_t s_brow[WPJ];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
   const int job_id = blockIdx.x;
   if (job_id >= n_jobs) return;
   const PoaJob J = jobs[job_id];
@@ -70,10 +96,11 @@ __global__ __launch_bounds__(64) void poa_strip_kernel(
   const uint32_t LS = J.ls;
   const uint32_t V = J.n_rows;
   const int32_t nstrips = static_cast<int32_t>(LS >> 6);
-  int32_t* __restrict__ pool;
-  if constexpr (LDSP) pool = lds;
-  else pool = gpool + J.pool_off;
-  int32_t* __restrict__ slot_ch = pool + (LDSP ? lds_slots : J.n_slots) * kSlotInts;  // per slot: H at column j0-1
+  const uint32_t nslot = LDSP ? lds_slots : J.n_slots;
+  int32_t* __restrict__ pool;  // this wave's pool: nslot x {H, F, O} x 64, then nslot boundary H
+  if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * (kSlotInts + 1);
+  else pool = gpool + J.pool_off + static_cast<uint64_t>(wave) * ((nslot * (kSlotInts + 1) + 63) / 64 * 64);
+  int32_t* __restrict__ slot_ch = pool + nslot * kSlotInts;  // per slot: H at column j0-1
   uint16_t* __restrict__ tbj = tb + J.tb_off;
   const uint32_t* __restrict__ rec = rec_all + static_cast<uint64_t>(J.rec_off) * kRecWords;
   const uint32_t* __restrict__ rps = row_pstart + J.pstart_off;
@@ -91,8 +118,11 @@ __global__ __launch_bounds__(64) void poa_strip_kernel(
     const int32_t j0 = s << 6;
     const int32_t j = j0 + lane;
     const uint8_t rc = seq[j - 1];  // seqs[seq_off - 1] is a zero pad byte (column 0)
-    const int32_t* __restrict__ bin = bnd + static_cast<uint64_t>((s + 1) & 1) * V * 4;
-    int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s & 1) * V * 4;
+    const int32_t* __restrict__ bin = bnd + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * V * 4;
+    int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * V * 4;
+    const int32_t pw = (wave + WPJ - 1) % WPJ;          // producer of strip s-1
+    const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
+    int32_t avail = -1;                                  // producer progress seen so far
     const bool write_bnd = s + 1 < nstrips;
     // virtual row 0 in slot 0
     pool[lane] = row0_h(P, j);
@@ -111,6 +141,10 @@ __global__ __launch_bounds__(64) void poa_strip_kernel(
         d.b2 = rc0[3 * rr + 2];
         d.b3 = 0;
       } else {
+        if (WPJ > 1) {
+          const int32_t need = need0 + static_cast<int32_t>(rr) + 1;
+          if (avail < need) avail = strip_wait_ge(&prog[pw], need, &s_err);
+        }
         const int4 v = *reinterpret_cast<const int4*>(bin + 4ull * rr);
         d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
       }
@@ -235,8 +269,12 @@ __global__ __launch_bounds__(64) void poa_strip_kernel(
       pF = F;
       pO = O;
       pcH = cH_in;
-      if (write_bnd && lane == 0)
-        *reinterpret_cast<int4*>(bout + 4ull * r) = make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH);
+      if (write_bnd) {
+        if (lane == 0) *reinterpret_cast<int4*>(bout + 4ull * r) = make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH);
+        if (WPJ > 1 && ((r & 7u) == 7u || r + 1 == V) && lane == 0)
+          __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
+                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
     };
 
@@ -257,18 +295,41 @@ __global__ __launch_bounds__(64) void poa_strip_kernel(
     __builtin_amdgcn_wave_barrier();
   };
 
+  if (WPJ > 1) {
+    if (lane == 0) {
+      prog[wave] = -1;
+      if (wave == 0) s_err = 0;
+    }
+    __syncthreads();
+  }
   if (V > 0) {
     using TrueT = std::integral_constant<bool, true>;
     using FalseT = std::integral_constant<bool, false>;
-    sweep(TrueT{}, 0);
-    for (int32_t s = 1; s < nstrips; ++s) sweep(FalseT{}, s);
+    for (int32_t s = wave; s < nstrips; s += WPJ) {
+      if (s == 0) sweep(TrueT{}, 0);
+      else sweep(FalseT{}, s);
+    }
   }
 
-  // make the wave's traceback-code stores visible to its own lane 0
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  // the owner of column L's strip holds the sink maximum; every wave's
+  // traceback-code stores must be visible to wave 0's lane 0
   best_row = __shfl(best_row, L & 63, 64);
+  if (WPJ > 1) {
+    if (lane == 0 && ((L >> 6) % WPJ) == wave) s_brow[wave] = best_row;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (wave != 0) return;
+    best_row = s_brow[(L >> 6) % WPJ];
+    if (s_err) {
+      if (lane == 0) aln_len[job_id] = -1;
+      return;
+    }
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
   if (lane != 0) return;
   auto tbc = [&](int32_t row, int32_t col) -> uint32_t { return tbj[static_cast<uint64_t>(row - 1) * LS + col]; };
   auto pred_of = [&](int32_t row, uint32_t k) -> int32_t {
@@ -280,16 +341,23 @@ __global__ __launch_bounds__(64) void poa_strip_kernel(
 
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   if (a.n_jobs <= 0) return hipSuccess;
-  if (a.lds_slots > 0) {
-    const size_t lds = static_cast<size_t>(a.lds_slots) * (kStripSlotBytes + 4);
-    hipLaunchKernelGGL(poa_strip_kernel<true>, dim3(a.n_jobs), dim3(64), lds, stream, a.jobs, a.n_jobs, a.score,
-                       a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.pool, a.aln,
-                       a.aln_len, a.lds_slots);
+  const int w = a.waves_per_job;
+  const bool lds_pool = a.lds_slots > 0;
+  const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * (kStripSlotBytes + 4) : 0;
+#define SVS_STRIP(LP, W)                                                                                     \
+  hipLaunchKernelGGL((poa_strip_kernel<LP, W>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, a.n_jobs, \
+                     a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.pool, \
+                     a.aln, a.aln_len, a.lds_slots)
+  if (lds_pool) {
+    if (w == 4) SVS_STRIP(true, 4);
+    else if (w == 2) SVS_STRIP(true, 2);
+    else SVS_STRIP(true, 1);
   } else {
-    hipLaunchKernelGGL(poa_strip_kernel<false>, dim3(a.n_jobs), dim3(64), 0, stream, a.jobs, a.n_jobs, a.score,
-                       a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.pool, a.aln,
-                       a.aln_len, 0u);
+    if (w == 4) SVS_STRIP(false, 4);
+    else if (w == 2) SVS_STRIP(false, 2);
+    else SVS_STRIP(false, 1);
   }
+#undef SVS_STRIP
   return hipGetLastError();
 }
 

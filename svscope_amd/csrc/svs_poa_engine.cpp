@@ -101,8 +101,8 @@ uint64_t job_bytes(const RowTables& tt, uint64_t L) {
     // traceback codes + two strip-boundary carry buffers (+ a global pool when
     // the graph needs more slots than the LDS pool holds)
     const uint64_t pool = (tt.n_slots > kStripMaxLdsSlots || strip_pool_forced_global())
-                              ? static_cast<uint64_t>(tt.n_slots) * 193 * 4 + 256 : 0;
-    return V * ls * 2 + V * 32 + pool + 256 + (V + L + 1) * 8;
+                              ? 4ull * round_up(static_cast<uint64_t>(tt.n_slots) * 193, 64) * 4 : 0;
+    return V * ls * 2 + V * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
   }
   return V * ls * 2 + static_cast<uint64_t>(tt.n_slots) * 3 * ls * 4 + (V + L + 1) * 8;
 }
@@ -116,6 +116,20 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   uint32_t max_preds = 0, max_slots = 1;
   for (size_t k = 0; k < nj; ++k) max_slots = std::max(max_slots, tasks[la.ids[k]].rows.n_slots);
   const bool lds_pool = max_slots <= kStripMaxLdsSlots && !strip_pool_forced_global();
+  // waves per job: enough strip-pipeline waves for ~4 waves per SIMD, only for
+  // reads wide enough (>= 8 strips per wave); SVS_POA_WPJ overrides
+  uint32_t min_strips = 0xFFFFFFFFu;
+  for (size_t k = 0; k < nj; ++k) {
+    const uint32_t ls = static_cast<uint32_t>(round_up(tasks[la.ids[k]].seqs[tasks[la.ids[k]].next].size() + 1, 64));
+    min_strips = std::min(min_strips, ls / 64);
+  }
+  int wpj = 1;
+  const char* we = std::getenv("SVS_POA_WPJ");
+  if (we && (std::atoi(we) == 1 || std::atoi(we) == 2 || std::atoi(we) == 4)) {
+    wpj = std::atoi(we);
+  } else {
+    while (wpj < 4 && static_cast<size_t>(wpj) * nj < 4096 && min_strips >= static_cast<uint32_t>(16 * wpj)) wpj *= 2;
+  }
   for (size_t k = 0; k < nj; ++k) {
     const auto& tt = tasks[la.ids[k]].rows;
     const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];
@@ -138,8 +152,8 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     n_pred += tt.pred_row.size();
     n_seq += J.ls + 64;
     n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
-    n_bnd += round_up(static_cast<uint64_t>(J.n_rows) * 8, 64);
-    if (!lds_pool) n_pool += round_up(static_cast<uint64_t>(J.n_slots) * 193, 64);
+    n_bnd += round_up(static_cast<uint64_t>(J.n_rows) * (J.ls / 64) * 4, 64);
+    if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 193, 64);
     n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
     max_preds = std::max(max_preds, tt.max_preds);
     st.dp_cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);
@@ -203,6 +217,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.aln = A.d_aln.as<int32_t>();
   pl.aln_len = A.d_alen.as<int32_t>();
   pl.lds_slots = lds_pool ? max_slots : 0;
+  pl.waves_per_job = wpj;
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
   SVS_HIP(launch_poa_strip(pl, A.stream));
   SVS_HIP(hipEventRecord(A.ev1, A.stream));
