@@ -6,7 +6,7 @@
 // reached by the reference through `poa(seqs, 1)` at
 // /root/reference/src/DataScanner.py:206,213 and DecisionMaker.py:160,171.
 //
-// Mapping (one job = one workgroup of WPJ waves, WPJ in {1, 2, 4}):
+// Mapping (one job = one workgroup of WPJ waves, WPJ in {1, 2, 4, 8}):
 //  * the DP matrix is swept strip by strip: strip s = columns 64s .. 64s+63,
 //    lane l owning column 64s + l; within a strip all graph rows are visited in
 //    rank order;
@@ -39,7 +39,22 @@ namespace svs {
 
 namespace {
 
-constexpr int kSlotInts = 3 * 64;  // H, F, O planes of one pool slot
+// One pool slot: 64 int32 H, then 64 uint16 D = dF | dO << 8 with
+// dF = min(H - F, tF), dO = min(H - O, tO) (see pack_fo).
+constexpr int kSlotInts = 64 + 32;
+
+// F and O enter the recurrence only through F + e (against H + g) and O + c
+// (against H + q), and F, O <= H.  So F matters only while H - F <= e - g and
+// O only while H - O <= c - q; storing the distance to H clamped at
+// tF = e - g + 1 and tO = c - q + 1 keeps every max and every equality test of
+// the recurrence and the traceback codes exact (a clamped F' = H - tF gives
+// F' + e = H + g - 1, below the H + g it is compared with, just like the true
+// F).  Halves the pool in LDS, so twice the waves fit on a CU.
+__device__ __forceinline__ uint32_t pack_fo(int32_t H, int32_t F, int32_t O, uint32_t tF, uint32_t tO) {
+  const uint32_t dF = min(static_cast<uint32_t>(H) - static_cast<uint32_t>(F), tF);
+  const uint32_t dO = min(static_cast<uint32_t>(H) - static_cast<uint32_t>(O), tO);
+  return dF | (dO << 8);
+}
 
 // Prefetched inputs of one row: its record and its carries into this strip
 // (strip 0: column-0 values H0, F0, O0 from fill_col0).
@@ -92,6 +107,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
   const int job_id = blockIdx.x;
   if (job_id >= n_jobs) return;
   const PoaJob J = jobs[job_id];
+  const uint32_t tF = static_cast<uint32_t>(P.e - P.g + 1), tO = static_cast<uint32_t>(P.c - P.q + 1);
   const int32_t L = static_cast<int32_t>(J.len);
   const uint32_t LS = J.ls;
   const uint32_t V = J.n_rows;
@@ -125,9 +141,11 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     int32_t avail = -1;                                  // producer progress seen so far
     const bool write_bnd = s + 1 < nstrips;
     // virtual row 0 in slot 0
-    pool[lane] = row0_h(P, j);
-    pool[64 + lane] = j == 0 ? 0 : SVS_NEG_INF;
-    pool[128 + lane] = j == 0 ? 0 : SVS_NEG_INF;
+    {
+      const int32_t h0 = row0_h(P, j), fo0 = j == 0 ? 0 : SVS_NEG_INF;
+      pool[lane] = h0;
+      reinterpret_cast<uint16_t*>(pool + 64)[lane] = static_cast<uint16_t>(pack_fo(h0, fo0, fo0, tF, tO));
+    }
     if (lane == 0) slot_ch[0] = FIRST ? 0 : row0_h(P, j0 - 1);
     __builtin_amdgcn_wave_barrier();
 
@@ -191,8 +209,9 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         } else {
           const int32_t* q = pool + ps * kSlotInts;
           hp = __builtin_nontemporal_load(q + lane);
-          fp = __builtin_nontemporal_load(q + 64 + lane);
-          op = __builtin_nontemporal_load(q + 128 + lane);
+          const uint32_t dd = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(q + 64) + lane);
+          fp = hp - static_cast<int32_t>(dd & 0xFFu);
+          op = hp - static_cast<int32_t>(dd >> 8);
         }
       };
       int32_t H, F, O, Q, E, prevQ, prevE, prevH;
@@ -261,8 +280,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       if (store) {
         int32_t* q = pool + own * kSlotInts;
         q[lane] = H;
-        q[64 + lane] = F;
-        q[128 + lane] = O;
+        reinterpret_cast<uint16_t*>(q + 64)[lane] = static_cast<uint16_t>(pack_fo(H, F, O, tF, tO));
         if (lane == 0) slot_ch[own] = cH_in;
       }
       pH = H;
@@ -349,11 +367,13 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
                      a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.pool, \
                      a.aln, a.aln_len, a.lds_slots)
   if (lds_pool) {
-    if (w == 4) SVS_STRIP(true, 4);
+    if (w == 8) SVS_STRIP(true, 8);
+    else if (w == 4) SVS_STRIP(true, 4);
     else if (w == 2) SVS_STRIP(true, 2);
     else SVS_STRIP(true, 1);
   } else {
-    if (w == 4) SVS_STRIP(false, 4);
+    if (w == 8) SVS_STRIP(false, 8);
+    else if (w == 4) SVS_STRIP(false, 4);
     else if (w == 2) SVS_STRIP(false, 2);
     else SVS_STRIP(false, 1);
   }

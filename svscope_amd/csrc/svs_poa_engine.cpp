@@ -38,6 +38,9 @@ void check_poa_config(const svs_poa_config& c) {
   // exactness conditions of the two-scan formulation (see poa_kernels.hip)
   if (!(c.g <= c.e && c.q <= c.c && c.g <= c.c && c.e <= c.c && c.g + c.q <= 2 * c.c))
     throw SvsError(SVS_E_UNSUPPORTED, "gap parameters outside the exact scan formulation");
+  // the strip kernel stores F and O as 8-bit distances to H clamped at e-g+1, c-q+1
+  if (c.e - c.g + 1 > 255 || c.c - c.q + 1 > 255)
+    throw SvsError(SVS_E_UNSUPPORTED, "gap parameters too far apart for the packed F/O pool");
 }
 
 namespace {
@@ -101,7 +104,7 @@ uint64_t job_bytes(const RowTables& tt, uint64_t L) {
     // traceback codes + two strip-boundary carry buffers (+ a global pool when
     // the graph needs more slots than the LDS pool holds)
     const uint64_t pool = (tt.n_slots > kStripMaxLdsSlots || strip_pool_forced_global())
-                              ? 4ull * round_up(static_cast<uint64_t>(tt.n_slots) * 193, 64) * 4 : 0;
+                              ? 8ull * round_up(static_cast<uint64_t>(tt.n_slots) * 97, 64) * 4 : 0;
     return V * ls * 2 + V * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
   }
   return V * ls * 2 + static_cast<uint64_t>(tt.n_slots) * 3 * ls * 4 + (V + L + 1) * 8;
@@ -116,8 +119,8 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   uint32_t max_preds = 0, max_slots = 1;
   for (size_t k = 0; k < nj; ++k) max_slots = std::max(max_slots, tasks[la.ids[k]].rows.n_slots);
   const bool lds_pool = max_slots <= kStripMaxLdsSlots && !strip_pool_forced_global();
-  // waves per job: enough strip-pipeline waves for ~4 waves per SIMD, only for
-  // reads wide enough (>= 8 strips per wave); SVS_POA_WPJ overrides
+  // waves per job: enough strip-pipeline waves to fill the CUs, only for reads
+  // wide enough to give every wave several strips; SVS_POA_WPJ overrides
   uint32_t min_strips = 0xFFFFFFFFu;
   for (size_t k = 0; k < nj; ++k) {
     const uint32_t ls = static_cast<uint32_t>(round_up(tasks[la.ids[k]].seqs[tasks[la.ids[k]].next].size() + 1, 64));
@@ -125,10 +128,12 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   }
   int wpj = 1;
   const char* we = std::getenv("SVS_POA_WPJ");
-  if (we && (std::atoi(we) == 1 || std::atoi(we) == 2 || std::atoi(we) == 4)) {
-    wpj = std::atoi(we);
+  const int wenv = we ? std::atoi(we) : 0;
+  if (wenv == 1 || wenv == 2 || wenv == 4 || wenv == 8) {
+    wpj = wenv;
   } else {
-    while (wpj < 4 && static_cast<size_t>(wpj) * nj < 4096 && min_strips >= static_cast<uint32_t>(16 * wpj)) wpj *= 2;
+    // ~6 waves per SIMD (1024 SIMDs); each wave keeps >= 6 strips
+    while (wpj < 8 && static_cast<size_t>(wpj) * nj < 6144 && min_strips >= static_cast<uint32_t>(6 * wpj)) wpj *= 2;
   }
   for (size_t k = 0; k < nj; ++k) {
     const auto& tt = tasks[la.ids[k]].rows;
@@ -153,7 +158,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     n_seq += J.ls + 64;
     n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
     n_bnd += round_up(static_cast<uint64_t>(J.n_rows) * (J.ls / 64) * 4, 64);
-    if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 193, 64);
+    if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 97, 64);
     n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
     max_preds = std::max(max_preds, tt.max_preds);
     st.dp_cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);

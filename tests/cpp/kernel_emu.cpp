@@ -222,7 +222,11 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
     std::fill(written.begin(), written.end(), 0);
     for (int l = 0; l < 64; ++l) {
       const int32_t j = j0 + l;
-      pool[l] = r0h(P, j); pool[64 + l] = j == 0 ? 0 : NEG_INF; pool[128 + l] = j == 0 ? 0 : NEG_INF;
+      const uint32_t tF = static_cast<uint32_t>(P.e - P.g + 1), tO = static_cast<uint32_t>(P.c - P.q + 1);
+      const int32_t h0 = r0h(P, j), fo = j == 0 ? 0 : NEG_INF;
+      pool[l] = h0;
+      pool[64 + l] = h0 - static_cast<int32_t>(std::min(static_cast<uint32_t>(h0) - static_cast<uint32_t>(fo), tF));
+      pool[128 + l] = h0 - static_cast<int32_t>(std::min(static_cast<uint32_t>(h0) - static_cast<uint32_t>(fo), tO));
     }
     slot_ch[0] = FIRST ? 0 : r0h(P, j0 - 1);
     written[0] = 1;
@@ -345,8 +349,14 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
       }
       if (store) {
         if (own == svs::kNoSlot || own == 0 || own >= T.n_slots) throw std::runtime_error("emu strip: bad own slot");
+        // the kernel keeps F, O as distances to H clamped at e-g+1 / c-q+1
+        const uint32_t tF = static_cast<uint32_t>(P.e - P.g + 1), tO = static_cast<uint32_t>(P.c - P.q + 1);
         for (int l = 0; l < 64; ++l) {
-          pool[own * 192 + l] = H[l]; pool[own * 192 + 64 + l] = Fv[l]; pool[own * 192 + 128 + l] = Ov[l];
+          const uint32_t dF = std::min(static_cast<uint32_t>(H[l]) - static_cast<uint32_t>(Fv[l]), tF);
+          const uint32_t dO = std::min(static_cast<uint32_t>(H[l]) - static_cast<uint32_t>(Ov[l]), tO);
+          pool[own * 192 + l] = H[l];
+          pool[own * 192 + 64 + l] = H[l] - static_cast<int32_t>(dF);
+          pool[own * 192 + 128 + l] = H[l] - static_cast<int32_t>(dO);
         }
         slot_ch[own] = cH_in;
         written[own] = 1;
