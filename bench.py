@@ -10,11 +10,12 @@ generator of SURVEY.md §8(d)) per GPU.  For N > 1 the script runs as one
 process per GPU under torch.distributed.run; every rank processes its own
 windows (weak scaling), time = max over ranks.  Rank 0 prints one JSON line.
 
-roofline: the dominant kernel is the POA DP (poa_nw_convex_kernel); achieved =
+roofline: the dominant kernel is the POA DP (poa_strip_kernel); achieved =
 algorithmic bytes (20 B per DP cell: the int32 H,E,F,O,Q planes of convex NW,
 SURVEY.md §8(d)) x cells per launch / mean launch time, from HIP events on the
-engine's stream.  traffic = measured HBM bytes per launch from the committed
-rocprofv3 PMC summary (profiles/), else null.
+engine's POA stream.  traffic = measured HBM bytes per DP cell from the
+committed rocprofv3 PMC summary (profiles/pmc_poa_traffic.json) x cells per
+launch, else null.
 cpu_baseline: the CPU oracle (C++ spoa restatement + numpy EM + literal
 Decision) on a bounded sample of the same windows, one process per core.
 """
@@ -67,13 +68,14 @@ def cpu_baseline(rows, cores):
                       f"(C++ spoa-NW-convex restatement, numpy EM, literal Decision); wall {wall:.1f}s"}
 
 
-def pmc_traffic():
+def pmc_traffic_per_cell():
+    """Measured HBM bytes per DP cell of the POA kernel from the committed
+    rocprofv3 PMC summary (FETCH_SIZE and WRITE_SIZE passes), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_poa_traffic.json")
     if not os.path.exists(path):
         return None
     try:
-        d = json.load(open(path))
-        return d.get("hbm_bytes_per_launch")
+        return float(json.load(open(path))["hbm_bytes_per_cell"])
     except Exception:
         return None
 
@@ -83,7 +85,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("SVS_BENCH_BATCH", "1024")))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("SVS_BENCH_BATCH", "2048")))
     ap.add_argument("--cpu-sample", type=int, default=-1, help="windows for the CPU baseline (-1 auto, 0 off)")
     ap.add_argument("--gen-procs", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
@@ -153,7 +155,8 @@ def main():
                 n_cpu = cores
             cpu = cpu_baseline(batches[W][:n_cpu], min(cores, n_cpu))
         value = total_windows / elapsed
-        traffic = pmc_traffic()
+        per_cell = pmc_traffic_per_cell()
+        traffic = round(per_cell * cells / max(1, launches)) if per_cell is not None else None
         out = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -171,7 +174,7 @@ def main():
                                    "(MSA POA + features + EM K=1..9 + consensus POA)",
                        "windows_per_step_per_gpu": B, "reads_per_window": N_READS, "ref_len": REF_LEN,
                        "parallelism": f"window shards x{world}"},
-            "roofline": {"bound": "hbm", "kernel": "poa_nw_convex_kernel",
+            "roofline": {"bound": "hbm", "kernel": "poa_strip_kernel",
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
