@@ -39,9 +39,11 @@ namespace svs {
 
 namespace {
 
-// One pool slot: 64 int32 H, then 64 uint16 D = dF | dO << 8 with
-// dF = min(H - F, tF), dO = min(H - O, tO) (see pack_fo).
-constexpr int kSlotInts = 64 + 32;
+// One pool slot: 65 int32 Hx = H at columns j0-1 .. j0+63 (so a successor
+// reads H[j] at Hx[l+1] and its diagonal H[j-1] at Hx[l], with no lane shift),
+// then 64 uint16 D = dF | dO << 8 with dF = min(H - F, tF), dO = min(H - O, tO)
+// (see pack_fo).
+constexpr int kSlotInts = 65 + 32;
 
 // F and O enter the recurrence only through F + e (against H + g) and O + c
 // (against H + q), and F, O <= H.  So F matters only while H - F <= e - g and
@@ -114,9 +116,8 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
   const int32_t nstrips = static_cast<int32_t>(LS >> 6);
   const uint32_t nslot = LDSP ? lds_slots : J.n_slots;
   int32_t* __restrict__ pool;  // this wave's pool: nslot x {H, F, O} x 64, then nslot boundary H
-  if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * (kSlotInts + 1);
-  else pool = gpool + J.pool_off + static_cast<uint64_t>(wave) * ((nslot * (kSlotInts + 1) + 63) / 64 * 64);
-  int32_t* __restrict__ slot_ch = pool + nslot * kSlotInts;  // per slot: H at column j0-1
+  if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * kSlotInts;
+  else pool = gpool + J.pool_off + static_cast<uint64_t>(wave) * ((nslot * kSlotInts + 63) / 64 * 64);
   uint16_t* __restrict__ tbj = tb + J.tb_off;
   const uint32_t* __restrict__ rec = rec_all + static_cast<uint64_t>(J.rec_off) * kRecWords;
   const uint32_t* __restrict__ rps = row_pstart + J.pstart_off;
@@ -143,10 +144,10 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     // virtual row 0 in slot 0
     {
       const int32_t h0 = row0_h(P, j), fo0 = j == 0 ? 0 : SVS_NEG_INF;
-      pool[lane] = h0;
-      reinterpret_cast<uint16_t*>(pool + 64)[lane] = static_cast<uint16_t>(pack_fo(h0, fo0, fo0, tF, tO));
+      pool[lane + 1] = h0;
+      if (lane == 0) pool[0] = FIRST ? 0 : row0_h(P, j0 - 1);
+      reinterpret_cast<uint16_t*>(pool + 65)[lane] = static_cast<uint16_t>(pack_fo(h0, fo0, fo0, tF, tO));
     }
-    if (lane == 0) slot_ch[0] = FIRST ? 0 : row0_h(P, j0 - 1);
     __builtin_amdgcn_wave_barrier();
 
     auto fetch = [&](RowIn& d, uint32_t r) {
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       }
     };
 
-    int32_t pH = 0, pF = 0, pO = 0, pcH = 0;  // the row just above (registers)
+    int32_t pH = 0, pF = 0, pO = 0, pHm = 0;  // the row just above (registers); pHm = its H[j-1]
     auto step = [&](uint32_t r, const RowIn& d) {
       const uint32_t w0 = __builtin_amdgcn_readfirstlane(d.w0);
       const uint32_t nb = w0 & 0xFFu;
@@ -192,35 +193,31 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         cr.cQ = jl * P.c + cr.run1;
         cr.cE = jl * P.e + cr.run2;
       }
-      const int32_t cH_in = cr.cH;  // H[r][j0 - 1]: the diagonal fill successors need
       const bool c0 = FIRST && lane == 0;
       const bool inner = FIRST ? (lane != 0 && j <= L) : true;
       const int32_t mc = rc == nb ? P.m : P.n;
-      // in-edge k: (H, F, O) at this strip and H at column j0-1
+      // in-edge k: H, F, O at column j and H at column j-1
       // (pool reads are nontemporal loads so that the compiler cannot merge them
       // with the register case into a select of pointers, which would force the
       // registers into scratch and every pool read onto the flat path)
-      auto pred_vals = [&](uint32_t ps, int32_t& hp, int32_t& fp, int32_t& op, int32_t& fill) {
-        const bool reg = ps == kNoSlot;
-        const int32_t fl = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(slot_ch + (reg ? 0u : ps)));
-        fill = reg ? pcH : fl;
-        if (reg) {
-          hp = pH; fp = pF; op = pO;
+      auto pred_vals = [&](uint32_t ps, int32_t& hp, int32_t& fp, int32_t& op, int32_t& hpm) {
+        if (ps == kNoSlot) {
+          hp = pH; fp = pF; op = pO; hpm = pHm;
         } else {
           const int32_t* q = pool + ps * kSlotInts;
-          hp = __builtin_nontemporal_load(q + lane);
-          const uint32_t dd = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(q + 64) + lane);
+          hpm = __builtin_nontemporal_load(q + lane);
+          hp = __builtin_nontemporal_load(q + lane + 1);
+          const uint32_t dd = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(q + 65) + lane);
           fp = hp - static_cast<int32_t>(dd & 0xFFu);
-          op = hp - static_cast<int32_t>(dd >> 8);
+          op = hp - static_cast<int32_t>((dd >> 8) & 0xFFu);
         }
       };
       int32_t H, F, O, Q, E, prevQ, prevE, prevH;
       uint32_t code;
       if (np <= 1) {
         const uint32_t ps = __builtin_amdgcn_readfirstlane(d.w2) & 0xFFFFu;  // np == 0: slot 0 (virtual row)
-        int32_t hp, fp, op, fill;
-        pred_vals(ps, hp, fp, op, fill);
-        const int32_t hpm = wave_shr1(hp, fill, lane);
+        int32_t hp, fp, op, hpm;
+        pred_vals(ps, hp, fp, op, hpm);
         F = imax(hp + P.g, fp + P.e);
         O = imax(hp + P.q, op + P.c);
         int32_t Hpre = imax(hpm + mc, imax(F, O));
@@ -246,9 +243,9 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         O = SVS_VNEG;
         int32_t Hd = SVS_VNEG;
         for (uint32_t k = 0; k < np; ++k) {
-          int32_t hp, fp, op, fill;
-          pred_vals(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hp, fp, op, fill);
-          const int32_t hpm = c0 ? 0 : wave_shr1(hp, fill, lane);
+          int32_t hp, fp, op, hpm;
+          pred_vals(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hp, fp, op, hpm);
+          if (FIRST) hpm = c0 ? 0 : hpm;
           F = imax(F, imax(hp + P.g, fp + P.e));
           O = imax(O, imax(hp + P.q, op + P.c));
           Hd = imax(Hd, hpm + mc);
@@ -258,9 +255,9 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         strip_gaps(P, lane, j, j0, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
         uint32_t diag_k = 31, up_k = 31, up_ext = 0, uc_k = 31, uc_stop = 0;
         for (uint32_t k = 0; k < np; ++k) {
-          int32_t hp, fp, op, fill;
-          pred_vals(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hp, fp, op, fill);
-          const int32_t hpm = c0 ? 0 : wave_shr1(hp, fill, lane);
+          int32_t hp, fp, op, hpm;
+          pred_vals(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hp, fp, op, hpm);
+          if (FIRST) hpm = c0 ? 0 : hpm;
           if (inner && diag_k == 31 && H == hpm + mc) diag_k = k;
           if (up_k == 31) {
             const bool a = H == fp + P.e, b = H == hp + P.g, c = H == op + P.c, dd = H == hp + P.q;
@@ -278,15 +275,17 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       }
       tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
       if (store) {
+        // Hx[l+1] = H[l], then Hx[l] = prevH[l] (= H[l-1], lane 0: H[j0-1]);
+        // the two full-wave writes agree wherever they overlap
         int32_t* q = pool + own * kSlotInts;
-        q[lane] = H;
-        reinterpret_cast<uint16_t*>(q + 64)[lane] = static_cast<uint16_t>(pack_fo(H, F, O, tF, tO));
-        if (lane == 0) slot_ch[own] = cH_in;
+        q[lane + 1] = H;
+        q[lane] = prevH;
+        reinterpret_cast<uint16_t*>(q + 65)[lane] = static_cast<uint16_t>(pack_fo(H, F, O, tF, tO));
       }
       pH = H;
       pF = F;
       pO = O;
-      pcH = cH_in;
+      pHm = prevH;
       if (write_bnd) {
         if (lane == 0) *reinterpret_cast<int4*>(bout + 4ull * r) = make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH);
         if (WPJ > 1 && ((r & 7u) == 7u || r + 1 == V) && lane == 0)
@@ -361,7 +360,7 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   if (a.n_jobs <= 0) return hipSuccess;
   const int w = a.waves_per_job;
   const bool lds_pool = a.lds_slots > 0;
-  const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * (kStripSlotBytes + 4) : 0;
+  const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * kStripSlotBytes : 0;
 #define SVS_STRIP(LP, W)                                                                                     \
   hipLaunchKernelGGL((poa_strip_kernel<LP, W>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, a.n_jobs, \
                      a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.pool, \

@@ -76,25 +76,34 @@ struct PinnedBuf {
   }
 };
 
-// Device + pinned buffers and a stream for one in-flight POA launch.
+// Device + pinned buffers for one in-flight POA launch of a task group.
+// Kernels go to the shared in-order POA stream (groups alternate on the GPU);
+// the group's own copy stream carries its H2D tables and D2H alignments, so
+// they overlap the other group's kernel.
 struct PoaArena {
   DeviceBuf d_in, d_tb, d_pool, d_aln, d_alen;
   PinnedBuf h_in, h_aln, h_alen;
-  hipStream_t stream = nullptr;  // shared, in-order: groups alternate on the GPU
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+  hipStream_t stream = nullptr;       // shared kernel stream
+  hipStream_t copy_stream = nullptr;  // this group's copies
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr, h2d = nullptr;
   PoaArena(int device, hipStream_t s) : stream(s) {
     SVS_HIP(hipSetDevice(device));
+    SVS_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
     SVS_HIP(hipEventCreate(&ev0));
     SVS_HIP(hipEventCreate(&ev1));
     SVS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    SVS_HIP(hipEventCreateWithFlags(&h2d, hipEventDisableTiming));
   }
   ~PoaArena() {
     if (stream) (void)hipStreamSynchronize(stream);
+    if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     for (DeviceBuf* b : {&d_in, &d_tb, &d_pool, &d_aln, &d_alen}) b->release();
     for (PinnedBuf* b : {&h_in, &h_aln, &h_alen}) b->release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (done) (void)hipEventDestroy(done);
+    if (h2d) (void)hipEventDestroy(h2d);
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
   }
   PoaArena(const PoaArena&) = delete;
   PoaArena& operator=(const PoaArena&) = delete;

@@ -50,9 +50,9 @@ struct PoaLaunch {
   uint32_t lds_slots;    // pool slots per wave held in LDS (max n_slots of the launch)
 };
 
-// Strip-major kernel: LDS bytes per pool slot (64 int32 H + 64 packed uint16
-// F/O distances) plus the slot's boundary H, and the largest pool kept in LDS.
-constexpr uint32_t kStripSlotBytes = 64 * 4 + 64 * 2;
+// Strip-major kernel: LDS bytes per pool slot (65 int32 H incl. the boundary
+// column + 64 packed uint16 F/O distances), and the largest pool kept in LDS.
+constexpr uint32_t kStripSlotBytes = 65 * 4 + 64 * 2;
 constexpr uint32_t kStripMaxLdsSlots = 80;
 
 constexpr uint32_t kPoaMaxSlotsMultiWave = 64;

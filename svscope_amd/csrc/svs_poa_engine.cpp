@@ -205,7 +205,9 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   A.h_aln.ensure(n_aln * 8);
   A.h_alen.ensure(nj * 4);
   char* dg = A.d_in.as<char>();
-  SVS_HIP(hipMemcpyAsync(dg, hs, off, hipMemcpyHostToDevice, A.stream));
+  SVS_HIP(hipMemcpyAsync(dg, hs, off, hipMemcpyHostToDevice, A.copy_stream));
+  SVS_HIP(hipEventRecord(A.h2d, A.copy_stream));
+  SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
   PoaLaunch pl{};
   pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
   pl.n_jobs = static_cast<int>(nj);
@@ -226,9 +228,10 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
   SVS_HIP(launch_poa_strip(pl, A.stream));
   SVS_HIP(hipEventRecord(A.ev1, A.stream));
-  SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 4, hipMemcpyDeviceToHost, A.stream));
-  SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, pl.aln, n_aln * 8, hipMemcpyDeviceToHost, A.stream));
-  SVS_HIP(hipEventRecord(A.done, A.stream));
+  SVS_HIP(hipStreamWaitEvent(A.copy_stream, A.ev1, 0));
+  SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 4, hipMemcpyDeviceToHost, A.copy_stream));
+  SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, pl.aln, n_aln * 8, hipMemcpyDeviceToHost, A.copy_stream));
+  SVS_HIP(hipEventRecord(A.done, A.copy_stream));
   st.launches += 1;
   st.alignments += nj;
   st.tb_bytes += n_tb * 2;
@@ -319,7 +322,9 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, c
   A.h_aln.ensure(n_aln * 8);
   A.h_alen.ensure(nj * 4);
   char* dg = A.d_in.as<char>();
-  SVS_HIP(hipMemcpyAsync(dg, hs, off, hipMemcpyHostToDevice, A.stream));
+  SVS_HIP(hipMemcpyAsync(dg, hs, off, hipMemcpyHostToDevice, A.copy_stream));
+  SVS_HIP(hipEventRecord(A.h2d, A.copy_stream));
+  SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
   PoaLaunch pl;
   pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
   pl.n_jobs = static_cast<int>(nj);
@@ -339,9 +344,10 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, c
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
   SVS_HIP(launch_poa_nw_convex(pl, A.stream));
   SVS_HIP(hipEventRecord(A.ev1, A.stream));
-  SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 4, hipMemcpyDeviceToHost, A.stream));
-  SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, pl.aln, n_aln * 8, hipMemcpyDeviceToHost, A.stream));
-  SVS_HIP(hipEventRecord(A.done, A.stream));
+  SVS_HIP(hipStreamWaitEvent(A.copy_stream, A.ev1, 0));
+  SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 4, hipMemcpyDeviceToHost, A.copy_stream));
+  SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, pl.aln, n_aln * 8, hipMemcpyDeviceToHost, A.copy_stream));
+  SVS_HIP(hipEventRecord(A.done, A.copy_stream));
   st.launches += 1;
   st.alignments += nj;
   st.tb_bytes += n_tb * 2;
@@ -527,7 +533,10 @@ PoaScheduler::PoaScheduler(svs_context* ctx, const svs_poa_config& cfg, svs_poa_
 }
 
 PoaScheduler::~PoaScheduler() {
-  for (auto& a : impl_->ctx->poa_arenas) (void)hipStreamSynchronize(a->stream);
+  for (auto& a : impl_->ctx->poa_arenas) {
+    (void)hipStreamSynchronize(a->stream);
+    (void)hipStreamSynchronize(a->copy_stream);
+  }
   impl_->st.host_graph_ms += impl_->host_ms;
   delete impl_;
 }
