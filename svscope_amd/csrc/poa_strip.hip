@@ -113,6 +113,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
   const int32_t L = static_cast<int32_t>(J.len);
   const uint32_t LS = J.ls;
   const uint32_t V = J.n_rows;
+  const uint32_t VP = (V + 3) & ~3u;  // carry rows per strip, padded to whole 64-B lines
   const int32_t nstrips = static_cast<int32_t>(LS >> 6);
   const uint32_t nslot = LDSP ? lds_slots : J.n_slots;
   int32_t* __restrict__ pool;  // this wave's pool: nslot x {H, F, O} x 64, then nslot boundary H
@@ -135,12 +136,13 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     const int32_t j0 = s << 6;
     const int32_t j = j0 + lane;
     const uint8_t rc = seq[j - 1];  // seqs[seq_off - 1] is a zero pad byte (column 0)
-    const int32_t* __restrict__ bin = bnd + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * V * 4;
-    int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * V * 4;
+    const int32_t* __restrict__ bin = bnd + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
+    int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
     const int32_t pw = (wave + WPJ - 1) % WPJ;          // producer of strip s-1
     const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
     int32_t avail = -1;                                  // producer progress seen so far
     const bool write_bnd = s + 1 < nstrips;
+    const bool owns_L = (L >> 6) == s;
     // virtual row 0 in slot 0
     {
       const int32_t h0 = row0_h(P, j), fo0 = j == 0 ? 0 : SVS_NEG_INF;
@@ -164,7 +166,15 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
           const int32_t need = need0 + static_cast<int32_t>(rr) + 1;
           if (avail < need) avail = strip_wait_ge(&prog[pw], need, &s_err);
         }
-        const int4 v = *reinterpret_cast<const int4*>(bin + 4ull * rr);
+        // Uniform (scalar-cache) load.  Safe: every carry line is written once
+        // per launch, by whole 64-B lines (strip blocks padded to 4 rows), and
+        // read only after its producer has finished the line (progress is
+        // published at multiples of 8 rows) and drained its stores, so no
+        // stale line can be cached.
+        // (inline asm: the compiler will not prove this load unclobbered)
+        typedef int sv4 __attribute__((ext_vector_type(4)));
+        sv4 v;
+        asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(v) : "s"(bin + 4ull * rr) : "memory");
         d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
       }
     };
@@ -179,6 +189,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       const uint32_t own = __builtin_amdgcn_readfirstlane(d.w1) & 0xFFFFu;
       int32_t H0 = 0, F0 = 0, O0 = 0;
       StripCarry cr;
+      if (!FIRST) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // carries of this row (asm s_load)
       if (FIRST) {
         H0 = __builtin_amdgcn_readfirstlane(d.b0);
         F0 = __builtin_amdgcn_readfirstlane(d.b1);
@@ -186,10 +197,10 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         cr = StripCarry{SVS_VNEG, SVS_VNEG, H0, SVS_NEG_INF, SVS_NEG_INF, H0};
       } else {
         const int32_t jl = j0 - 1;
-        cr.run1 = __builtin_amdgcn_readfirstlane(d.b0);
-        cr.run2 = __builtin_amdgcn_readfirstlane(d.b1);
-        cr.cHpre = __builtin_amdgcn_readfirstlane(d.b2);
-        cr.cH = __builtin_amdgcn_readfirstlane(d.b3);
+        cr.run1 = d.b0;
+        cr.run2 = d.b1;
+        cr.cHpre = d.b2;
+        cr.cH = d.b3;
         cr.cQ = jl * P.c + cr.run1;
         cr.cE = jl * P.e + cr.run2;
       }
@@ -227,16 +238,25 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
           Hpre = c0 ? H0 : Hpre;
         }
         strip_gaps(P, lane, j, j0, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
+        // One in-edge: F = max(hp+g, fp+e) and O = max(hp+q, op+c), so "some
+        // up move fits" (H equals one of the four) is H == max(F, O); likewise
+        // E = max(prevE+e, prevH+g), Q = max(prevQ+c, prevH+q) make "some left
+        // move fits" H == max(E, Q); and F always equals hp+g or fp+e, so the
+        // up-chain in-edge is 0 whenever there is an in-edge.  Same codes as
+        // assemble_code over the individual tests, fewer instructions.
         const bool dg = inner && H == hpm + mc;
-        const bool ua = H == fp + P.e, ub = H == hp + P.g, uc = H == op + P.c, ud = H == hp + P.q;
-        const bool va = F == hp + P.g, vb = F == fp + P.e, vc = O == hp + P.q, vd = O == op + P.c;
-        const bool vm = np != 0 && (va || vb || vc || vd);
-        const bool la = inner && H == prevE + P.e, lb = inner && H == prevH + P.g;
-        const bool lc = inner && H == prevQ + P.c, ld = inner && H == prevH + P.q;
+        const bool up = H == imax(F, O);
+        const bool ua = H == fp + P.e, ub = H == hp + P.g, uc = H == op + P.c;
+        const bool lf = inner && H == imax(E, Q);
+        const bool la = H == prevE + P.e, lb = H == prevH + P.g, lc = H == prevQ + P.c;
         const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
-        code = assemble_code(dg ? 0u : 31u, (ua || ub || uc || ud) ? 0u : 31u, (ua || (!ub && uc)) ? 1u : 0u,
-                             la || lb || lc || ld, la || (!lb && lc), lbit, vm ? 0u : 31u,
-                             (vm && (va || (!vb && vc))) ? 1u : 0u);
+        const bool va = F == hp + P.g, vb = F == fp + P.e, vc = O == hp + P.q;
+        const uint32_t upc = (ua || (!ub && uc)) ? 5u : 1u;
+        const uint32_t lfc = (la || (!lb && lc)) ? 6u : 2u;
+        code = dg ? 0u : (up ? upc : (lf ? lfc : 3u));
+        code |= lbit ? 0x100u : 0u;
+        if (np != 0) code |= (va || (!vb && vc)) ? 0x200u : 0u;
+        else code |= 31u << 10;
       } else {
         const uint32_t* __restrict__ spill = pslot + rps[r];
         F = SVS_VNEG;
@@ -292,7 +312,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
           __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
                              __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      if (sink && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
+      if (sink && owns_L && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
     };
 
     // rows in pairs with two statically named prefetch sets (no waits on
