@@ -166,15 +166,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
           const int32_t need = need0 + static_cast<int32_t>(rr) + 1;
           if (avail < need) avail = strip_wait_ge(&prog[pw], need, &s_err);
         }
-        // Uniform (scalar-cache) load.  Safe: every carry line is written once
-        // per launch, by whole 64-B lines (strip blocks padded to 4 rows), and
-        // read only after its producer has finished the line (progress is
-        // published at multiples of 8 rows) and drained its stores, so no
-        // stale line can be cached.
-        // (inline asm: the compiler will not prove this load unclobbered)
-        typedef int sv4 __attribute__((ext_vector_type(4)));
-        sv4 v;
-        asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(v) : "s"(bin + 4ull * rr) : "memory");
+        const int4 v = *reinterpret_cast<const int4*>(bin + 4ull * rr);
         d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
       }
     };
@@ -189,7 +181,6 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       const uint32_t own = __builtin_amdgcn_readfirstlane(d.w1) & 0xFFFFu;
       int32_t H0 = 0, F0 = 0, O0 = 0;
       StripCarry cr;
-      if (!FIRST) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // carries of this row (asm s_load)
       if (FIRST) {
         H0 = __builtin_amdgcn_readfirstlane(d.b0);
         F0 = __builtin_amdgcn_readfirstlane(d.b1);
@@ -197,10 +188,10 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         cr = StripCarry{SVS_VNEG, SVS_VNEG, H0, SVS_NEG_INF, SVS_NEG_INF, H0};
       } else {
         const int32_t jl = j0 - 1;
-        cr.run1 = d.b0;
-        cr.run2 = d.b1;
-        cr.cHpre = d.b2;
-        cr.cH = d.b3;
+        cr.run1 = __builtin_amdgcn_readfirstlane(d.b0);
+        cr.run2 = __builtin_amdgcn_readfirstlane(d.b1);
+        cr.cHpre = __builtin_amdgcn_readfirstlane(d.b2);
+        cr.cH = __builtin_amdgcn_readfirstlane(d.b3);
         cr.cQ = jl * P.c + cr.run1;
         cr.cE = jl * P.e + cr.run2;
       }

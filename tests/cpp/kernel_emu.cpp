@@ -344,6 +344,23 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
         code |= (lbit ? 1u : 0u) << 8;
         code |= cs << 9;
         code |= ck << 10;
+        if (np <= 1) {
+          // the kernel's fast-path formula (identities H==max(F,O), H==max(E,Q))
+          int32_t hp, fp, op, hpm;
+          vals(0, l, hp, fp, op, hpm);
+          if (c0) hpm = 0;
+          const bool dg = inner && H[l] == hpm + mc;
+          const bool up = H[l] == std::max(Fv[l], Ov[l]);
+          const bool ua = H[l] == fp + P.e, ub = H[l] == hp + P.g, uc = H[l] == op + P.c;
+          const bool lf = inner && H[l] == std::max(E[l], Q[l]);
+          const bool la = H[l] == pE[l] + P.e, lb = H[l] == pH[l] + P.g, lc = H[l] == pQ[l] + P.c;
+          const bool va = Fv[l] == hp + P.g, vb = Fv[l] == fp + P.e, vc = Ov[l] == hp + P.q;
+          uint32_t c2 = dg ? 0u : (up ? ((ua || (!ub && uc)) ? 5u : 1u) : (lf ? ((la || (!lb && lc)) ? 6u : 2u) : 3u));
+          c2 |= lbit ? 0x100u : 0u;
+          if (np != 0) c2 |= (va || (!vb && vc)) ? 0x200u : 0u;
+          else c2 |= 31u << 10;
+          if (c2 != code) throw std::runtime_error("emu strip: fast-path code formula differs");
+        }
         tb[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
         if (sink && j == L && H[l] > best) { best = H[l]; best_row = static_cast<int32_t>(r) + 1; }
       }
