@@ -137,11 +137,26 @@ struct EmShared {
   uint64_t rng_off;
 };
 
-// M-step (pitheta_updating). Returns via shared flag whether a re-init happened.
-__device__ void m_step(const EmWindow& W, int K, const uint8_t* __restrict__ x, const double* __restrict__ g,
+constexpr int kMaxK = 15;      // K = 1..max_C, max_C <= 15 (host check)
+constexpr int kMaxReads = 256;  // reads per window (host check); XT rows padded to 64
+
+// Per-workgroup LDS: gamma staged for the M-step, E-step partial sums
+// (4/chunks feature slices x N reads x K).
+struct EmLds {
+  double g[kMaxReads * kMaxK];
+  double part[kMaxReads * kMaxK];
+};
+
+__device__ __forceinline__ int read_pad(int N) { return (N + 63) & ~63; }
+
+// M-step (pitheta_updating :162-188).  One thread per feature f: its 64 read
+// symbols come from the feature-major XT row (four 16-B loads), gamma from
+// LDS; theta[k][f][a] = sum_i gamma[i,k] [x_if == a] / gsum[k] for every k,
+// and LT[(f*5 + a)*K + k] = log(clip(theta)) for the E-step's gathers.
+__device__ void m_step(const EmWindow& W, int K, const uint8_t* __restrict__ xt, const double* __restrict__ g,
                        double* __restrict__ pi, double* __restrict__ gsum, double* __restrict__ th,
                        double* __restrict__ lt, const double* __restrict__ rng, uint64_t rng_len, double eps,
-                       EmShared* sh) {
+                       EmShared* sh, EmLds* L) {
   const int N = W.n_reads, nf = W.n_feat, tid = threadIdx.x;
   if (tid < K) {
     double s = 0.0;
@@ -149,6 +164,7 @@ __device__ void m_step(const EmWindow& W, int K, const uint8_t* __restrict__ x, 
     gsum[tid] = s;
     pi[tid] = s / N;
   }
+  for (int r = tid; r < N * K; r += blockDim.x) L->g[r] = g[r];
   __syncthreads();
   if (tid == 0) {
     int bad = 0;
@@ -167,44 +183,84 @@ __device__ void m_step(const EmWindow& W, int K, const uint8_t* __restrict__ x, 
       for (int r = tid; r < K * nf; r += blockDim.x) {
         const double e0 = e[5 * r], e1 = e[5 * r + 1], e2 = e[5 * r + 2], e3 = e[5 * r + 3], e4 = e[5 * r + 4];
         const double inv = 1.0 / ((((e0 + e1) + e2) + e3) + e4);
+        const double t5[5] = {e0 * inv, e1 * inv, e2 * inv, e3 * inv, e4 * inv};
         double* t = th + 5 * static_cast<int64_t>(r);
-        t[0] = e0 * inv; t[1] = e1 * inv; t[2] = e2 * inv; t[3] = e3 * inv; t[4] = e4 * inv;
+        const int k = r / nf, f = r % nf;
+        for (int a = 0; a < 5; ++a) {
+          t[a] = t5[a];
+          lt[(static_cast<int64_t>(f) * 5 + a) * K + k] = log(clip_eps(t5[a], eps));
+        }
       }
     }
     __syncthreads();
     if (tid == 0) sh->rng_off += static_cast<uint64_t>(K) * nf * 5;
   } else {
-    for (int r = tid; r < K * nf; r += blockDim.x) {
-      const int k = r / nf, f = r % nf;
-      Acc5 acc;
-      for (int i = 0; i < N; ++i) acc.add(x[static_cast<int64_t>(i) * nf + f], g[i * K + k]);
-      double* t = th + 5 * static_cast<int64_t>(r);
-      const double d = gsum[k];
-      t[0] = acc.v0 / d; t[1] = acc.v1 / d; t[2] = acc.v2 / d; t[3] = acc.v3 / d; t[4] = acc.v4 / d;
+    const int NP = read_pad(N);
+    for (int f = tid; f < nf; f += blockDim.x) {
+      for (int k = 0; k < K; ++k) {
+        Acc5 acc;
+        // 16 reads at a time: one 16-B load of the feature row (L1-resident
+        // across the k loop), symbols unpacked from registers
+        const uint4* row = reinterpret_cast<const uint4*>(xt + static_cast<int64_t>(f) * NP);
+        for (int h = 0; h * 16 < N; ++h) {
+          const uint4 q = row[h];
+          const uint32_t xw[4] = {q.x, q.y, q.z, q.w};
+          const double* gc = L->g + (h * 16) * K + k;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (h * 16 + i < N) acc.add(static_cast<uint8_t>(xw[i >> 2] >> (8 * (i & 3))), gc[i * K]);
+        }
+        const double d = gsum[k];
+        const double t5[5] = {acc.v0 / d, acc.v1 / d, acc.v2 / d, acc.v3 / d, acc.v4 / d};
+        double* t = th + 5 * (static_cast<int64_t>(k) * nf + f);
+        for (int a = 0; a < 5; ++a) {
+          t[a] = t5[a];
+          lt[(static_cast<int64_t>(f) * 5 + a) * K + k] = log(clip_eps(t5[a], eps));
+        }
+      }
     }
   }
   __syncthreads();
-  for (int r = tid; r < K * nf * 5; r += blockDim.x) lt[r] = log(clip_eps(th[r], eps));
-  __syncthreads();
 }
 
-// E-step (gamma_updating) + the feature part of loglik, A[i,k] = sum_f log theta'[k,f,x_if].
-__device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ x, const double* __restrict__ pi,
+// E-step (gamma_updating :132-155) + the feature part of loglik,
+// A[i,k] = sum_f log theta'[k,f,x_if].  Lane = read, each of the 4 waves sums
+// a quarter of the features (gathers LT rows (f, x_if) of K contiguous
+// doubles), then the quarters are added in wave order.
+__device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xt, const double* __restrict__ pi,
                        const double* __restrict__ lt, double* __restrict__ A, double* __restrict__ M,
-                       double* __restrict__ g) {
+                       double* __restrict__ g, EmLds* L) {
   const int N = W.n_reads, nf = W.n_feat, tid = threadIdx.x;
-  for (int r = tid; r < N * K; r += blockDim.x) {
-    const int i = r / K, k = r % K;
-    Acc5 d;
-    const uint8_t* xi = x + static_cast<int64_t>(i) * nf;
-    const double* lk = lt + static_cast<int64_t>(k) * nf * 5;
-    for (int f = 0; f < nf; ++f) {
-      const uint8_t a = xi[f];
-      d.add(a, lk[5 * f + a]);
+  const int lane = tid & 63, wave = tid >> 6;
+  const int NP = read_pad(N), chunks = NP >> 6;       // 64-read chunks (1..4)
+  const int slices = 4 / chunks;                       // feature slices per chunk
+  const int chunk = wave % chunks, slice = wave / chunks;
+  const int i = chunk * 64 + lane;
+  double acc[kMaxK];
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) acc[k] = 0.0;
+  const int fs = (nf + slices - 1) / slices;
+  if (slice < slices && i < N) {
+    const int f0 = slice * fs, f1 = min(nf, f0 + fs);
+    for (int f = f0; f < f1; ++f) {
+      const int a = xt[static_cast<int64_t>(f) * NP + i];
+      const double* row = lt + (static_cast<int64_t>(f) * 5 + a) * K;
+#pragma unroll
+      for (int k = 0; k < kMaxK; ++k)
+        if (k < K) acc[k] += row[k];
     }
-    const double a_ik = (((d.v0 + d.v1) + d.v2) + d.v3) + d.v4;
+  }
+  if (slice < slices && i < N) {
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k)
+      if (k < K) L->part[(slice * N + i) * K + k] = acc[k];
+  }
+  __syncthreads();
+  for (int r = tid; r < N * K; r += blockDim.x) {
+    double a_ik = L->part[r];
+    for (int sl = 1; sl < slices; ++sl) a_ik += L->part[sl * N * K + r];
     A[r] = a_ik;
-    M[r] = a_ik + log(pi[k]);
+    M[r] = a_ik + log(pi[r % K]);
   }
   __syncthreads();
   for (int r = tid; r < N * K; r += blockDim.x) {
@@ -221,11 +277,12 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
                                                          EmConfig cfg, double* __restrict__ ws,
                                                          double* __restrict__ outd, int32_t* __restrict__ outi) {
   __shared__ EmShared sh;
+  __shared__ EmLds lds;
   const EmWindow W = wins[blockIdx.x];
   const int N = W.n_reads, nf = W.n_feat, kmax = W.kmax, tid = threadIdx.x;
   const uint8_t* x = X + W.x_off;
   const int32_t* lab = labels + W.lab_off;
-  // workspace layout (doubles): per-K theta | lt | gamma per K | pi per K | gsum | A | M | lik per K
+  // workspace layout (doubles): per-K theta | lt | gamma per K | pi per K | gsum | A | M | lik per K | XT
   double* theta_all = ws + W.ws_off;
   const int nk = kmax - 1;
   const int64_t th_total = static_cast<int64_t>(nk) * (nk + 1) / 2 * nf * 5;
@@ -237,8 +294,17 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
   double* A = gsum + 16;
   double* M = A + static_cast<int64_t>(N) * 16;
   double* lik_all = M + static_cast<int64_t>(N) * 16;
+  uint8_t* xt = reinterpret_cast<uint8_t*>(lik_all + static_cast<int64_t>(nk) * N + 8);
   double* bic = outd + W.outd_off;  // nk BICs, then N lik of the chosen K
+  // feature-major copy of the reads: XT[f][i] (row stride N rounded up to
+  // 64), pad symbol 5 for i >= N
+  const int NP = read_pad(N);
+  for (int64_t r = tid; r < static_cast<int64_t>(nf) * NP; r += blockDim.x) {
+    const int f = static_cast<int>(r / NP), i = static_cast<int>(r % NP);
+    xt[r] = i < N ? x[static_cast<int64_t>(i) * nf + f] : 5;
+  }
   if (tid == 0) { sh.rng_off = 0; sh.error = 0; sh.reinit = 0; }
+  __threadfence_block();
   __syncthreads();
   const double logN = log(static_cast<double>(N));
   for (int K = 1; K <= nk; ++K) {
@@ -252,11 +318,11 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
     for (int tries = 5; isnan(b0) && tries != 0; --tries) {
       for (int r = tid; r < N * K; r += blockDim.x) g[r] = (lk[r / K] - 1 == r % K) ? 1.0 : 0.0;
       __syncthreads();
-      m_step(W, K, x, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh);
-      e_step(W, K, x, pi, lt, A, M, g);
+      m_step(W, K, xt, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh, &lds);
+      e_step(W, K, xt, pi, lt, A, M, g, &lds);
       for (int it = 0; it < cfg.n_step; ++it) {
-        m_step(W, K, x, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh);
-        e_step(W, K, x, pi, lt, A, M, g);
+        m_step(W, K, xt, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh, &lds);
+        e_step(W, K, xt, pi, lt, A, M, g, &lds);
         for (int i = tid; i < N; i += blockDim.x) {
           double s = 0.0;
           for (int k = 0; k < K; ++k) s += (A[i * K + k] + log(clip_eps(pi[k], cfg.eps))) * g[i * K + k];

@@ -6,7 +6,7 @@
 // reached by the reference through `poa(seqs, 1)` at
 // /root/reference/src/DataScanner.py:206,213 and DecisionMaker.py:160,171.
 //
-// Mapping (one job = one workgroup of WPJ waves, WPJ in {1, 2, 4, 8}):
+// Mapping (one job = one workgroup of WPJ waves, WPJ in 1..8):
 //  * the DP matrix is swept strip by strip: strip s = columns 64s .. 64s+63,
 //    lane l owning column 64s + l; within a strip all graph rows are visited in
 //    rank order;
@@ -29,6 +29,7 @@
 // dependency chain.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <algorithm>
 #include <type_traits>
 
 #include "poa_graph.hpp"
@@ -367,6 +368,59 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
   aln_len[job_id] = poa_traceback(P, V, L, best_row, tbc, pred_of, aln + 2 * J.aln_off);
 }
 
+namespace {
+
+template <bool LP>
+const void* strip_kernel_ptr(int w) {
+  switch (w) {
+    case 8: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 8>);
+    case 7: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 7>);
+    case 6: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 6>);
+    case 5: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 5>);
+    case 4: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 4>);
+    case 3: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 3>);
+    case 2: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 2>);
+    default: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 1>);
+  }
+}
+
+}  // namespace
+
+// Waves per job for a launch: the largest WPJ (1..8, each wave keeping >= 6
+// strips) for which every job's workgroup is resident at once, from the
+// kernel's register count and the LDS its pool needs; jobs that do not all fit
+// even at WPJ = 1 run with WPJ = 1.  (Non-resident workgroups would start only
+// when others finish: a tail of whole job lengths.)
+int choose_strip_wpj(int device, size_t n_jobs, uint32_t lds_slots, uint32_t min_strips) {
+  static int n_cu = 0, lds_cu = 0;
+  if (n_cu == 0) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 1;
+    n_cu = prop.multiProcessorCount;
+    lds_cu = static_cast<int>(prop.maxSharedMemoryPerMultiProcessor);
+    if (lds_cu <= 0) lds_cu = 160 * 1024;
+  }
+  const bool lds_pool = lds_slots > 0;
+  int best = 1;
+  for (int w = 1; w <= 8; ++w) {
+    if (!lds_pool && (w & (w - 1))) continue;
+    if (w > 1 && min_strips < static_cast<uint32_t>(6 * w)) break;
+    hipFuncAttributes attr;
+    if (hipFuncGetAttributes(&attr, lds_pool ? strip_kernel_ptr<true>(w) : strip_kernel_ptr<false>(w)) != hipSuccess)
+      break;
+    const int vg = std::max(8, (attr.numRegs + 7) / 8 * 8);
+    const int waves_cu = 4 * std::min(8, 512 / vg);
+    int blocks_cu = waves_cu / w;
+    if (lds_pool) {
+      const int lds_block = w * static_cast<int>(lds_slots * kStripSlotBytes) + static_cast<int>(attr.sharedSizeBytes);
+      blocks_cu = std::min(blocks_cu, lds_cu / std::max(1, lds_block));
+    }
+    if (blocks_cu <= 0) break;
+    if (n_jobs <= static_cast<size_t>(blocks_cu) * n_cu) best = w;
+  }
+  return best;
+}
+
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   if (a.n_jobs <= 0) return hipSuccess;
   const int w = a.waves_per_job;
@@ -377,14 +431,20 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
                      a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.pool, \
                      a.aln, a.aln_len, a.lds_slots)
   if (lds_pool) {
-    if (w == 8) SVS_STRIP(true, 8);
-    else if (w == 4) SVS_STRIP(true, 4);
-    else if (w == 2) SVS_STRIP(true, 2);
-    else SVS_STRIP(true, 1);
+    switch (w) {
+      case 8: SVS_STRIP(true, 8); break;
+      case 7: SVS_STRIP(true, 7); break;
+      case 6: SVS_STRIP(true, 6); break;
+      case 5: SVS_STRIP(true, 5); break;
+      case 4: SVS_STRIP(true, 4); break;
+      case 3: SVS_STRIP(true, 3); break;
+      case 2: SVS_STRIP(true, 2); break;
+      default: SVS_STRIP(true, 1); break;
+    }
   } else {
-    if (w == 8) SVS_STRIP(false, 8);
-    else if (w == 4) SVS_STRIP(false, 4);
-    else if (w == 2) SVS_STRIP(false, 2);
+    if (w >= 8) SVS_STRIP(false, 8);
+    else if (w >= 4) SVS_STRIP(false, 4);
+    else if (w >= 2) SVS_STRIP(false, 2);
     else SVS_STRIP(false, 1);
   }
 #undef SVS_STRIP

@@ -59,6 +59,7 @@ constexpr uint32_t kPoaMaxSlotsMultiWave = 64;
 
 hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream);
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream);
+int choose_strip_wpj(int device, size_t n_jobs, uint32_t lds_slots, uint32_t min_strips);
 hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
                                 hipStream_t stream);
 

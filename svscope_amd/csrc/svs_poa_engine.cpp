@@ -129,11 +129,10 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   int wpj = 1;
   const char* we = std::getenv("SVS_POA_WPJ");
   const int wenv = we ? std::atoi(we) : 0;
-  if (wenv == 1 || wenv == 2 || wenv == 4 || wenv == 8) {
-    wpj = wenv;
+  if (wenv >= 1 && wenv <= 8) {
+    wpj = (lds_pool || (wenv & (wenv - 1)) == 0) ? wenv : 1;
   } else {
-    // ~6 waves per SIMD (1024 SIMDs); each wave keeps >= 6 strips
-    while (wpj < 8 && static_cast<size_t>(wpj) * nj < 6144 && min_strips >= static_cast<uint32_t>(6 * wpj)) wpj *= 2;
+    wpj = choose_strip_wpj(ctx->device, nj, lds_pool ? max_slots : 0, min_strips);
   }
   for (size_t k = 0; k < nj; ++k) {
     const auto& tt = tasks[la.ids[k]].rows;

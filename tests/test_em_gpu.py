@@ -67,3 +67,24 @@ def test_emcluster_signature():
     K, Xo, R, theta, gamma, pie, bics = EMCluster(X, initselection=1)
     assert K == int(gold["c05_K"]) and Xo is X
     assert theta.shape == (K, X.shape[1], 5) and gamma.shape == (X.shape[0], K) and pie.shape == (K,)
+
+
+def test_em_matches_oracle_many_reads_and_wide_windows():
+    """Windows beyond one 64-read chunk (up to the kernel's 256 reads) and a
+    config-3-sized feature matrix (64 reads x ~1600 columns)."""
+    from svscope_amd.reads_cluster import em_cluster_batch
+    rs = np.random.RandomState(7)
+    mats = []
+    for n, nf in [(65, 40), (100, 80), (200, 30), (256, 24), (64, 1600)]:
+        protos = rs.randint(0, 5, size=(2, nf))
+        X = protos[rs.randint(0, 2, size=n)]
+        flip = rs.random_sample(X.shape) < 0.08
+        X[flip] = rs.randint(0, 5, size=int(flip.sum()))
+        mats.append(X)
+    got = em_cluster_batch(mats)
+    for X, r in zip(mats, got):
+        o = em_oracle.em_cluster(X)
+        assert r["K"] == o["K"]
+        np.testing.assert_array_equal(r["Rclust"], o["Rclust"])
+        np.testing.assert_allclose(r["BICList"], o["BICList"], rtol=1e-9, atol=1e-5)
+        np.testing.assert_allclose(r["lik"], o["lik"], rtol=0, atol=1e-5)
