@@ -249,6 +249,38 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         code |= lbit ? 0x100u : 0u;
         if (np != 0) code |= (va || (!vb && vc)) ? 0x200u : 0u;
         else code |= 31u << 10;
+      } else if (!FIRST && np == 2) {
+        // Two in-edges (the common merge row), both kept in registers between
+        // the DP and the code tests.  Per in-edge k, Fk = max(hp+g, fp+e) and
+        // Ok = max(hp+q, op+c): "an up move to k fits" is H == max(Fk, Ok), and
+        // "k continues the up-gap run" is F == Fk || O == Ok (F, O, H bound
+        // every term from above off column 0, so these equal the four-way
+        // tests of the generic loop below).
+        const uint32_t w2 = __builtin_amdgcn_readfirstlane(d.w2);
+        int32_t hp0, fp0, op0, hm0, hp1, fp1, op1, hm1;
+        pred_vals(w2 & 0xFFFFu, hp0, fp0, op0, hm0);
+        pred_vals(w2 >> 16, hp1, fp1, op1, hm1);
+        const int32_t F0k = imax(hp0 + P.g, fp0 + P.e), O0k = imax(hp0 + P.q, op0 + P.c);
+        const int32_t F1k = imax(hp1 + P.g, fp1 + P.e), O1k = imax(hp1 + P.q, op1 + P.c);
+        F = imax(F0k, F1k);
+        O = imax(O0k, O1k);
+        const int32_t D0 = hm0 + mc, D1 = hm1 + mc;
+        const int32_t Hpre = imax(imax(D0, D1), imax(F, O));
+        strip_gaps(P, lane, j, j0, true, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
+        const bool up0 = H == imax(F0k, O0k), up1 = H == imax(F1k, O1k);
+        const int32_t hpu = up0 ? hp0 : hp1, fpu = up0 ? fp0 : fp1, opu = up0 ? op0 : op1;
+        const bool ua = H == fpu + P.e, ub = H == hpu + P.g, uc = H == opu + P.c;
+        const bool ch0 = F == F0k || O == O0k;
+        const int32_t hpc = ch0 ? hp0 : hp1, fpc = ch0 ? fp0 : fp1;
+        const bool va = F == hpc + P.g, vb = F == fpc + P.e, vc = O == hpc + P.q;
+        const bool lf = H == imax(E, Q);
+        const bool la = H == prevE + P.e, lb = H == prevH + P.g, lc = H == prevQ + P.c;
+        const bool lbit = prevH + P.g == E || prevH + P.q == Q;
+        const uint32_t upc = ((ua || (!ub && uc)) ? 5u : 1u) | (up0 ? 0u : 8u);
+        const uint32_t lfc = (la || (!lb && lc)) ? 6u : 2u;
+        code = H == D0 ? 0u : (H == D1 ? 8u : (up0 || up1 ? upc : (lf ? lfc : 3u)));
+        code |= lbit ? 0x100u : 0u;
+        code |= ((va || (!vb && vc)) ? 0x200u : 0u) | (ch0 ? 0u : (1u << 10));
       } else {
         const uint32_t* __restrict__ spill = pslot + rps[r];
         F = SVS_VNEG;

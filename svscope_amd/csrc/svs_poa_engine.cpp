@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -131,9 +132,15 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   const int wenv = we ? std::atoi(we) : 0;
   if (wenv >= 1 && wenv <= 8) {
     wpj = (lds_pool || (wenv & (wenv - 1)) == 0) ? wenv : 1;
-  } else {
+  } else if (std::getenv("SVS_POA_WPJ_RESIDENT")) {
     wpj = choose_strip_wpj(ctx->device, nj, lds_pool ? max_slots : 0, min_strips);
+  } else {
+    // ~6 waves per SIMD (1024 SIMDs); each wave keeps >= 6 strips.  Measured
+    // faster than keeping every workgroup resident (r01_v16): more waves per
+    // job shorten each job even when some workgroups start late.
+    while (wpj < 8 && static_cast<size_t>(wpj) * nj < 6144 && min_strips >= static_cast<uint32_t>(6 * wpj)) wpj *= 2;
   }
+  if (std::getenv("SVS_POA_DEBUG")) std::fprintf(stderr, "[svs] strip launch: %zu jobs, wpj %d, slots %u\n", nj, wpj, max_slots);
   for (size_t k = 0; k < nj; ++k) {
     const auto& tt = tasks[la.ids[k]].rows;
     const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];

@@ -361,6 +361,29 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
           else c2 |= 31u << 10;
           if (c2 != code) throw std::runtime_error("emu strip: fast-path code formula differs");
         }
+        if (np == 2 && !FIRST) {
+          // the kernel's two-in-edge formula
+          int32_t hp0, fp0, op0, hm0, hp1, fp1, op1, hm1;
+          vals(0, l, hp0, fp0, op0, hm0);
+          vals(1, l, hp1, fp1, op1, hm1);
+          const int32_t F0k = std::max(hp0 + P.g, fp0 + P.e), O0k = std::max(hp0 + P.q, op0 + P.c);
+          const int32_t F1k = std::max(hp1 + P.g, fp1 + P.e), O1k = std::max(hp1 + P.q, op1 + P.c);
+          const int32_t Fr = Fv[l], Or = Ov[l], Hh = H[l];
+          const bool up0 = Hh == std::max(F0k, O0k), up1 = Hh == std::max(F1k, O1k);
+          const int32_t hpu = up0 ? hp0 : hp1, fpu = up0 ? fp0 : fp1, opu = up0 ? op0 : op1;
+          const bool ua = Hh == fpu + P.e, ub = Hh == hpu + P.g, uc = Hh == opu + P.c;
+          const bool ch0 = Fr == F0k || Or == O0k;
+          const int32_t hpc = ch0 ? hp0 : hp1, fpc = ch0 ? fp0 : fp1;
+          const bool va = Fr == hpc + P.g, vb = Fr == fpc + P.e, vc = Or == hpc + P.q;
+          const bool lf = Hh == std::max(E[l], Q[l]);
+          const bool la = Hh == pE[l] + P.e, lb = Hh == pH[l] + P.g, lc = Hh == pQ[l] + P.c;
+          const uint32_t upc = ((ua || (!ub && uc)) ? 5u : 1u) | (up0 ? 0u : 8u);
+          const uint32_t lfc = (la || (!lb && lc)) ? 6u : 2u;
+          uint32_t c2 = Hh == hm0 + mc ? 0u : (Hh == hm1 + mc ? 8u : (up0 || up1 ? upc : (lf ? lfc : 3u)));
+          c2 |= lbit ? 0x100u : 0u;
+          c2 |= ((va || (!vb && vc)) ? 0x200u : 0u) | (ch0 ? 0u : (1u << 10));
+          if (c2 != code) throw std::runtime_error("emu strip: two-in-edge code formula differs");
+        }
         tb[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
         if (sink && j == L && H[l] > best) { best = H[l]; best_row = static_cast<int32_t>(r) + 1; }
       }
