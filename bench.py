@@ -138,6 +138,7 @@ def main():
     kms = sum(st["kernel_ms"] for st in poa_stats)
     launches = sum(st["launches"] for st in poa_stats)
     host_ms = sum(st["host_graph_ms"] for st in poa_stats)
+    wait_ms = sum(st.get("gpu_wait_ms", 0.0) for st in poa_stats)
     phases = {}
     for name, st in stats:
         if name == "phases":
@@ -183,7 +184,8 @@ def main():
             "cpu_baseline": cpu,
             "breakdown": {"poa_cells": cells, "poa_kernel_ms": round(kms, 2), "poa_launches": launches,
                           "gcups": round(cells / (kms * 1e-3) / 1e9, 3) if kms else None,
-                          "host_graph_ms": round(host_ms, 1), "em_output_windows": n_em,
+                          "host_graph_ms": round(host_ms, 1), "host_wait_for_gpu_ms": round(wait_ms, 1),
+                          "em_output_windows": n_em,
                           "phases_s": phases,
                           "em_dtype": "f64"},
         }

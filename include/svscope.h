@@ -53,6 +53,7 @@ typedef struct svs_poa_stats {
   double kernel_ms;         /* sum of per-launch durations (HIP events) */
   double host_graph_ms;     /* host graph update / export time */
   double wall_ms;
+  double gpu_wait_ms;       /* host time blocked waiting for a launch's results */
 } svs_poa_stats;
 
 /* One context per host thread; owns a HIP stream and device arenas. */

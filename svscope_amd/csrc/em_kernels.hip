@@ -227,7 +227,7 @@ __device__ void m_step(const EmWindow& W, int K, const uint8_t* __restrict__ xt,
 // A[i,k] = sum_f log theta'[k,f,x_if].  Lane = read, each of the 4 waves sums
 // a quarter of the features (gathers LT rows (f, x_if) of K contiguous
 // doubles), then the quarters are added in wave order.
-__device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xt, const double* __restrict__ pi,
+__device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xr, const double* __restrict__ pi,
                        const double* __restrict__ lt, double* __restrict__ A, double* __restrict__ M,
                        double* __restrict__ g, EmLds* L) {
   const int N = W.n_reads, nf = W.n_feat, tid = threadIdx.x;
@@ -239,15 +239,26 @@ __device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xt,
   double acc[kMaxK];
 #pragma unroll
   for (int k = 0; k < kMaxK; ++k) acc[k] = 0.0;
-  const int fs = (nf + slices - 1) / slices;
+  // feature slices in whole 16-feature blocks: one 16-B load of the read's
+  // symbols, then 16 independent LT row gathers in flight
+  const int nfp = (nf + 15) & ~15;
+  const int fs = ((nfp / 16 + slices - 1) / slices) * 16;
   if (slice < slices && i < N) {
     const int f0 = slice * fs, f1 = min(nf, f0 + fs);
-    for (int f = f0; f < f1; ++f) {
-      const int a = xt[static_cast<int64_t>(f) * NP + i];
-      const double* row = lt + (static_cast<int64_t>(f) * 5 + a) * K;
+    const uint8_t* xi = xr + static_cast<int64_t>(i) * nfp;
+    for (int c = f0; c < f1; c += 16) {
+      const uint4 q = *reinterpret_cast<const uint4*>(xi + c);
+      const uint32_t xw[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-      for (int k = 0; k < kMaxK; ++k)
-        if (k < K) acc[k] += row[k];
+      for (int b = 0; b < 16; ++b) {
+        if (c + b < f1) {
+          const int a = (xw[b >> 2] >> (8 * (b & 3))) & 0xFF;
+          const double* row = lt + (static_cast<int64_t>(c + b) * 5 + a) * K;
+#pragma unroll
+          for (int k = 0; k < kMaxK; ++k)
+            if (k < K) acc[k] += row[k];
+        }
+      }
     }
   }
   if (slice < slices && i < N) {
@@ -294,7 +305,8 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
   double* A = gsum + 16;
   double* M = A + static_cast<int64_t>(N) * 16;
   double* lik_all = M + static_cast<int64_t>(N) * 16;
-  uint8_t* xt = reinterpret_cast<uint8_t*>(lik_all + static_cast<int64_t>(nk) * N + 8);
+  uint8_t* xt = reinterpret_cast<uint8_t*>(
+      (reinterpret_cast<uintptr_t>(lik_all + static_cast<int64_t>(nk) * N) + 63) & ~static_cast<uintptr_t>(63));
   double* bic = outd + W.outd_off;  // nk BICs, then N lik of the chosen K
   // feature-major copy of the reads: XT[f][i] (row stride N rounded up to
   // 64), pad symbol 5 for i >= N
@@ -302,6 +314,13 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
   for (int64_t r = tid; r < static_cast<int64_t>(nf) * NP; r += blockDim.x) {
     const int f = static_cast<int>(r / NP), i = static_cast<int>(r % NP);
     xt[r] = i < N ? x[static_cast<int64_t>(i) * nf + f] : 5;
+  }
+  // read-major copy with rows padded to 16 features (16-B aligned loads)
+  const int nfp = (nf + 15) & ~15;
+  uint8_t* xr = xt + static_cast<int64_t>(nf) * NP;
+  for (int64_t r = tid; r < static_cast<int64_t>(N) * nfp; r += blockDim.x) {
+    const int i = static_cast<int>(r / nfp), f = static_cast<int>(r % nfp);
+    xr[r] = f < nf ? x[static_cast<int64_t>(i) * nf + f] : 0;
   }
   if (tid == 0) { sh.rng_off = 0; sh.error = 0; sh.reinit = 0; }
   __threadfence_block();
@@ -319,10 +338,10 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
       for (int r = tid; r < N * K; r += blockDim.x) g[r] = (lk[r / K] - 1 == r % K) ? 1.0 : 0.0;
       __syncthreads();
       m_step(W, K, xt, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh, &lds);
-      e_step(W, K, xt, pi, lt, A, M, g, &lds);
+      e_step(W, K, xr, pi, lt, A, M, g, &lds);
       for (int it = 0; it < cfg.n_step; ++it) {
         m_step(W, K, xt, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh, &lds);
-        e_step(W, K, xt, pi, lt, A, M, g, &lds);
+        e_step(W, K, xr, pi, lt, A, M, g, &lds);
         for (int i = tid; i < N; i += blockDim.x) {
           double s = 0.0;
           for (int k = 0; k < K; ++k) s += (A[i * K + k] + log(clip_eps(pi[k], cfg.eps))) * g[i * K + k];

@@ -365,7 +365,9 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, c
 // Waits for the launch and folds its alignments back into the graphs.
 void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_stats& st, double& host_ms) {
   PoaArena& A = *la.arena;
+  const auto tw0 = Clock::now();
   SVS_HIP(hipEventSynchronize(A.done));  // the other group's launch may still be queued behind it
+  st.gpu_wait_ms += ms_since(tw0);
   float ms = 0.f;
   SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
   st.kernel_ms += ms;
