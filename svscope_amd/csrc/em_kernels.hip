@@ -223,6 +223,36 @@ __device__ void m_step(const EmWindow& W, int K, const uint8_t* __restrict__ xt,
   __syncthreads();
 }
 
+// Sum over features [f0, f1) of LT[(f*5 + x_if)*K + k] for one read (its
+// padded read-major symbol row xi), k = 0..K-1, into out[0..K-1].
+template <int K>
+__device__ __forceinline__ void e_accumulate(const uint8_t* __restrict__ xi, const double* __restrict__ lt, int f0,
+                                             int f1, double* __restrict__ out) {
+  double acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = 0.0;
+  int c = f0;
+  for (; c + 16 <= f1; c += 16) {
+    const uint4 q = *reinterpret_cast<const uint4*>(xi + c);
+    const uint32_t xw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const int a = (xw[b >> 2] >> (8 * (b & 3))) & 0xFF;
+      const double* row = lt + (static_cast<int64_t>(c + b) * 5 + a) * K;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc[k] += row[k];
+    }
+  }
+  for (; c < f1; ++c) {
+    const int a = xi[c];
+    const double* row = lt + (static_cast<int64_t>(c) * 5 + a) * K;
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] += row[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) out[k] = acc[k];
+}
+
 // E-step (gamma_updating :132-155) + the feature part of loglik,
 // A[i,k] = sum_f log theta'[k,f,x_if].  Lane = read, each of the 4 waves sums
 // a quarter of the features (gathers LT rows (f, x_if) of K contiguous
@@ -236,35 +266,22 @@ __device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xr,
   const int slices = 4 / chunks;                       // feature slices per chunk
   const int chunk = wave % chunks, slice = wave / chunks;
   const int i = chunk * 64 + lane;
-  double acc[kMaxK];
-#pragma unroll
-  for (int k = 0; k < kMaxK; ++k) acc[k] = 0.0;
   // feature slices in whole 16-feature blocks: one 16-B load of the read's
-  // symbols, then 16 independent LT row gathers in flight
+  // symbols, then 16 x K independent LT gathers in flight (K is a template
+  // constant so the loads are not split by per-k branches)
   const int nfp = (nf + 15) & ~15;
   const int fs = ((nfp / 16 + slices - 1) / slices) * 16;
   if (slice < slices && i < N) {
     const int f0 = slice * fs, f1 = min(nf, f0 + fs);
     const uint8_t* xi = xr + static_cast<int64_t>(i) * nfp;
-    for (int c = f0; c < f1; c += 16) {
-      const uint4 q = *reinterpret_cast<const uint4*>(xi + c);
-      const uint32_t xw[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-      for (int b = 0; b < 16; ++b) {
-        if (c + b < f1) {
-          const int a = (xw[b >> 2] >> (8 * (b & 3))) & 0xFF;
-          const double* row = lt + (static_cast<int64_t>(c + b) * 5 + a) * K;
-#pragma unroll
-          for (int k = 0; k < kMaxK; ++k)
-            if (k < K) acc[k] += row[k];
-        }
-      }
+    double* out = L->part + (slice * N + i) * K;
+    switch (K) {
+#define SVS_EK(KK) case KK: e_accumulate<KK>(xi, lt, f0, f1, out); break;
+      SVS_EK(1) SVS_EK(2) SVS_EK(3) SVS_EK(4) SVS_EK(5) SVS_EK(6) SVS_EK(7) SVS_EK(8)
+      SVS_EK(9) SVS_EK(10) SVS_EK(11) SVS_EK(12) SVS_EK(13) SVS_EK(14) SVS_EK(15)
+#undef SVS_EK
+      default: break;
     }
-  }
-  if (slice < slices && i < N) {
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k)
-      if (k < K) L->part[(slice * N + i) * K + k] = acc[k];
   }
   __syncthreads();
   for (int r = tid; r < N * K; r += blockDim.x) {
