@@ -258,15 +258,14 @@ void PoaGraph::export_strip_rows(RowTables* t) const {
     const uint32_t a = t->pstart[r], b = t->pstart[r + 1];
     uint32_t* w = t->rec.data() + static_cast<size_t>(r) * kRecWords;
     w[0] = static_cast<uint8_t>(base_[node]) | (out_[node].empty() ? 0x100u : 0u) | (store ? 0x200u : 0u) |
-           ((b - a) << 10);
-    w[1] = store ? slot[r] : kNoSlot;
-    if (a == b) w[2] = 0;  // source: in-edge from the virtual row 0 (slot 0)
+           ((b - a) << 10) | ((store ? slot[r] : kNoSlot) << 16);
+    w[1] = 0;  // a source's in-edge comes from the virtual row 0 (slot 0)
     for (uint32_t k = a; k < b; ++k) {
       const uint32_t pr = t->pred_row[k] - 1;
       const uint32_t ps = (pr + 1 == r) ? kNoSlot : slot[pr];
       t->pred_slot[k] = ps;
       const uint32_t i = k - a;
-      if (i < kInlinePreds) w[2 + i / 2] |= ps << (16 * (i & 1));
+      if (i < kInlinePreds) w[1] |= ps << (16 * i);
     }
     for (uint32_t k = a; k < b; ++k) {
       const uint32_t pr = t->pred_row[k] - 1;

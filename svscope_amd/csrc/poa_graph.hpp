@@ -26,16 +26,17 @@ struct RowTables {
   uint32_t n_slots = 1;
   uint32_t max_preds = 0;
   // Strip-kernel tables (export_strip_rows): kRecWords words per row
-  //   w0: base | sink << 8 | store << 9 | np << 10
-  //   w1: own pool slot (kNoSlot: not stored)
-  //   w2, w3: 16-bit pool slots of the first kInlinePreds in-edges, kNoSlot =
-  //         "the row just above" (kept in registers); further in-edges are in
-  //         pred_slot[pstart[r] + k]
+  //   w0: base | sink << 8 | store << 9 | np << 10 | own pool slot << 16
+  //       (kNoSlot: not stored)
+  //   w1: 16-bit pool slots of in-edges 0 and 1 (rows with at most
+  //       kInlinePreds in-edges), kNoSlot = "the row just above" (kept in
+  //       registers); rows with more in-edges read all slots from
+  //       pred_slot[pstart[r] + k]
   std::vector<uint32_t> rec;
 };
 
-constexpr uint32_t kRecWords = 4;
-constexpr uint32_t kInlinePreds = 4;
+constexpr uint32_t kRecWords = 2;
+constexpr uint32_t kInlinePreds = 2;
 constexpr uint32_t kNoSlot = 0xFFFF;
 
 // Column 0 of the NW matrix depends only on the graph (gap runs down the

@@ -62,14 +62,13 @@ __device__ __forceinline__ uint32_t pack_fo(int32_t H, int32_t F, int32_t O, uin
 // Prefetched inputs of one row: its record and its carries into this strip
 // (strip 0: column-0 values H0, F0, O0 from fill_col0).
 struct RowIn {
-  uint32_t w0, w1, w2, w3;
+  uint32_t w0, w1;
   int32_t b0, b1, b2, b3;
 };
 
 __device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, const uint32_t* __restrict__ spill) {
   if (k >= kInlinePreds) return spill[k];
-  const uint32_t w = k < 2 ? d.w2 : d.w3;
-  return (w >> (16 * (k & 1))) & 0xFFFFu;
+  return (d.w1 >> (16 * k)) & 0xFFFFu;
 }
 
 }  // namespace
@@ -99,8 +98,8 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore P, const uint32_t* __restrict__ rec_all,
     const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
     const uint32_t* __restrict__ pred_slot, const int32_t* __restrict__ col0, const uint8_t* __restrict__ seqs,
-    uint16_t* __restrict__ tb, int32_t* __restrict__ bnd_all, int32_t* __restrict__ gpool,
-    int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
+    uint16_t* __restrict__ tb, int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
+    int32_t* __restrict__ gpool, int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
   extern __shared__ int32_t lds[];
   __shared__ int32_t prog[WPJ];  // per wave: strip * (V + 1) + rows done, carries published
   __shared__ int32_t s_err;
@@ -114,7 +113,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
   const int32_t L = static_cast<int32_t>(J.len);
   const uint32_t LS = J.ls;
   const uint32_t V = J.n_rows;
-  const uint32_t VP = (V + 3) & ~3u;  // carry rows per strip, padded to whole 64-B lines
+  const uint32_t VP = (V + 7) & ~7u;  // carry rows per strip, padded to whole 128-B lines
   const int32_t nstrips = static_cast<int32_t>(LS >> 6);
   const uint32_t nslot = LDSP ? lds_slots : J.n_slots;
   int32_t* __restrict__ pool;  // this wave's pool: nslot x {H, F, O} x 64, then nslot boundary H
@@ -128,6 +127,13 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
   const int32_t* __restrict__ rc0 = col0 + 3ull * J.row_off;
   const uint8_t* __restrict__ seq = seqs + J.seq_off;
   int32_t* __restrict__ bnd = bnd_all + J.bnd_off;
+  // The same carry buffer, read-only: loads through it are uniform and never
+  // clobbered by this kernel's stores (those go through bnd), so they become
+  // scalar-cache loads.  Safe because every carry line is written once per
+  // launch, by whole 128-B lines (strip blocks padded to 8 rows), and read only
+  // after its producer has finished the line (progress is published at
+  // multiples of 8 rows after a release) and drained its stores.
+  const int32_t* __restrict__ bndr = bnd_rd + J.bnd_off;
 
   int32_t best = SVS_NEG_INF;  // meaningful on the lane owning column L
   int32_t best_row = 0;
@@ -137,7 +143,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     const int32_t j0 = s << 6;
     const int32_t j = j0 + lane;
     const uint8_t rc = seq[j - 1];  // seqs[seq_off - 1] is a zero pad byte (column 0)
-    const int32_t* __restrict__ bin = bnd + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
+    const int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
     int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
     const int32_t pw = (wave + WPJ - 1) % WPJ;          // producer of strip s-1
     const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     auto fetch = [&](RowIn& d, uint32_t r) {
       const uint32_t rr = r < V ? r : V - 1;
       const uint32_t* w = rec + static_cast<uint64_t>(rr) * kRecWords;
-      d.w0 = w[0]; d.w1 = w[1]; d.w2 = w[2]; d.w3 = w[3];
+      d.w0 = w[0]; d.w1 = w[1];
       if (FIRST) {
         d.b0 = rc0[3 * rr];
         d.b1 = rc0[3 * rr + 1];
@@ -179,7 +185,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       const bool sink = (w0 >> 8) & 1u;
       const bool store = (w0 >> 9) & 1u;
       const uint32_t np = (w0 >> 10) & 31u;
-      const uint32_t own = __builtin_amdgcn_readfirstlane(d.w1) & 0xFFFFu;
+      const uint32_t own = w0 >> 16;
       int32_t H0 = 0, F0 = 0, O0 = 0;
       StripCarry cr;
       if (FIRST) {
@@ -218,7 +224,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       int32_t H, F, O, Q, E, prevQ, prevE, prevH;
       uint32_t code;
       if (np <= 1) {
-        const uint32_t ps = __builtin_amdgcn_readfirstlane(d.w2) & 0xFFFFu;  // np == 0: slot 0 (virtual row)
+        const uint32_t ps = __builtin_amdgcn_readfirstlane(d.w1) & 0xFFFFu;  // np == 0: slot 0 (virtual row)
         int32_t hp, fp, op, hpm;
         pred_vals(ps, hp, fp, op, hpm);
         F = imax(hp + P.g, fp + P.e);
@@ -256,7 +262,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         // "k continues the up-gap run" is F == Fk || O == Ok (F, O, H bound
         // every term from above off column 0, so these equal the four-way
         // tests of the generic loop below).
-        const uint32_t w2 = __builtin_amdgcn_readfirstlane(d.w2);
+        const uint32_t w2 = __builtin_amdgcn_readfirstlane(d.w1);
         int32_t hp0, fp0, op0, hm0, hp1, fp1, op1, hm1;
         pred_vals(w2 & 0xFFFFu, hp0, fp0, op0, hm0);
         pred_vals(w2 >> 16, hp1, fp1, op1, hm1);
@@ -460,8 +466,8 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * kStripSlotBytes : 0;
 #define SVS_STRIP(LP, W)                                                                                     \
   hipLaunchKernelGGL((poa_strip_kernel<LP, W>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, a.n_jobs, \
-                     a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.pool, \
-                     a.aln, a.aln_len, a.lds_slots)
+                     a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.bnd, \
+                     a.pool, a.aln, a.aln_len, a.lds_slots)
   if (lds_pool) {
     switch (w) {
       case 8: SVS_STRIP(true, 8); break;

@@ -106,7 +106,7 @@ uint64_t job_bytes(const RowTables& tt, uint64_t L) {
     // the graph needs more slots than the LDS pool holds)
     const uint64_t pool = (tt.n_slots > kStripMaxLdsSlots || strip_pool_forced_global())
                               ? 8ull * round_up(static_cast<uint64_t>(tt.n_slots) * 97, 64) * 4 : 0;
-    return V * ls * 2 + round_up(V, 4) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
+    return V * ls * 2 + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
   }
   return V * ls * 2 + static_cast<uint64_t>(tt.n_slots) * 3 * ls * 4 + (V + L + 1) * 8;
 }
@@ -163,7 +163,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     n_pred += tt.pred_row.size();
     n_seq += J.ls + 64;
     n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
-    n_bnd += round_up(round_up(J.n_rows, 4) * (J.ls / 64) * 4, 64);
+    n_bnd += round_up(round_up(J.n_rows, 8) * (J.ls / 64) * 4, 64);
     if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 97, 64);
     n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
     max_preds = std::max(max_preds, tt.max_preds);

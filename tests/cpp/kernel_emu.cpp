@@ -235,7 +235,7 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
       const uint32_t* w = T.rec.data() + static_cast<size_t>(r) * svs::kRecWords;
       const uint32_t nb = w[0] & 0xFF, np = (w[0] >> 10) & 31;
       const bool sink = (w[0] >> 8) & 1, store = (w[0] >> 9) & 1;
-      const uint32_t own = w[1] & 0xFFFF;
+      const uint32_t own = w[0] >> 16;
       int32_t run1, run2, cHpre, cQ, cE, cH, H0 = 0, F0 = 0, O0 = 0;
       if (FIRST) {
         H0 = T.col0[3 * r]; F0 = T.col0[3 * r + 1]; O0 = T.col0[3 * r + 2];
@@ -248,7 +248,7 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
       const uint32_t npass = np ? np : 1;
       auto slot_of = [&](uint32_t k) -> uint32_t {
         if (np == 0) return 0;
-        if (k < svs::kInlinePreds) return (w[2 + k / 2] >> (16 * (k & 1))) & 0xFFFF;
+        if (np <= svs::kInlinePreds) return (w[1] >> (16 * k)) & 0xFFFF;
         return T.pred_slot[T.pstart[r] + k];
       };
       auto vals = [&](uint32_t k, int l, int32_t& hp, int32_t& fp, int32_t& op, int32_t& hpm) {
