@@ -362,7 +362,12 @@ __global__ __launch_bounds__(256) void poa_nw_convex_kernel(
     const uint32_t a = rps[row - 1], b = rps[row];
     return (b == a) ? 0 : static_cast<int32_t>(prow[a + k]);
   };
-  aln_len[job_id] = poa_traceback(P, V, L, best_row, tbc, pred_of, aln + 2 * J.aln_off);
+  int32_t* __restrict__ out = aln + 2 * J.aln_off;
+  auto emit = [&](int64_t n, int32_t a, int32_t b) {
+    out[2 * n] = a;
+    out[2 * n + 1] = b;
+  };
+  aln_len[job_id] = poa_traceback(P, V, L, best_row, tbc, pred_of, emit);
 }
 
 hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream) {

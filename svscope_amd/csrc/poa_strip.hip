@@ -59,6 +59,64 @@ __device__ __forceinline__ uint32_t pack_fo(int32_t H, int32_t F, int32_t O, uin
   return dF | (dO << 8);
 }
 
+// d = (lane > 0 ? a[lane-1] : d) + b, one DPP-combined VALU op (wave_shr:1
+// leaves lane 0 unwritten; the caller preloads d with lane 0's value).
+__device__ __forceinline__ int32_t shr1_add(int32_t d, int32_t a, int32_t b) {
+  asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(a), "v"(b));
+  return d;
+}
+// d = (lane > 0 ? a[lane-1] : 0) + b (bound_ctrl: lane 0 reads zero).
+__device__ __forceinline__ int32_t shr1_add_bc(int32_t a, int32_t b) {
+  int32_t d;
+  asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+               : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+
+// Lane constants of one strip (columns j = j0 + lane, j0 > 0) for the
+// horizontal-gap scans of strip_gaps_nf.
+struct StripConst {
+  int32_t qjc;  // q - j c
+  int32_t k1;   // (g - j e) - (q - j c)
+  int32_t k2;   // (j-1) c + g - j e; lane 0: VNEG + that
+  int32_t t2b;  // (j-1) c + g - j e; lane 0: VNEG
+  int32_t jc, je, ve, vc;
+};
+
+struct GapOut {
+  int32_t Q, E, H, prevH, prevEe, prevQc;  // prevEe = E[j-1] + e, prevQc = Q[j-1] + c
+};
+
+// strip_gaps (poa_wave.hpp) for a strip after the first: every lane is an
+// inner column, and the lane shifts that feed an addition are DPP-combined
+// adds (P1's input Hpre[j-1] + q - jc, P2's P1[j-1] + (j-1)c + g - je, and the
+// E[j-1] + e / Q[j-1] + c terms of the traceback tests).  Same values.
+__device__ __forceinline__ void strip_gaps_nf(const PoaScore& P, int32_t j0, int32_t Hpre, const StripConst& K,
+                                              StripCarry& cr, GapOut& o) {
+  int32_t p1 = shr1_add(cr.cHpre + K.qjc, Hpre, K.qjc);
+  const int32_t u = p1 + K.k1;  // Hpre[j-1] + g - j e
+  p1 = wave_prefix_max(p1);
+  int32_t p2 = imax(u, shr1_add_bc(p1, K.k2));
+  p2 = wave_prefix_max(p2);
+  const int32_t T1 = cr.cQ + P.g - j0 * P.e;
+  const int32_t T2 = cr.run1 + K.t2b;
+  o.Q = K.jc + imax(p1, cr.run1);
+  o.E = K.je + imax(imax(p2, imax(cr.run2, T1)), T2);
+  o.H = imax(Hpre, imax(o.E, o.Q));
+  o.prevEe = shr1_add(cr.cE + P.e, o.E, K.ve);
+  o.prevQc = shr1_add(cr.cQ + P.c, o.Q, K.vc);
+  o.prevH = wave_shr1(o.H, cr.cH, 0);
+  const int32_t jl = j0 + 63;
+  const int32_t p1l = readlane63(p1), p2l = readlane63(p2), hl = readlane63(Hpre);
+  const int32_t T2l = cr.run1 + (jl - 1) * P.c + P.g - jl * P.e;
+  cr.run2 = imax(imax(cr.run2, p2l), imax(T1, T2l));
+  cr.run1 = imax(cr.run1, p1l);
+  cr.cQ = jl * P.c + cr.run1;
+  cr.cE = jl * P.e + cr.run2;
+  cr.cHpre = hl;
+  cr.cH = imax(hl, imax(cr.cE, cr.cQ));
+}
+
 // Prefetched inputs of one row: its record and its carries into this strip
 // (strip 0: column-0 values H0, F0, O0 from fill_col0).
 struct RowIn {
@@ -150,6 +208,18 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     int32_t avail = -1;                                  // producer progress seen so far
     const bool write_bnd = s + 1 < nstrips;
     const bool owns_L = (L >> 6) == s;
+    StripConst K;
+    if (!FIRST) {
+      const int32_t ge = P.g - j * P.e, c1 = (j - 1) * P.c;
+      K.qjc = P.q - j * P.c;
+      K.k1 = ge - K.qjc;
+      K.k2 = lane == 0 ? SVS_VNEG + c1 + ge : c1 + ge;
+      K.t2b = lane == 0 ? SVS_VNEG : c1 + ge;
+      K.jc = j * P.c;
+      K.je = j * P.e;
+      K.ve = P.e;
+      K.vc = P.c;
+    }
     // virtual row 0 in slot 0
     {
       const int32_t h0 = row0_h(P, j), fo0 = j == 0 ? 0 : SVS_NEG_INF;
@@ -221,8 +291,20 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
           op = hp - static_cast<int32_t>((dd >> 8) & 0xFFu);
         }
       };
-      int32_t H, F, O, Q, E, prevQ, prevE, prevH;
+      int32_t H, F, O, Q, E, prevH, prevEe, prevQc;  // prevEe = E[j-1] + e, prevQc = Q[j-1] + c
       uint32_t code;
+      auto gaps = [&](int32_t Hpre, bool inner_) {
+        if (FIRST) {
+          int32_t prevQ, prevE;
+          strip_gaps(P, lane, j, j0, inner_, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
+          prevEe = prevE + P.e;
+          prevQc = prevQ + P.c;
+        } else {
+          GapOut o;
+          strip_gaps_nf(P, j0, Hpre, K, cr, o);
+          Q = o.Q; E = o.E; H = o.H; prevH = o.prevH; prevEe = o.prevEe; prevQc = o.prevQc;
+        }
+      };
       if (np <= 1) {
         const uint32_t ps = __builtin_amdgcn_readfirstlane(d.w1) & 0xFFFFu;  // np == 0: slot 0 (virtual row)
         int32_t hp, fp, op, hpm;
@@ -235,7 +317,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
           O = c0 ? O0 : O;
           Hpre = c0 ? H0 : Hpre;
         }
-        strip_gaps(P, lane, j, j0, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
+        gaps(Hpre, inner);
         // One in-edge: F = max(hp+g, fp+e) and O = max(hp+q, op+c), so "some
         // up move fits" (H equals one of the four) is H == max(F, O); likewise
         // E = max(prevE+e, prevH+g), Q = max(prevQ+c, prevH+q) make "some left
@@ -246,7 +328,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         const bool up = H == imax(F, O);
         const bool ua = H == fp + P.e, ub = H == hp + P.g, uc = H == op + P.c;
         const bool lf = inner && H == imax(E, Q);
-        const bool la = H == prevE + P.e, lb = H == prevH + P.g, lc = H == prevQ + P.c;
+        const bool la = H == prevEe, lb = H == prevH + P.g, lc = H == prevQc;
         const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
         const bool va = F == hp + P.g, vb = F == fp + P.e, vc = O == hp + P.q;
         const uint32_t upc = (ua || (!ub && uc)) ? 5u : 1u;
@@ -272,7 +354,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         O = imax(O0k, O1k);
         const int32_t D0 = hm0 + mc, D1 = hm1 + mc;
         const int32_t Hpre = imax(imax(D0, D1), imax(F, O));
-        strip_gaps(P, lane, j, j0, true, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
+        gaps(Hpre, true);
         const bool up0 = H == imax(F0k, O0k), up1 = H == imax(F1k, O1k);
         const int32_t hpu = up0 ? hp0 : hp1, fpu = up0 ? fp0 : fp1, opu = up0 ? op0 : op1;
         const bool ua = H == fpu + P.e, ub = H == hpu + P.g, uc = H == opu + P.c;
@@ -280,7 +362,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         const int32_t hpc = ch0 ? hp0 : hp1, fpc = ch0 ? fp0 : fp1;
         const bool va = F == hpc + P.g, vb = F == fpc + P.e, vc = O == hpc + P.q;
         const bool lf = H == imax(E, Q);
-        const bool la = H == prevE + P.e, lb = H == prevH + P.g, lc = H == prevQ + P.c;
+        const bool la = H == prevEe, lb = H == prevH + P.g, lc = H == prevQc;
         const bool lbit = prevH + P.g == E || prevH + P.q == Q;
         const uint32_t upc = ((ua || (!ub && uc)) ? 5u : 1u) | (up0 ? 0u : 8u);
         const uint32_t lfc = (la || (!lb && lc)) ? 6u : 2u;
@@ -302,7 +384,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         }
         if (c0) { F = F0; O = O0; }
         const int32_t Hpre = c0 ? H0 : imax(Hd, imax(F, O));
-        strip_gaps(P, lane, j, j0, inner, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
+        gaps(Hpre, inner);
         uint32_t diag_k = 31, up_k = 31, up_ext = 0, uc_k = 31, uc_stop = 0;
         for (uint32_t k = 0; k < np; ++k) {
           int32_t hp, fp, op, hpm;
@@ -318,8 +400,8 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
             if (a || b || c || dd) { uc_k = k; uc_stop = (a || (!b && c)) ? 1u : 0u; }
           }
         }
-        const bool la = inner && H == prevE + P.e, lb = inner && H == prevH + P.g;
-        const bool lc = inner && H == prevQ + P.c, ld = inner && H == prevH + P.q;
+        const bool la = inner && H == prevEe, lb = inner && H == prevH + P.g;
+        const bool lc = inner && H == prevQc, ld = inner && H == prevH + P.q;
         const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
         code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k, uc_stop);
       }
@@ -397,13 +479,63 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
-  if (lane != 0) return;
-  auto tbc = [&](int32_t row, int32_t col) -> uint32_t { return tbj[static_cast<uint64_t>(row - 1) * LS + col]; };
-  auto pred_of = [&](int32_t row, uint32_t k) -> int32_t {
-    const uint32_t a = rps[row - 1], b = rps[row];
-    return (b == a) ? 0 : static_cast<int32_t>(prow[a + k]);
+  // Traceback by the whole of wave 0 in lockstep (every value it branches on
+  // is uniform).  Codes come from 16 x 16 tiles (rows r-15..r, columns
+  // c-15..c, four gathers per lane issued together) and in-edge rows 0 and 1
+  // from 64-row tiles, so the path pays one HBM round trip per tile instead of
+  // one or two per step.
+  best_row = __builtin_amdgcn_readfirstlane(best_row);
+  int32_t t_r = INT32_MIN / 2, t_c = INT32_MIN / 2, p_r = INT32_MIN / 2;
+  uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;  // element e = 64 v + lane: (t_r - e / 16, t_c - e % 16)
+  int32_t pn = 0, p0 = 0, p1 = 0;           // lane l: in-edge count and in-edges 0, 1 of row p_r - l
+  auto tbc = [&](int32_t row, int32_t col) -> uint32_t {
+    const uint32_t dr = static_cast<uint32_t>(t_r - row), dc = static_cast<uint32_t>(t_c - col);
+    if (dr >= 16u || dc >= 16u) {
+      t_r = row;
+      t_c = col;
+      const int32_t cc = col - (lane & 15), r0 = row - (lane >> 4);
+      auto ld = [&](int32_t rr) -> uint32_t {
+        return (rr >= 1 && cc >= 0) ? tbj[static_cast<uint64_t>(rr - 1) * LS + cc] : 0u;
+      };
+      t0 = ld(r0);
+      t1 = ld(r0 - 4);
+      t2 = ld(r0 - 8);
+      t3 = ld(r0 - 12);
+      return __builtin_amdgcn_readfirstlane(t0);
+    }
+    const uint32_t e = dr * 16 + dc, l = e & 63u, v = e >> 6;
+    const uint32_t x0 = __builtin_amdgcn_readlane(t0, l), x1 = __builtin_amdgcn_readlane(t1, l);
+    const uint32_t x2 = __builtin_amdgcn_readlane(t2, l), x3 = __builtin_amdgcn_readlane(t3, l);
+    return v == 0 ? x0 : (v == 1 ? x1 : (v == 2 ? x2 : x3));
   };
-  aln_len[job_id] = poa_traceback(P, V, L, best_row, tbc, pred_of, aln + 2 * J.aln_off);
+  auto pred_of = [&](int32_t row, uint32_t k) -> int32_t {
+    if (k >= 2) {
+      const uint32_t a = rps[row - 1], b = rps[row];
+      return (b == a) ? 0 : static_cast<int32_t>(prow[a + k]);
+    }
+    if (static_cast<uint32_t>(p_r - row) >= 64u) {
+      p_r = row;
+      const int32_t rr = row - lane;
+      uint32_t a = 0, b = 0;
+      if (rr >= 1) { a = rps[rr - 1]; b = rps[rr]; }
+      pn = static_cast<int32_t>(b - a);
+      p0 = pn > 0 ? static_cast<int32_t>(prow[a]) : 0;
+      p1 = pn > 1 ? static_cast<int32_t>(prow[a + 1]) : 0;
+    }
+    const uint32_t l = static_cast<uint32_t>(p_r - row);
+    const int32_t n = __builtin_amdgcn_readlane(pn, l);
+    const int32_t x = __builtin_amdgcn_readlane(k == 0 ? p0 : p1, l);
+    return n == 0 ? 0 : x;
+  };
+  int32_t* __restrict__ out = aln + 2 * J.aln_off;
+  auto emit = [&](int64_t n, int32_t a, int32_t b) {
+    if (lane == 0) {
+      out[2 * n] = a;
+      out[2 * n + 1] = b;
+    }
+  };
+  const int32_t nout = poa_traceback(P, V, L, best_row, tbc, pred_of, emit);
+  if (lane == 0) aln_len[job_id] = nout;
 }
 
 namespace {

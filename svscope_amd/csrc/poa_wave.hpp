@@ -111,11 +111,13 @@ __device__ __forceinline__ uint32_t assemble_code(uint32_t diag_k, uint32_t up_k
 // Lane-0 traceback (spoa SisdAlignmentEngine backtrack order, kNW convex)
 // from (best_row, L) to (0, 0); writes (row, pos) pairs in reverse into out.
 // tbc(row, col): traceback code of DP cell (row >= 1); pred_of(row, k): 1-based
-// DP row of in-edge k of row `row` (0 = virtual row 0).  Returns the pair
-// count, or -1 for an inconsistent path.
-template <class Tbc, class PredOf>
+// DP row of in-edge k of row `row` (0 = virtual row 0); emit(n, a, b) stores
+// pair n.  Returns the pair count, or -1 for an inconsistent path.  Control
+// flow depends only on its arguments and on tbc / pred_of results, so a whole
+// wave may run it in lockstep (the strip kernel's tile-cached codes).
+template <class Tbc, class PredOf, class Emit>
 __device__ int32_t poa_traceback(const PoaScore& P, uint32_t V, int32_t L, int32_t best_row, Tbc tbc,
-                                 PredOf pred_of, int32_t* __restrict__ out) {
+                                 PredOf pred_of, Emit emit) {
   const int64_t cap = static_cast<int64_t>(V) + L + 1;
   int64_t n = 0;
   int32_t i = best_row, jj = L;
@@ -139,16 +141,14 @@ __device__ int32_t poa_traceback(const PoaScore& P, uint32_t V, int32_t L, int32
       else { ok = false; break; }
     }
     if (n >= cap) { ok = false; break; }
-    out[2 * n] = (pi == i) ? -1 : i - 1;
-    out[2 * n + 1] = (pj == jj) ? -1 : jj - 1;
+    emit(n, (pi == i) ? -1 : i - 1, (pj == jj) ? -1 : jj - 1);
     ++n;
     i = pi;
     jj = pj;
     if (el) {
       while (true) {
         if (n >= cap || jj <= 0) { ok = false; break; }
-        out[2 * n] = -1;
-        out[2 * n + 1] = jj - 1;
+        emit(n, -1, jj - 1);
         ++n;
         --jj;
         bool stop;
@@ -166,8 +166,7 @@ __device__ int32_t poa_traceback(const PoaScore& P, uint32_t V, int32_t L, int32
         const uint32_t k = (code >> 10) & 31u;
         const bool stop = (code >> 9) & 1u;
         const int32_t nxt = (k == 31u) ? 0 : pred_of(i, k);
-        out[2 * n] = i - 1;
-        out[2 * n + 1] = -1;
+        emit(n, i - 1, -1);
         ++n;
         i = nxt;
         if (stop || i == 0) break;

@@ -83,7 +83,46 @@ struct Launch {
   std::vector<PoaJob> jobs;
   size_t n_aln = 0;
   PoaArena* arena = nullptr;
+  int wpj = 0;
+  int gid = 0;
 };
+
+// Optional timeline (SVS_POA_TRACE=<file>): one line per host phase and per
+// kernel, times in ms from the scheduler's start (kernel times placed on the
+// GPU clock through an event recorded on the kernel stream at start).
+struct PoaTrace {
+  FILE* f = nullptr;
+  Clock::time_point t0;
+  hipEvent_t e0 = nullptr;
+  void open(hipStream_t s) {
+    const char* path = std::getenv("SVS_POA_TRACE");
+    if (!path) return;
+    f = std::fopen(path, "a");
+    if (!f) return;
+    SVS_HIP(hipEventCreate(&e0));
+    SVS_HIP(hipEventRecord(e0, s));
+    t0 = Clock::now();
+    std::fprintf(f, "# begin\n");
+  }
+  double at(Clock::time_point t) const { return std::chrono::duration<double, std::milli>(t - t0).count(); }
+  void host(const char* what, int g, Clock::time_point a, size_t n) {
+    if (f) std::fprintf(f, "host %s %d %.3f %.3f %zu\n", what, g, at(a), at(Clock::now()), n);
+  }
+  void kernel(int g, hipEvent_t k0, hipEvent_t k1, size_t n, int wpj, uint64_t cells) {
+    if (!f) return;
+    float a = 0.f, b = 0.f;
+    SVS_HIP(hipEventElapsedTime(&a, e0, k0));
+    SVS_HIP(hipEventElapsedTime(&b, e0, k1));
+    std::fprintf(f, "kern %d %.3f %.3f %zu %d %llu\n", g, a, b, n, wpj, static_cast<unsigned long long>(cells));
+  }
+  void close() {
+    if (!f) return;
+    std::fclose(f);
+    f = nullptr;
+    (void)hipEventDestroy(e0);
+  }
+};
+PoaTrace g_trace;
 
 // Kernel selection: the strip-major kernel (poa_strip.hip) unless
 // SVS_POA_KERNEL=rows asks for the row-major one (poa_kernels.hip).
@@ -231,6 +270,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.aln_len = A.d_alen.as<int32_t>();
   pl.lds_slots = lds_pool ? max_slots : 0;
   pl.waves_per_job = wpj;
+  la.wpj = wpj;
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
   SVS_HIP(launch_poa_strip(pl, A.stream));
   SVS_HIP(hipEventRecord(A.ev1, A.stream));
@@ -371,6 +411,12 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   float ms = 0.f;
   SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
   st.kernel_ms += ms;
+  if (g_trace.f) {
+    uint64_t cells = 0;
+    for (const PoaJob& J : la.jobs) cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);
+    g_trace.host("wait", la.gid, tw0, la.ids.size());
+    g_trace.kernel(la.gid, A.ev0, A.ev1, la.ids.size(), la.wpj, cells);
+  }
   auto th0 = Clock::now();
   const int32_t* alen = A.h_alen.as<int32_t>();
   const int32_t* aout = A.h_aln.as<int32_t>();
@@ -388,6 +434,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
     ++t.next;
   });
   host_ms += ms_since(th0);
+  g_trace.host("fold", la.gid, th0, la.ids.size());
 }
 
 // Task group: a disjoint subset of the active tasks with its own arena.
@@ -427,11 +474,16 @@ struct PoaScheduler::Impl {
     for (int g = 0; g < 2; ++g) groups[g].arena = ctx->poa_arenas[g].get();
   }
 
-  // Moves queued tasks into the group: at most half of the queue (so the other
-  // group gets work too) and at most `cap` active tasks.
+  // Moves queued tasks into the group, up to `cap` active tasks; when the
+  // other group also has room, at most half of the queue, so that both groups
+  // start their share in the same step (staggered starts leave a tail of
+  // small launches when the tasks end).
   void refill(Group& g) {
     if (queue.empty() || g.active.size() >= cap) return;
-    size_t take = std::min(cap - g.active.size(), std::max<size_t>(1, (queue.size() + 1) / 2));
+    const Group& o = groups[1 - gid(g)];
+    const size_t room = cap - g.active.size();
+    const size_t share = o.active.size() < cap ? std::max<size_t>(1, (queue.size() + 1) / 2) : queue.size();
+    size_t take = std::min(room, share);
     while (take-- > 0 && !queue.empty()) {
       g.active.push_back(queue.front());
       queue.pop_front();
@@ -468,15 +520,19 @@ struct PoaScheduler::Impl {
       std::vector<uint32_t> ids, fin;
       for (size_t i = 0; i < g.active.size(); ++i) (needs[i] ? ids : fin).push_back(g.active[i]);
       host_ms += ms_since(th0);
+      g_trace.host("prep", gid(g), th0, g.active.size());
       g.active = ids;
       if (!fin.empty()) {
+        const auto td0 = Clock::now();
         done(fin);
-        for (uint32_t id : fin) {
-          PoaTask& t = tasks[id];
+        // graphs hold many small allocations: release them on the pool
+        ctx->pool->parallel_for(fin.size(), [&](size_t i) {
+          PoaTask& t = tasks[fin[i]];
           t.graph = PoaGraph();
           t.rows = RowTables();
           std::vector<std::string>().swap(t.seqs);
-        }
+        });
+        g_trace.host("done", gid(g), td0, fin.size());
         if (ids.empty()) continue;  // refill and try again
       }
       uint64_t total = 0;
@@ -484,7 +540,10 @@ struct PoaScheduler::Impl {
       if (total <= budget) {
         g.la.ids = std::move(ids);
         g.la.arena = g.arena;
+        g.la.gid = gid(g);
+        const auto tp0 = Clock::now();
         pack_and_launch(ctx, g.la, tasks, score, st, host_ms);
+        g_trace.host("pack", gid(g), tp0, g.la.ids.size());
         g.pending = true;
         return;
       }
@@ -502,6 +561,7 @@ struct PoaScheduler::Impl {
         Launch sub;
         sub.ids.assign(ids.begin() + first, ids.begin() + last);
         sub.arena = g.arena;
+        sub.gid = gid(g);
         pack_and_launch(ctx, sub, tasks, score, st, host_ms);
         finish(ctx, sub, tasks, st, host_ms);
         first = last;
@@ -509,7 +569,10 @@ struct PoaScheduler::Impl {
     }
   }
 
+  int gid(const Group& g) const { return static_cast<int>(&g - groups); }
+
   void run(const DoneFn& done, const PollFn& poll) {
+    g_trace.open(ctx->stream);
     for (Group& g : groups) advance(g, done);
     for (;;) {
       bool progressed = false;
@@ -520,17 +583,22 @@ struct PoaScheduler::Impl {
         advance(g, done);
         progressed = true;
       }
+      const auto tq0 = Clock::now();
       const bool outside = poll(false);
+      g_trace.host("poll", -1, tq0, 0);
       for (Group& g : groups)
         if (!g.pending && !queue.empty()) advance(g, done);
       const bool busy = groups[0].pending || groups[1].pending;
       if (progressed || busy) continue;
       if (outside) {
+        const auto tb0 = Clock::now();
         poll(true);
+        g_trace.host("block", -1, tb0, 0);
         continue;
       }
       break;
     }
+    g_trace.close();
   }
 };
 
