@@ -160,7 +160,7 @@ typedef struct svs_decision_config {
   double scutoff;      /* 0.05 */
   svs_poa_config poa;  /* poa(seqs, 1) defaults; genmsa ignored */
   svs_em_config em;    /* EMCluster defaults: max_c 9, n_step 20, seed 2023 */
-  int32_t em_batch;    /* windows per EM launch while MSAs are still running (0: 512) */
+  int32_t em_batch;    /* max windows per EM launch (0: 512); the first launch of a call takes half */
   int32_t reserved;
 } svs_decision_config;
 

@@ -9,6 +9,7 @@
 // the MSA instead of edge-label walks) and export_rows() writes the
 // rank-ordered row tables the HIP DP kernel consumes.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -33,6 +34,81 @@ struct RowTables {
   //       registers); rows with more in-edges read all slots from
   //       pred_slot[pstart[r] + k]
   std::vector<uint32_t> rec;
+};
+
+// Adjacency list of one node: up to four entries inline, more on the heap.
+// Nearly every node has one or two in/out edges and no aligned partner, so a
+// graph of thousands of nodes costs a handful of allocations instead of one or
+// two per list (those made folding and releasing graphs allocator-bound).
+class NodeList {
+ public:
+  NodeList() = default;
+  NodeList(const NodeList& o) { assign(o); }
+  NodeList(NodeList&& o) noexcept { steal(o); }
+  NodeList& operator=(const NodeList& o) {
+    if (this != &o) { release(); assign(o); }
+    return *this;
+  }
+  NodeList& operator=(NodeList&& o) noexcept {
+    if (this != &o) { release(); steal(o); }
+    return *this;
+  }
+  ~NodeList() { release(); }
+
+  uint32_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  const uint32_t* begin() const { return data(); }
+  const uint32_t* end() const { return data() + n_; }
+  uint32_t operator[](size_t i) const { return data()[i]; }
+  void push_back(uint32_t v) {
+    if (n_ == cap_) grow();
+    data()[n_++] = v;
+  }
+
+ private:
+  static constexpr uint32_t kInline = 4;
+  bool on_heap() const { return cap_ > kInline; }
+  uint32_t* data() { return on_heap() ? u_.heap : u_.inl; }
+  const uint32_t* data() const { return on_heap() ? u_.heap : u_.inl; }
+  void grow() {
+    const uint32_t cap = cap_ * 2;
+    uint32_t* h = new uint32_t[cap];
+    std::copy(data(), data() + n_, h);
+    release_heap();
+    u_.heap = h;
+    cap_ = cap;
+  }
+  void release_heap() {
+    if (on_heap()) delete[] u_.heap;
+  }
+  void release() {
+    release_heap();
+    n_ = 0;
+    cap_ = kInline;
+  }
+  void assign(const NodeList& o) {
+    n_ = 0;
+    cap_ = kInline;
+    if (o.n_ > kInline) {
+      u_.heap = new uint32_t[o.cap_];
+      cap_ = o.cap_;
+    }
+    std::copy(o.begin(), o.end(), data());
+    n_ = o.n_;
+  }
+  void steal(NodeList& o) {
+    n_ = o.n_;
+    cap_ = o.cap_;
+    if (o.on_heap()) u_.heap = o.u_.heap;
+    else std::copy(o.u_.inl, o.u_.inl + o.n_, u_.inl);
+    o.n_ = 0;
+    o.cap_ = kInline;
+  }
+  uint32_t n_ = 0, cap_ = kInline;
+  union {
+    uint32_t inl[kInline];
+    uint32_t* heap;
+  } u_;
 };
 
 constexpr uint32_t kRecWords = 2;
@@ -76,9 +152,9 @@ class PoaGraph {
   uint32_t branch_complete(uint32_t rank, std::vector<int64_t>& score, std::vector<int64_t>& pred);
 
   std::vector<char> base_;
-  std::vector<std::vector<uint32_t>> in_;    // edge ids into node, insertion order
-  std::vector<std::vector<uint32_t>> out_;   // edge ids out of node
-  std::vector<std::vector<uint32_t>> aligned_;
+  std::vector<NodeList> in_;    // edge ids into node, insertion order
+  std::vector<NodeList> out_;   // edge ids out of node
+  std::vector<NodeList> aligned_;
   std::vector<uint32_t> cov_, cov_last_;     // distinct sequences touching a node's edges
   std::vector<uint32_t> e_tail_, e_head_;
   std::vector<int64_t> e_w_;

@@ -91,13 +91,19 @@ struct GapOut {
 // inner column, and the lane shifts that feed an addition are DPP-combined
 // adds (P1's input Hpre[j-1] + q - jc, P2's P1[j-1] + (j-1)c + g - je, and the
 // E[j-1] + e / Q[j-1] + c terms of the traceback tests).  Same values.
+//
+// The P2 scan of strip_gaps, scan(max(B[k], P1[k-1] + f(k))) with
+// B[k] = Hpre[k-1] + g - k e and f(k) = (k-1) c + g - k e, equals
+// max(scan(B)[j], P1[j-1] + f(j)): P1 is a prefix max and f is non-decreasing
+// (f(k+1) - f(k) = c - e >= 0, checked on host), so the P1 term's own prefix
+// max is its last value.  The scans of A (P1's input) and B are therefore
+// independent and run interleaved (wave_prefix_max2).
 __device__ __forceinline__ void strip_gaps_nf(const PoaScore& P, int32_t j0, int32_t Hpre, const StripConst& K,
                                               StripCarry& cr, GapOut& o) {
   int32_t p1 = shr1_add(cr.cHpre + K.qjc, Hpre, K.qjc);
-  const int32_t u = p1 + K.k1;  // Hpre[j-1] + g - j e
-  p1 = wave_prefix_max(p1);
-  int32_t p2 = imax(u, shr1_add_bc(p1, K.k2));
-  p2 = wave_prefix_max(p2);
+  int32_t u = p1 + K.k1;  // Hpre[j-1] + g - j e
+  wave_prefix_max2(p1, u);
+  const int32_t p2 = imax(u, shr1_add_bc(p1, K.k2));
   const int32_t T1 = cr.cQ + P.g - j0 * P.e;
   const int32_t T2 = cr.run1 + K.t2b;
   o.Q = K.jc + imax(p1, cr.run1);
@@ -543,6 +549,7 @@ namespace {
 template <bool LP>
 const void* strip_kernel_ptr(int w) {
   switch (w) {
+    case 16: return LP ? reinterpret_cast<const void*>(&poa_strip_kernel<true, 16>) : nullptr;
     case 8: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 8>);
     case 7: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 7>);
     case 6: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 6>);
@@ -602,6 +609,7 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
                      a.pool, a.aln, a.aln_len, a.lds_slots)
   if (lds_pool) {
     switch (w) {
+      case 16: SVS_STRIP(true, 16); break;
       case 8: SVS_STRIP(true, 8); break;
       case 7: SVS_STRIP(true, 7); break;
       case 6: SVS_STRIP(true, 6); break;

@@ -39,6 +39,32 @@ __device__ __forceinline__ int32_t wave_prefix_max(int32_t x) {
   return x;
 }
 
+// Two independent inclusive prefix-max scans, interleaved: each DPP step of
+// one scan is the other's wait state, so the pair costs 6 s_nop 0 instead of
+// 12 s_nop 1 and the two dependency chains overlap.
+__device__ __forceinline__ void wave_prefix_max2(int32_t& a, int32_t& b) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf"
+      : "+v"(a), "+v"(b));
+}
+
 // lane l <- x[l-1]; lane 0 <- fill (wave-uniform).  DPP wave_shr:1.
 __device__ __forceinline__ int32_t wave_shr1(int32_t x, int32_t fill, int /*lane*/) {
   return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xF, 0xF, false);

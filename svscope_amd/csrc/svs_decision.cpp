@@ -82,9 +82,15 @@ svs_decision_result* run_decision(svs_context* ctx, int32_t n, const svs_decisio
   svs_em_config ecfg = cfg.em;
   ecfg.want_params = 0;
 
+  // At most em_batch windows per EM launch, the first launch half that: when
+  // every MSA of the batch completes in the same step, the GPU has nothing to
+  // run until the first labels arrive, so the first EM launch is kept short.
   auto start_em = [&]() {
     auto b = std::make_unique<EmBatch>();
-    b->windows.swap(em_ready);
+    const size_t cap = st.em_launches == 0 ? std::max<size_t>(1, em_batch / 2) : em_batch;
+    const size_t take = std::min(cap, em_ready.size());
+    b->windows.assign(em_ready.begin(), em_ready.begin() + static_cast<std::ptrdiff_t>(take));
+    em_ready.erase(em_ready.begin(), em_ready.begin() + static_cast<std::ptrdiff_t>(take));
     b->t0 = Clock::now();
     std::vector<svs_em_window> ew(b->windows.size());
     int64_t xoff = 0;

@@ -54,6 +54,9 @@ struct PoaLaunch {
 // column + 64 packed uint16 F/O distances), and the largest pool kept in LDS.
 constexpr uint32_t kStripSlotBytes = 65 * 4 + 64 * 2;
 constexpr uint32_t kStripMaxLdsSlots = 80;
+// LDS a strip workgroup's pools may take (160 KiB per CU on gfx950, less the
+// kernel's own few static words)
+constexpr uint64_t kStripLdsBytes = 160 * 1024 - 256;
 
 constexpr uint32_t kPoaMaxSlotsMultiWave = 64;
 

@@ -169,7 +169,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   int wpj = 1;
   const char* we = std::getenv("SVS_POA_WPJ");
   const int wenv = we ? std::atoi(we) : 0;
-  if (wenv >= 1 && wenv <= 8) {
+  if ((wenv >= 1 && wenv <= 8) || (wenv == 16 && lds_pool)) {
     wpj = (lds_pool || (wenv & (wenv - 1)) == 0) ? wenv : 1;
   } else if (std::getenv("SVS_POA_WPJ_RESIDENT")) {
     wpj = choose_strip_wpj(ctx->device, nj, lds_pool ? max_slots : 0, min_strips);
@@ -178,7 +178,12 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     // faster than keeping every workgroup resident (r01_v16): more waves per
     // job shorten each job even when some workgroups start late.
     while (wpj < 8 && static_cast<size_t>(wpj) * nj < 6144 && min_strips >= static_cast<uint32_t>(6 * wpj)) wpj *= 2;
+    // the small launches at the end of a batch: 16 waves per job (>= 2 strips
+    // each), or the few remaining jobs leave most SIMDs idle
+    if (lds_pool && wpj == 8 && nj < 512 && min_strips >= 32) wpj = 16;
   }
+  // the per-wave LDS pools of one workgroup must fit the CU's LDS
+  while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * kStripSlotBytes > kStripLdsBytes) wpj /= 2;
   if (std::getenv("SVS_POA_DEBUG")) std::fprintf(stderr, "[svs] strip launch: %zu jobs, wpj %d, slots %u\n", nj, wpj, max_slots);
   for (size_t k = 0; k < nj; ++k) {
     const auto& tt = tasks[la.ids[k]].rows;
@@ -402,10 +407,21 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, c
   st.d2h_bytes += n_aln * 8 + nj * 4;
 }
 
-// Waits for the launch and folds its alignments back into the graphs.
-void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_stats& st, double& host_ms) {
+// Waits for the launch and folds its alignments back into the graphs.  While
+// the launch is still running, `idle` (if given) is called for host work that
+// is off the critical path until it returns false.
+void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_stats& st, double& host_ms,
+            const std::function<bool()>& idle = nullptr) {
   PoaArena& A = *la.arena;
   const auto tw0 = Clock::now();
+  if (idle) {
+    for (;;) {
+      const hipError_t q = hipEventQuery(A.done);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) SVS_HIP(q);
+      if (!idle()) break;
+    }
+  }
   SVS_HIP(hipEventSynchronize(A.done));  // the other group's launch may still be queued behind it
   st.gpu_wait_ms += ms_since(tw0);
   float ms = 0.f;
@@ -466,6 +482,8 @@ struct PoaScheduler::Impl {
   size_t cap;
   size_t budget;
   double host_ms = 0.0;
+  std::vector<uint32_t> graves;  // finished tasks whose storage is not yet released
+  bool queue_dirty = false;      // tasks were queued since the last sort
 
   Impl(svs_context* c, const svs_poa_config& k, svs_poa_stats& s)
       : ctx(c), cfg(k), score{k.m, k.n, k.g, k.e, k.q, k.c}, st(s), cap(active_jobs_per_group()),
@@ -480,6 +498,14 @@ struct PoaScheduler::Impl {
   // small launches when the tasks end).
   void refill(Group& g) {
     if (queue.empty() || g.active.size() >= cap) return;
+    // longest remaining task first, so the long tasks (germline-cluster
+    // consensus) do not form a tail of small launches at the end
+    if (queue_dirty) {
+      std::stable_sort(queue.begin(), queue.end(), [this](uint32_t a, uint32_t b) {
+        return tasks[a].seqs.size() - tasks[a].next > tasks[b].seqs.size() - tasks[b].next;
+      });
+      queue_dirty = false;
+    }
     const Group& o = groups[1 - gid(g)];
     const size_t room = cap - g.active.size();
     const size_t share = o.active.size() < cap ? std::max<size_t>(1, (queue.size() + 1) / 2) : queue.size();
@@ -525,13 +551,9 @@ struct PoaScheduler::Impl {
       if (!fin.empty()) {
         const auto td0 = Clock::now();
         done(fin);
-        // graphs hold many small allocations: release them on the pool
-        ctx->pool->parallel_for(fin.size(), [&](size_t i) {
-          PoaTask& t = tasks[fin[i]];
-          t.graph = PoaGraph();
-          t.rows = RowTables();
-          std::vector<std::string>().swap(t.seqs);
-        });
+        // graphs hold many small allocations: freeing a thousand of them takes
+        // seconds, so they are released later, while the GPU runs (reap)
+        for (uint32_t id : fin) graves.push_back(id);
         g_trace.host("done", gid(g), td0, fin.size());
         if (ids.empty()) continue;  // refill and try again
       }
@@ -571,6 +593,24 @@ struct PoaScheduler::Impl {
 
   int gid(const Group& g) const { return static_cast<int>(&g - groups); }
 
+  // Releases the storage of up to one pool-width chunk of finished tasks;
+  // false when none are left.
+  bool reap() {
+    if (graves.empty()) return false;
+    const auto t0 = Clock::now();
+    const size_t n = std::min<size_t>(graves.size(), 4 * ctx->pool->size());
+    const size_t base = graves.size() - n;
+    ctx->pool->parallel_for(n, [&](size_t i) {
+      PoaTask& t = tasks[graves[base + i]];
+      t.graph = PoaGraph();
+      t.rows = RowTables();
+      std::vector<std::string>().swap(t.seqs);
+    });
+    graves.resize(base);
+    g_trace.host("reap", -1, t0, n);
+    return true;
+  }
+
   void run(const DoneFn& done, const PollFn& poll) {
     g_trace.open(ctx->stream);
     for (Group& g : groups) advance(g, done);
@@ -578,7 +618,7 @@ struct PoaScheduler::Impl {
       bool progressed = false;
       for (Group& g : groups) {
         if (!g.pending) continue;
-        finish(ctx, g.la, tasks, st, host_ms);
+        finish(ctx, g.la, tasks, st, host_ms, [this] { return reap(); });
         g.pending = false;
         advance(g, done);
         progressed = true;
@@ -597,6 +637,8 @@ struct PoaScheduler::Impl {
         continue;
       }
       break;
+    }
+    while (reap()) {
     }
     g_trace.close();
   }
@@ -622,6 +664,7 @@ uint32_t PoaScheduler::add(PoaTask&& t) {
   t.next = 0;
   impl_->tasks.push_back(std::move(t));
   impl_->queue.push_back(id);
+  impl_->queue_dirty = true;
   return id;
 }
 

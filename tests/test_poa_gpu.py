@@ -95,12 +95,13 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_WPJ": "8"},
     {"SVS_POA_WPJ": "3"},
     {"SVS_POA_WPJ": "7"},
+    {"SVS_POA_WPJ": "16"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "1"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "4"},
 ])
 def test_kernel_variants_match_oracle(env):
     """Every POA kernel variant gives the oracle's result: row-major with 1/2/4
-    waves per job, strip-major with 1/2/3/4/7/8 pipelined waves per job, and the
+    waves per job, strip-major with 1/2/3/4/7/8/16 pipelined waves per job, and the
     strip-major kernel with its pool in global memory."""
     import os
     from svscope_amd import synth
