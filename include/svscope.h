@@ -54,6 +54,9 @@ typedef struct svs_poa_stats {
   double host_graph_ms;     /* host graph update / export time */
   double wall_ms;
   double gpu_wait_ms;       /* host time blocked waiting for a launch's results */
+  uint64_t cells_computed;  /* DP cells the kernel evaluated (64-column strip rows x 64;
+                               below dp_cells when the exact pruning skips rows) */
+  uint64_t prune_retries;   /* pruned alignments re-run unpruned (bound above the optimum) */
 } svs_poa_stats;
 
 /* One context per host thread; owns a HIP stream and device arenas. */

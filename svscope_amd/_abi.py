@@ -39,7 +39,8 @@ class PoaStats(ctypes.Structure):
     _fields_ = [("dp_cells", ctypes.c_uint64), ("alignments", ctypes.c_uint64), ("launches", ctypes.c_uint64),
                 ("tb_bytes", ctypes.c_uint64), ("pool_bytes", ctypes.c_uint64), ("h2d_bytes", ctypes.c_uint64),
                 ("d2h_bytes", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("host_graph_ms", ctypes.c_double),
-                ("wall_ms", ctypes.c_double), ("gpu_wait_ms", ctypes.c_double)]
+                ("wall_ms", ctypes.c_double), ("gpu_wait_ms", ctypes.c_double),
+                ("cells_computed", ctypes.c_uint64), ("prune_retries", ctypes.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

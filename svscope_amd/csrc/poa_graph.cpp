@@ -267,10 +267,32 @@ void PoaGraph::export_strip_rows(RowTables* t) const {
       const uint32_t i = k - a;
       if (i < kInlinePreds) w[1] |= ps << (16 * i);
     }
+    w[3] = 0;
     for (uint32_t k = a; k < b; ++k) {
       const uint32_t pr = t->pred_row[k] - 1;
-      if (pr + 1 != r && lds_last[pr] == r + 1) free_slots.push_back(slot[pr]);
+      if (pr + 1 != r && lds_last[pr] == r + 1) {
+        free_slots.push_back(slot[pr]);
+        if (slot[pr] < 32) w[3] |= 1u << slot[pr];  // the pruning kernel's liveness bits
+      }
     }
+  }
+  // path lengths to a sink, over the rank order backwards (every out-edge
+  // leads to a higher rank)
+  static thread_local std::vector<uint32_t> dmin, dmax;
+  dmin.assign(V, 0);
+  dmax.assign(V, 0);
+  for (uint32_t r = V; r-- > 0;) {
+    const uint32_t node = rank_to_node_[r];
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    for (uint32_t e : out_[node]) {
+      const uint32_t h = node_to_rank_[e_head_[e]];
+      lo = std::min(lo, dmin[h] + 1);
+      hi = std::max(hi, dmax[h] + 1);
+    }
+    if (out_[node].empty()) lo = 0;
+    dmin[r] = lo;
+    dmax[r] = hi;
+    t->rec[static_cast<size_t>(r) * kRecWords + 2] = std::min(lo, 0xFFFFu) | (std::min(hi, 0xFFFFu) << 16);
   }
   t->n_slots = next;
 }

@@ -33,6 +33,12 @@ struct RowTables {
   //       kInlinePreds in-edges), kNoSlot = "the row just above" (kept in
   //       registers); rows with more in-edges read all slots from
   //       pred_slot[pstart[r] + k]
+  //   w2: dmin | dmax << 16: fewest / most nodes on a path from the row's
+  //       node (exclusive) to a sink (inclusive), clamped to 0xFFFF; they
+  //       bound the score any alignment can still gain below the row (the
+  //       kernel's exact pruning, poa_strip.hip)
+  //   w3: bit p set for each slot p < 32 whose last reader is this row; the
+  //       pruning kernel clears their liveness after it
   std::vector<uint32_t> rec;
 };
 
@@ -111,7 +117,7 @@ class NodeList {
   } u_;
 };
 
-constexpr uint32_t kRecWords = 2;
+constexpr uint32_t kRecWords = 4;
 constexpr uint32_t kInlinePreds = 2;
 constexpr uint32_t kNoSlot = 0xFFFF;
 

@@ -126,7 +126,7 @@ __device__ __forceinline__ void strip_gaps_nf(const PoaScore& P, int32_t j0, int
 // Prefetched inputs of one row: its record and its carries into this strip
 // (strip 0: column-0 values H0, F0, O0 from fill_col0).
 struct RowIn {
-  uint32_t w0, w1;
+  uint32_t w0, w1, w2, w3;
   int32_t b0, b1, b2, b3;
 };
 
@@ -157,7 +157,7 @@ __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, 
 // ...; strip s reads the carries wave (w-1) mod WPJ left for strip s-1, which
 // it publishes every 8 rows through an LDS progress counter (workgroup-scope
 // release / acquire), so the waves form a row-skewed pipeline over strips.
-template <bool LDSP, int WPJ>
+template <bool LDSP, int WPJ, bool PRUNE>
 __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore P, const uint32_t* __restrict__ rec_all,
     const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
@@ -167,7 +167,8 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
   extern __shared__ int32_t lds[];
   __shared__ int32_t prog[WPJ];  // per wave: strip * (V + 1) + rows done, carries published
   __shared__ int32_t s_err;
-  __shared__ int32_t s_brow[WPJ];
+  __shared__ int32_t s_brow[WPJ], s_best[WPJ];
+  __shared__ uint32_t s_rows[WPJ];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
   const int job_id = blockIdx.x;
@@ -201,6 +202,29 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
 
   int32_t best = SVS_NEG_INF;  // meaningful on the lane owning column L
   int32_t best_row = 0;
+  // Exact pruning (J.lb != kNoPrune).  With ub(cell) an upper bound of the
+  // score any completion of an alignment through the cell can still add
+  // (every remaining read base matched, the fewest excess gaps the paths from
+  // the row's node to a sink allow: m rr + cg max(0, dmin - rr)
+  // - (m - cg) max(0, rr - dmax)), a cell with H + ub < lb cannot lie on an
+  // alignment scoring >= lb, and ub never grows along a move, so every cell
+  // whose maximum comes from such a cell is dead too.  Per strip, a row is
+  // alive when some cell of it at columns j0-1 .. j0+63 is (its computed cells,
+  // or the carry from strip s-1; in strip 0 the column-0 cell).  A row none of
+  // whose inputs (carry / column-0 cell, in-edge rows) is alive is not
+  // computed: its slot, registers and carry to strip s+1 become VNEG.  When
+  // nothing in the strip is alive the sweep jumps ahead 64 rows at a time to
+  // the next row with an alive input (fast_forward), then resets every pool
+  // slot to VNEG.  Alive cells keep their exact values and traceback codes: a
+  // dead input (VNEG, or the real values of a computed dead row) has every term
+  // below an alive cell's maximum.  If the best
+  // sink score reaches lb, lb <= the optimum, every cell of every optimal path
+  // was computed and the traceback is spoa's; otherwise the job returns
+  // kPruneRetry and the host runs it again with no bound.
+  const int32_t lb = J.lb;
+  const bool prune = PRUNE && lb != kNoPrune;
+  const int32_t cg = imax(imax(P.g, P.e), imax(P.q, P.c));  // best per-base gap score (<= 0, host-checked)
+  uint32_t rows_done = 0;
 
   auto sweep = [&](auto first_tag, int32_t s) {
     constexpr bool FIRST = decltype(first_tag)::value;
@@ -214,6 +238,22 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     int32_t avail = -1;                                  // producer progress seen so far
     const bool write_bnd = s + 1 < nstrips;
     const bool owns_L = (L >> 6) == s;
+    // pruning state of this strip: slot liveness bits (slots < 64, host-checked;
+    // slot 0 = the virtual row 0, alive when row0_h + m (L - j) reaches lb at
+    // some column j0-1 .. j0+63, i.e. at j0-1: it decreases along j), and the
+    // register row's liveness
+    const bool slot0_alive = FIRST || !prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb;
+    uint32_t alive = slot0_alive ? 1u : 0u;  // bit p: slot p alive (pruning: < 32 slots, host-checked)
+    bool reg_alive = false;
+    const int32_t rrem = L - j;              // read bases after column j
+    const int32_t mrr = P.m * rrem;
+    // m rr + cg max(0, dmin - rr) - (m - cg) max(0, rr - dmax) as
+    // m rr + d (d >= 0 ? cg : m - cg) with d = clamp(rr, dmin, dmax) - rr
+    auto ub_of = [&](uint32_t w2, int32_t rr, int32_t mr) -> int32_t {
+      const int32_t dmin = static_cast<int32_t>(w2 & 0xFFFFu), dmax = static_cast<int32_t>(w2 >> 16);
+      const int32_t d = min(imax(rr, dmin), dmax) - rr;
+      return mr + d * (d >= 0 ? cg : P.m - cg);
+    };
     StripConst K;
     if (!FIRST) {
       const int32_t ge = P.g - j * P.e, c1 = (j - 1) * P.c;
@@ -238,7 +278,12 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     auto fetch = [&](RowIn& d, uint32_t r) {
       const uint32_t rr = r < V ? r : V - 1;
       const uint32_t* w = rec + static_cast<uint64_t>(rr) * kRecWords;
-      d.w0 = w[0]; d.w1 = w[1];
+      if constexpr (PRUNE) {
+        const uint4 v = *reinterpret_cast<const uint4*>(w);
+        d.w0 = v.x; d.w1 = v.y; d.w2 = v.z; d.w3 = v.w;
+      } else {
+        d.w0 = w[0]; d.w1 = w[1]; d.w2 = 0; d.w3 = 0;
+      }
       if (FIRST) {
         d.b0 = rc0[3 * rr];
         d.b1 = rc0[3 * rr + 1];
@@ -262,6 +307,53 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       const bool store = (w0 >> 9) & 1u;
       const uint32_t np = (w0 >> 10) & 31u;
       const uint32_t own = w0 >> 16;
+      auto slot_alive = [&](uint32_t ps) -> bool {
+        if (ps == kNoSlot) return reg_alive;
+        return ((alive >> ps) & 1u) != 0;
+      };
+      auto publish = [&]() {
+        if (WPJ > 1 && write_bnd && ((r & 7u) == 7u || r + 1 == V) && lane == 0)
+          __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
+                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
+      const int32_t cH_in = FIRST ? SVS_VNEG : __builtin_amdgcn_readfirstlane(d.b3);
+      if (prune) {
+        // the row's own input: the carry (strip 0: the column-0 cell)
+        bool live;
+        if (FIRST) {
+          const int32_t h0 = __builtin_amdgcn_readfirstlane(d.b0);
+          live = h0 + ub_of(__builtin_amdgcn_readfirstlane(d.w2), L, P.m * L) >= lb;
+        } else {
+          live = cH_in > SVS_VNEG / 2;
+        }
+        if (!live) {
+          const uint32_t wp = __builtin_amdgcn_readfirstlane(d.w1);
+          live = slot_alive(wp & 0xFFFFu) || (np >= 2 && slot_alive(wp >> 16));
+          if (!live && np > kInlinePreds) {
+            const uint32_t* __restrict__ spill = pslot + rps[r];
+            for (uint32_t k = kInlinePreds; k < np && !live; ++k)
+              live = slot_alive(__builtin_amdgcn_readfirstlane(spill[k]));
+          }
+        }
+        if (!live) {
+          // no alive input: the row's cells are all dead, never computed
+          if (store) {
+            int32_t* q = pool + own * kSlotInts;
+            q[lane + 1] = SVS_VNEG;
+            q[lane] = SVS_VNEG;
+            reinterpret_cast<uint16_t*>(q + 65)[lane] = 0;  // F = O = H = VNEG
+          }
+          // own slot dead, slots whose last reader this row is (w3) released
+          alive &= ~(__builtin_amdgcn_readfirstlane(d.w3) | (store ? 1u << own : 0u));
+          pH = pF = pO = pHm = SVS_VNEG;
+          reg_alive = false;
+          if (write_bnd && lane == 0)
+            *reinterpret_cast<int4*>(bout + 4ull * r) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
+          publish();
+          return;
+        }
+      }
+      if constexpr (PRUNE) ++rows_done;
       int32_t H0 = 0, F0 = 0, O0 = 0;
       StripCarry cr;
       if (FIRST) {
@@ -412,6 +504,15 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k, uc_stop);
       }
       tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+      bool any_alive = true;
+      if (prune) {
+        const int32_t ub = ub_of(__builtin_amdgcn_readfirstlane(d.w2), rrem, mrr);
+        any_alive = __builtin_amdgcn_ballot_w64(rrem >= 0 && H + ub >= lb) != 0;
+        const bool out_alive = any_alive || cH_in > SVS_VNEG / 2;
+        reg_alive = out_alive;
+        const uint32_t ob = store ? 1u << own : 0u;
+        alive = ((alive & ~ob) | (out_alive ? ob : 0u)) & ~__builtin_amdgcn_readfirstlane(d.w3);
+      }
       if (store) {
         // Hx[l+1] = H[l], then Hx[l] = prevH[l] (= H[l-1], lane 0: H[j0-1]);
         // the two full-wave writes agree wherever they overlap
@@ -424,26 +525,88 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       pF = F;
       pO = O;
       pHm = prevH;
-      if (write_bnd) {
-        if (lane == 0) *reinterpret_cast<int4*>(bout + 4ull * r) = make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH);
-        if (WPJ > 1 && ((r & 7u) == 7u || r + 1 == V) && lane == 0)
-          __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
-                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (write_bnd && lane == 0) {
+        *reinterpret_cast<int4*>(bout + 4ull * r) =
+            any_alive ? make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH) : make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
       }
+      publish();
       if (sink && owns_L && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
     };
+
+    // Pruning: with no slot (but the virtual row's) and not the register row
+    // alive, the next rows are alive only through their carry (strip 0: the
+    // column-0 cell) or, while the virtual row is, as sources (no in-edge).
+    // Scans 64 rows per step with one load per lane, hands VNEG carries on for
+    // the rows it passes, and returns the first row with such an input (or V).
+    auto fast_forward = [&](uint32_t r) -> uint32_t {
+      while (r < V) {
+        const uint32_t rr = r + static_cast<uint32_t>(lane);
+        const bool in = rr < V;
+        bool cand = false;
+        if (FIRST) {
+          if (in) {
+            const uint32_t w2 = rec[static_cast<uint64_t>(rr) * kRecWords + 2];
+            cand = rc0[3 * rr] + ub_of(w2, L, P.m * L) >= lb;
+          }
+        } else {
+          if (WPJ > 1) {
+            const int32_t need = need0 + static_cast<int32_t>(min(V, r + 64));
+            if (avail < need) avail = strip_wait_ge(&prog[pw], need, &s_err);
+          }
+          if (in) cand = __builtin_nontemporal_load(bin + 4ull * rr + 3) > SVS_VNEG / 2;
+        }
+        if (slot0_alive && in) cand = cand || ((rec[static_cast<uint64_t>(rr) * kRecWords] >> 10) & 31u) == 0;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
+        const uint32_t n = m ? static_cast<uint32_t>(__builtin_ctzll(m)) : min(64u, V - r);
+        if (write_bnd && static_cast<uint32_t>(lane) < n)
+          *reinterpret_cast<int4*>(bout + 4ull * rr) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
+        r += n;
+        if (m) break;
+      }
+      // rows passed over left stale pool slots: every slot but the virtual row's to VNEG
+      for (uint32_t p = 1; p < nslot; ++p) {
+        int32_t* q = pool + p * kSlotInts;
+        q[lane + 1] = SVS_VNEG;
+        if (lane == 0) q[0] = SVS_VNEG;
+        reinterpret_cast<uint16_t*>(q + 65)[lane] = 0;
+      }
+      pH = pF = pO = pHm = SVS_VNEG;
+      // carries of every row before r are stored: publish whole 8-row lines
+      if (WPJ > 1 && write_bnd && lane == 0) {
+        const uint32_t done = r >= V ? V : (r & ~7u);
+        __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(done),
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      return r;
+    };
+    auto dead_strip = [&]() { return (alive & ~1u) == 0 && !reg_alive; };
 
     // rows in pairs with two statically named prefetch sets (no waits on
     // loads still in flight when a set is refilled)
     RowIn A, B;
-    fetch(A, 0);
-    fetch(B, 1);
-    for (uint32_t r = 0; r < V; r += 2) {
+    uint32_t r = 0;
+    if (prune) r = fast_forward(0);
+    fetch(A, r);
+    fetch(B, r + 1);
+    while (r < V) {
       step(r, A);
+      if (prune && dead_strip()) {
+        r = fast_forward(r + 1);
+        fetch(A, r);
+        fetch(B, r + 1);
+        continue;
+      }
       fetch(A, r + 2);
       if (r + 1 >= V) break;
       step(r + 1, B);
+      if (prune && dead_strip()) {
+        r = fast_forward(r + 2);
+        fetch(A, r);
+        fetch(B, r + 1);
+        continue;
+      }
       fetch(B, r + 3);
+      r += 2;
     }
     // this strip's boundary stores must land before the next strip reads them
     __builtin_amdgcn_s_waitcnt(0);
@@ -469,13 +632,23 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
   // the owner of column L's strip holds the sink maximum; every wave's
   // traceback-code stores must be visible to wave 0's lane 0
   best_row = __shfl(best_row, L & 63, 64);
+  best = __shfl(best, L & 63, 64);
   if (WPJ > 1) {
-    if (lane == 0 && ((L >> 6) % WPJ) == wave) s_brow[wave] = best_row;
+    if (lane == 0) {
+      s_rows[wave] = rows_done;
+      if (((L >> 6) % WPJ) == wave) {
+        s_brow[wave] = best_row;
+        s_best[wave] = best;
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     if (wave != 0) return;
     best_row = s_brow[(L >> 6) % WPJ];
+    best = s_best[(L >> 6) % WPJ];
+    rows_done = 0;
+    for (int w = 0; w < WPJ; ++w) rows_done += s_rows[w];
     if (s_err) {
       if (lane == 0) aln_len[job_id] = -1;
       return;
@@ -491,6 +664,16 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
   // from 64-row tiles, so the path pays one HBM round trip per tile instead of
   // one or two per step.
   best_row = __builtin_amdgcn_readfirstlane(best_row);
+  best = __builtin_amdgcn_readfirstlane(best);
+  if constexpr (!PRUNE) rows_done = V * static_cast<uint32_t>(nstrips);
+  if (lane == 0) {
+    aln_len[n_jobs + job_id] = best;
+    aln_len[2 * n_jobs + job_id] = static_cast<int32_t>(rows_done);
+  }
+  if (prune && best < lb) {
+    if (lane == 0) aln_len[job_id] = kPruneRetry;
+    return;
+  }
   int32_t t_r = INT32_MIN / 2, t_c = INT32_MIN / 2, p_r = INT32_MIN / 2;
   uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;  // element e = 64 v + lane: (t_r - e / 16, t_c - e % 16)
   int32_t pn = 0, p0 = 0, p1 = 0;           // lane l: in-edge count and in-edges 0, 1 of row p_r - l
@@ -549,15 +732,15 @@ namespace {
 template <bool LP>
 const void* strip_kernel_ptr(int w) {
   switch (w) {
-    case 16: return LP ? reinterpret_cast<const void*>(&poa_strip_kernel<true, 16>) : nullptr;
-    case 8: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 8>);
-    case 7: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 7>);
-    case 6: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 6>);
-    case 5: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 5>);
-    case 4: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 4>);
-    case 3: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 3>);
-    case 2: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 2>);
-    default: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 1>);
+    case 16: return LP ? reinterpret_cast<const void*>(&poa_strip_kernel<true, 16, false>) : nullptr;
+    case 8: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 8, false>);
+    case 7: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 7, false>);
+    case 6: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 6, false>);
+    case 5: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 5, false>);
+    case 4: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 4, false>);
+    case 3: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 3, false>);
+    case 2: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 2, false>);
+    default: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 1, false>);
   }
 }
 
@@ -603,10 +786,18 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   const int w = a.waves_per_job;
   const bool lds_pool = a.lds_slots > 0;
   const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * kStripSlotBytes : 0;
-#define SVS_STRIP(LP, W)                                                                                     \
-  hipLaunchKernelGGL((poa_strip_kernel<LP, W>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, a.n_jobs, \
-                     a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.bnd, \
+#define SVS_STRIP2(LP, W, PR)                                                                                     \
+  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, a.n_jobs, \
+                     a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.bnd,     \
                      a.pool, a.aln, a.aln_len, a.lds_slots)
+#define SVS_STRIP(LP, W)          \
+  do {                            \
+    if (a.prune) {                \
+      SVS_STRIP2(LP, W, true);    \
+    } else {                      \
+      SVS_STRIP2(LP, W, false);   \
+    }                             \
+  } while (0)
   if (lds_pool) {
     switch (w) {
       case 16: SVS_STRIP(true, 16); break;
@@ -626,6 +817,7 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
     else SVS_STRIP(false, 1);
   }
 #undef SVS_STRIP
+#undef SVS_STRIP2
   return hipGetLastError();
 }
 

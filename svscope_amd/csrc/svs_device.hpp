@@ -25,8 +25,14 @@ struct PoaJob {
   uint32_t n_slots;   // pool slots (slot 0 = virtual row 0)
   uint64_t bnd_off;   // strip kernel: int32 strip-boundary carries, 2 x n_rows x 4
   uint32_t rec_off;   // strip kernel: row records (kRecWords uint32 per row), in rows
-  uint32_t pad_;
+  int32_t lb;         // strip kernel: pruning bound (kNoPrune = off), see poa_strip.hip
 };
+
+// PoaJob::lb value that turns the strip kernel's exact pruning off.
+constexpr int32_t kNoPrune = INT32_MIN;
+// aln_len[job] for a pruned job whose best sink score fell below its bound
+// (the bound was not a lower bound of the optimum: run it again unpruned).
+constexpr int32_t kPruneRetry = -2;
 
 struct PoaLaunch {
   const PoaJob* jobs;
@@ -42,12 +48,14 @@ struct PoaLaunch {
   uint16_t* tb;
   int32_t* pool;
   int32_t* aln;
-  int32_t* aln_len;
+  int32_t* aln_len;    // per job: path length; strip kernel also [n_jobs + job] best
+                       // sink score and [2 n_jobs + job] strip rows computed
   int waves_per_job;  // 1, 2 or 4 (column-chunk waves per job)
   // strip-major kernel
   const uint32_t* rec;   // row records (export_strip_rows)
   int32_t* bnd;          // strip-boundary carries
   uint32_t lds_slots;    // pool slots per wave held in LDS (max n_slots of the launch)
+  bool prune;            // some job has a pruning bound: the pruning kernel variant
 };
 
 // Strip-major kernel: LDS bytes per pool slot (65 int32 H incl. the boundary

@@ -39,6 +39,12 @@ struct PoaTask {
   size_t next = 0;      // index of the next sequence to align
   PoaGraph graph;
   RowTables rows;       // exported row tables of the current step (capacity reused across steps)
+  // exact pruning of the strip kernel (svs_poa_engine.cpp: prune_bound)
+  double rate = 0.0;      // best score / read length of the last alignment that needed no retry
+  bool have_rate = false;
+  bool retry = false;     // the current sequence's pruned run missed its bound: run it unpruned
+  uint8_t n_retries = 0;
+
   std::string consensus;
   std::vector<std::string> msa;
 };

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -138,6 +139,26 @@ bool strip_pool_forced_global() {
   return e && std::string(e) == "1";
 }
 
+// Exact pruning bound of a strip job (poa_strip.hip): lb = the score per read
+// base of the task's last alignment that needed no retry x this read's length,
+// less a slack of SVS_POA_PRUNE_SLACK (default 0.05) x m x length.  Any value is exact: a
+// bound above the optimum only costs a retry with no bound.  Off for the first
+// alignment of a task, for a retry, after two retries of one task, for graphs
+// too long for the 16-bit path lengths of the row records, and for score
+// parameters the kernel's upper bound does not cover (SVS_POA_PRUNE=0: off).
+int32_t prune_bound(const PoaTask& t, const PoaScore& P, uint32_t n_rows, uint32_t len) {
+  const char* pe = std::getenv("SVS_POA_PRUNE");
+  const bool on = !(pe && std::string(pe) == "0");
+  const char* se = std::getenv("SVS_POA_PRUNE_SLACK");
+  const double slack = se ? std::atof(se) : 0.05;
+  const int32_t cg = std::max(std::max(P.g, P.e), std::max(P.q, P.c));
+  if (!on || !t.have_rate || t.retry || t.n_retries >= 2 || n_rows > 0xFFFFu || len > (1u << 20)) return kNoPrune;
+  if (cg > 0 || P.m < P.n || P.m < 0) return kNoPrune;
+  const double lb = std::floor(t.rate * len - slack * P.m * len);
+  if (lb < -1e9 || lb > 1e9) return kNoPrune;
+  return static_cast<int32_t>(lb);
+}
+
 uint64_t job_bytes(const RowTables& tt, uint64_t L) {
   const uint64_t ls = round_up(L + 1, 64), V = tt.pstart.size() - 1;
   if (use_strip_kernel()) {
@@ -157,6 +178,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   la.jobs.assign(nj, PoaJob{});
   uint64_t n_rows = 0, n_pstart = 0, n_pred = 0, n_seq = 0, n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
   uint32_t max_preds = 0, max_slots = 1;
+  bool any_prune = false;
   for (size_t k = 0; k < nj; ++k) max_slots = std::max(max_slots, tasks[la.ids[k]].rows.n_slots);
   const bool lds_pool = max_slots <= kStripMaxLdsSlots && !strip_pool_forced_global();
   // waves per job: enough strip-pipeline waves to fill the CUs, only for reads
@@ -202,6 +224,9 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     J.bnd_off = n_bnd;
     J.pool_off = n_pool;
     J.aln_off = n_aln;
+    J.lb = prune_bound(tasks[la.ids[k]], score, J.n_rows, J.len);
+    if (J.n_slots > 32) J.lb = kNoPrune;  // the kernel tracks slot liveness in 32 bits
+    any_prune = any_prune || J.lb != kNoPrune;
     n_rows += J.n_rows;
     n_pstart += J.n_rows + 1;
     n_pred += tt.pred_row.size();
@@ -251,9 +276,9 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   A.d_tb.ensure(n_tb * 2 + 4096);
   A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096);
   A.d_aln.ensure(n_aln * 8);
-  A.d_alen.ensure(nj * 4);
+  A.d_alen.ensure(nj * 12);
   A.h_aln.ensure(n_aln * 8);
-  A.h_alen.ensure(nj * 4);
+  A.h_alen.ensure(nj * 12);
   char* dg = A.d_in.as<char>();
   SVS_HIP(hipMemcpyAsync(dg, hs, off, hipMemcpyHostToDevice, A.copy_stream));
   SVS_HIP(hipEventRecord(A.h2d, A.copy_stream));
@@ -274,13 +299,14 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.aln = A.d_aln.as<int32_t>();
   pl.aln_len = A.d_alen.as<int32_t>();
   pl.lds_slots = lds_pool ? max_slots : 0;
+  pl.prune = any_prune;
   pl.waves_per_job = wpj;
   la.wpj = wpj;
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
   SVS_HIP(launch_poa_strip(pl, A.stream));
   SVS_HIP(hipEventRecord(A.ev1, A.stream));
   SVS_HIP(hipStreamWaitEvent(A.copy_stream, A.ev1, 0));
-  SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 4, hipMemcpyDeviceToHost, A.copy_stream));
+  SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 12, hipMemcpyDeviceToHost, A.copy_stream));
   SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, pl.aln, n_aln * 8, hipMemcpyDeviceToHost, A.copy_stream));
   SVS_HIP(hipEventRecord(A.done, A.copy_stream));
   st.launches += 1;
@@ -288,7 +314,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   st.tb_bytes += n_tb * 2;
   st.pool_bytes += (n_bnd + n_pool) * 4;
   st.h2d_bytes += off;
-  st.d2h_bytes += n_aln * 8 + nj * 4;
+  st.d2h_bytes += n_aln * 8 + nj * 12;
 }
 
 // Packs the launch's tables into the arena's pinned buffer and enqueues
@@ -401,6 +427,7 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, c
   SVS_HIP(hipEventRecord(A.done, A.copy_stream));
   st.launches += 1;
   st.alignments += nj;
+  st.cells_computed += n_tb;  // the row-major kernel evaluates every cell
   st.tb_bytes += n_tb * 2;
   st.pool_bytes += n_pool * 4;
   st.h2d_bytes += off;
@@ -436,16 +463,38 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   auto th0 = Clock::now();
   const int32_t* alen = A.h_alen.as<int32_t>();
   const int32_t* aout = A.h_aln.as<int32_t>();
-  ctx->pool->parallel_for(la.ids.size(), [&](size_t k) {
+  const size_t nj = la.ids.size();
+  const bool strip = use_strip_kernel();
+  if (strip) {
+    for (size_t k = 0; k < nj; ++k) {
+      st.cells_computed += 64ull * static_cast<uint32_t>(alen[2 * nj + k]);
+      if (alen[k] == kPruneRetry) st.prune_retries += 1;
+    }
+  }
+  ctx->pool->parallel_for(nj, [&](size_t k) {
     const int32_t n = alen[k];
+    auto& t = tasks[la.ids[k]];
+    if (strip && n == kPruneRetry) {
+      // the bound was above the optimum: the same sequence again, unpruned
+      t.retry = true;
+      t.n_retries += 1;
+      return;
+    }
     if (n < 0) throw SvsError(SVS_E_INTERNAL, "GPU traceback reported an inconsistent path");
+    if (strip) {
+      const uint32_t len = la.jobs[k].len;
+      if (!t.retry && len > 0) {
+        t.rate = static_cast<double>(alen[nj + k]) / len;
+        t.have_rate = true;
+      }
+      t.retry = false;
+    }
     const int32_t* p = aout + 2 * la.jobs[k].aln_off;
     std::vector<int32_t> fwd(2 * static_cast<size_t>(n));
     for (int32_t x = 0; x < n; ++x) {
       fwd[2 * x] = p[2 * (n - 1 - x)];
       fwd[2 * x + 1] = p[2 * (n - 1 - x) + 1];
     }
-    auto& t = tasks[la.ids[k]];
     t.graph.add_alignment_ranks(fwd, t.seqs[t.next]);
     ++t.next;
   });

@@ -204,7 +204,30 @@ std::vector<int32_t> emu_align(const svs::RowTables& T, const std::string& seq, 
 // per strip, a 64-column pool with the planner's slots, register pass-through
 // for in-edges from the row just above, per-slot boundary H, and the per-row
 // carries handed from strip to strip.
-std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string& seq, const Score& P) {
+// Exact pruning (poa_strip.hip): with lb <= the optimum, a strip row is
+// skipped when none of its inputs is alive, and a computed row whose every
+// cell has H + ub < lb is marked dead; *retry is set when the best sink score
+// falls below lb (the bound did not hold: the caller re-runs with no pruning).
+struct StripPrune {
+  int32_t lb = INT32_MIN / 2;  // no pruning
+  bool retry = false;
+  int32_t best = 0;  // best sink score at column L (the optimum when lb held)
+  uint64_t rows_done = 0, rows_all = 0;
+  uint64_t rows_slow_skip = 0;  // rows skipped one by one (not inside a fast_forward jump)
+};
+
+int32_t upper_suffix(const Score& P, int32_t rr, uint32_t w2) {
+  const int32_t dmin = static_cast<int32_t>(w2 & 0xFFFF), dmax = static_cast<int32_t>(w2 >> 16);
+  const int32_t cg = std::max(std::max(P.g, P.e), std::max(P.q, P.c));
+  if (std::getenv("EMU_LOOSE")) return P.m * rr;
+  return P.m * rr + cg * std::max(0, dmin - rr) - (P.m - cg) * std::max(0, rr - dmax);
+}
+
+std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string& seq, const Score& P,
+                                     StripPrune* prune = nullptr) {
+  StripPrune none;
+  StripPrune& PR = prune ? *prune : none;
+  const bool on = prune != nullptr;
   const int32_t L = static_cast<int32_t>(seq.size());
   const uint64_t LS = (static_cast<uint64_t>(L) + 1 + 63) / 64 * 64;
   const uint32_t V = static_cast<uint32_t>(T.pstart.size() - 1);
@@ -230,12 +253,62 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
     }
     slot_ch[0] = FIRST ? 0 : r0h(P, j0 - 1);
     written[0] = 1;
+    std::vector<uint8_t> slot_alive(T.n_slots, 0);
+    // the virtual row 0: alive when row0_h + m (L - j) reaches lb at j0-1
+    slot_alive[0] = FIRST || !on || static_cast<int64_t>(r0h(P, j0 - 1)) + P.m * (L - j0 + 1) >= PR.lb;
+    bool reg_alive = false;
     int32_t pHv[64], pFv[64], pOv[64], pcH = 0;
     for (uint32_t r = 0; r < V; ++r) {
       const uint32_t* w = T.rec.data() + static_cast<size_t>(r) * svs::kRecWords;
       const uint32_t nb = w[0] & 0xFF, np = (w[0] >> 10) & 31;
       const bool sink = (w[0] >> 8) & 1, store = (w[0] >> 9) & 1;
       const uint32_t own = w[0] >> 16;
+      PR.rows_all += 1;
+      // the kernel's freed-slot bits (w3) and its fast_forward condition
+      auto clear_freed = [&]() {
+        for (uint32_t f = 0; f < 32 && f < slot_alive.size(); ++f)
+          if ((w[3] >> f) & 1u) slot_alive[f] = 0;
+      };
+      bool dead_state = !reg_alive;
+      for (size_t k = 1; k < slot_alive.size(); ++k) dead_state = dead_state && !slot_alive[k];
+      if (on && dead_state) {
+        // the kernel's fast_forward: rows passed over, then every slot but the
+        // virtual row's reset to VNEG (idempotent here, row by row)
+        for (uint32_t p = 1; p < T.n_slots; ++p) {
+          for (int l = 0; l < 192; ++l) pool[p * 192 + l] = VNEG;
+          slot_ch[p] = VNEG;
+          written[p] = 1;
+        }
+        for (int l = 0; l < 64; ++l) { pHv[l] = VNEG; pFv[l] = VNEG; pOv[l] = VNEG; }
+        pcH = VNEG;
+      }
+      if (on) {
+        // skip: no live input (carry from strip s-1 / strip 0's column-0 cell,
+        // or an in-edge row's slot in this strip; a source reads slot 0)
+        const bool carry_alive = FIRST ? static_cast<int64_t>(T.col0[3 * r]) + upper_suffix(P, L, w[2]) >= PR.lb
+                                       : bin[4 * r + 3] > VNEG / 2;
+        bool pred_alive = np == 0 && slot_alive[0];
+        for (uint32_t k = 0; k < np; ++k) {
+          const uint32_t ps = np <= svs::kInlinePreds ? (w[1] >> (16 * k)) & 0xFFFF : T.pred_slot[T.pstart[r] + k];
+          pred_alive = pred_alive || (ps == svs::kNoSlot ? reg_alive : slot_alive[ps] != 0);
+        }
+        if (!carry_alive && !pred_alive) {
+          if (store) {
+            for (int l = 0; l < 192; ++l) pool[own * 192 + l] = VNEG;
+            slot_ch[own] = VNEG;
+            written[own] = 1;
+            slot_alive[own] = 0;
+          }
+          clear_freed();
+          for (int l = 0; l < 64; ++l) { pHv[l] = VNEG; pFv[l] = VNEG; pOv[l] = VNEG; }
+          pcH = VNEG;
+          reg_alive = false;
+          for (int x = 0; x < 4; ++x) bout[4 * r + x] = VNEG;
+          if (!dead_state) PR.rows_slow_skip += 1;
+          continue;
+        }
+      }
+      PR.rows_done += 1;
       int32_t run1, run2, cHpre, cQ, cE, cH, H0 = 0, F0 = 0, O0 = 0;
       if (FIRST) {
         H0 = T.col0[3 * r]; F0 = T.col0[3 * r + 1]; O0 = T.col0[3 * r + 2];
@@ -273,9 +346,11 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
         for (uint32_t k = 0; k < npass; ++k) {
           int32_t hp, fp, op, hpm;
           vals(k, l, hp, fp, op, hpm);
-          F = std::max(F, std::max(hp + P.g, fp + P.e));
-          O = std::max(O, std::max(hp + P.q, op + P.c));
-          D = std::max(D, (c0 ? 0 : hpm) + mc);
+          // no floor: a dead in-edge (VNEG) gives VNEG + g etc., as in the kernel
+          const int32_t f = std::max(hp + P.g, fp + P.e), o = std::max(hp + P.q, op + P.c), d = (c0 ? 0 : hpm) + mc;
+          F = k == 0 ? f : std::max(F, f);
+          O = k == 0 ? o : std::max(O, o);
+          D = k == 0 ? d : std::max(D, d);
         }
         if (c0) { F = F0; O = O0; }
         Fv[l] = F; Ov[l] = O; Hd[l] = D;
@@ -359,7 +434,12 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
           c2 |= lbit ? 0x100u : 0u;
           if (np != 0) c2 |= (va || (!vb && vc)) ? 0x200u : 0u;
           else c2 |= 31u << 10;
-          if (c2 != code) throw std::runtime_error("emu strip: fast-path code formula differs");
+          if (c2 != code) {
+            char buf[512];
+            snprintf(buf, sizeof buf, "emu strip: fast-path code formula differs (code %x fast %x np %u r %u l %d s %d H %d F %d O %d E %d Q %d hp %d fp %d op %d hpm %d pE %d pH %d pQ %d lb %d)",
+                     code, c2, np, r, l, s, H[l], Fv[l], Ov[l], E[l], Q[l], hp, fp, op, hpm, pE[l], pH[l], pQ[l], PR.lb);
+            throw std::runtime_error(buf);
+          }
         }
         if (np == 2 && !FIRST) {
           // the kernel's two-in-edge formula
@@ -387,6 +467,16 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
         tb[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
         if (sink && j == L && H[l] > best) { best = H[l]; best_row = static_cast<int32_t>(r) + 1; }
       }
+      bool any_alive = false;
+      for (int l = 0; l < 64; ++l) {
+        const int32_t j = j0 + l;
+        if (j <= L && static_cast<int64_t>(H[l]) + upper_suffix(P, L - j, w[2]) >= PR.lb) any_alive = true;
+      }
+      const bool carry_in_alive = FIRST ? false : cH_in > VNEG / 2;
+      const bool out_alive = any_alive || carry_in_alive;
+      reg_alive = out_alive;
+      if (store && on) slot_alive[own] = out_alive;
+      if (on) clear_freed();
       if (store) {
         if (own == svs::kNoSlot || own == 0 || own >= T.n_slots) throw std::runtime_error("emu strip: bad own slot");
         // the kernel keeps F, O as distances to H clamped at e-g+1 / c-q+1
@@ -403,8 +493,17 @@ std::vector<int32_t> emu_align_strip(const svs::RowTables& T, const std::string&
       }
       for (int l = 0; l < 64; ++l) { pHv[l] = H[l]; pFv[l] = Fv[l]; pOv[l] = Ov[l]; }
       pcH = cH_in;
-      bout[4 * r] = run1; bout[4 * r + 1] = run2; bout[4 * r + 2] = cHpre; bout[4 * r + 3] = cH;
+      if (any_alive || !on) {
+        bout[4 * r] = run1; bout[4 * r + 1] = run2; bout[4 * r + 2] = cHpre; bout[4 * r + 3] = cH;
+      } else {
+        for (int x = 0; x < 4; ++x) bout[4 * r + x] = VNEG;
+      }
     }
+  }
+  PR.best = best;
+  if (best < PR.lb) {
+    PR.retry = true;
+    return {};
   }
   return emu_traceback(T, tb, LS, L, best_row, P);
 }
@@ -416,6 +515,7 @@ struct EmuResult {
   double graph_ms = 0, dp_ms = 0;
   // row-structure counters over every exported table (tools/row_stats.py)
   uint64_t rows = 0, np0 = 0, np1 = 0, np2 = 0, pred_prev = 0, must_store = 0, slot_sum = 0, tables = 0;
+  uint64_t rows_done = 0, rows_all = 0, rows_slow = 0;  // strip rows computed / total / skipped one by one under EMU_PRUNE
 };
 
 void row_stats(const svs::RowTables& T, EmuResult* r) {
@@ -456,7 +556,28 @@ void* emu_poa(int n, const char* const* seqs, const int* lens, int m, int mis, i
       auto t1 = std::chrono::steady_clock::now();
       r->max_slots = std::max(r->max_slots, T.n_slots);
       if (!strip) row_stats(T, r);
-      auto aln = strip ? emu_align_strip(T, seq, P) : emu_align(T, seq, P);
+      std::vector<int32_t> aln;
+      const char* pm = std::getenv("EMU_PRUNE");
+      if (strip && pm) {
+        // exactness check of the pruning: with lb = the optimum (the tightest
+        // valid bound) the alignment must not change; with lb above it the
+        // kernel must ask for a retry
+        StripPrune full;
+        aln = emu_align_strip(T, seq, P, &full);
+        StripPrune tight;
+        tight.lb = full.best - std::atoi(pm);
+        const auto aln2 = emu_align_strip(T, seq, P, &tight);
+        if (tight.retry || aln2 != aln) throw std::runtime_error("emu strip: pruned alignment differs");
+        StripPrune over;
+        over.lb = full.best + 1;
+        emu_align_strip(T, seq, P, &over);
+        if (!over.retry) throw std::runtime_error("emu strip: lb above the optimum not detected");
+        r->rows_done += tight.rows_done;
+        r->rows_all += tight.rows_all;
+        r->rows_slow += tight.rows_slow_skip;
+      } else {
+        aln = strip ? emu_align_strip(T, seq, P) : emu_align(T, seq, P);
+      }
       auto t2 = std::chrono::steady_clock::now();
       graph.add_alignment_ranks(aln, seq);
       auto t3 = std::chrono::steady_clock::now();
@@ -477,6 +598,12 @@ void emu_row_stats(void* h, uint64_t* out) {
   auto* r = static_cast<EmuResult*>(h);
   const uint64_t v[8] = {r->rows, r->np0, r->np1, r->np2, r->pred_prev, r->must_store, r->slot_sum, r->tables};
   for (int i = 0; i < 8; ++i) out[i] = v[i];
+}
+void emu_prune_rows(void* h, uint64_t* out) {
+  auto* r = static_cast<EmuResult*>(h);
+  out[0] = r->rows_done;
+  out[1] = r->rows_all;
+  out[2] = r->rows_slow;
 }
 void emu_free(void* h) { delete static_cast<EmuResult*>(h); }
 double emu_graph_ms(void* h) { return static_cast<EmuResult*>(h)->graph_ms; }

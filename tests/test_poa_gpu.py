@@ -98,11 +98,18 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_WPJ": "16"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "1"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "4"},
+    {"SVS_POA_PRUNE": "0"},
+    {"SVS_POA_PRUNE_SLACK": "0", "SVS_POA_WPJ": "1"},
+    {"SVS_POA_PRUNE_SLACK": "0", "SVS_POA_WPJ": "8"},
+    {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_WPJ": "4"},
+    {"SVS_POA_PRUNE_SLACK": "0", "SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "2"},
 ])
 def test_kernel_variants_match_oracle(env):
     """Every POA kernel variant gives the oracle's result: row-major with 1/2/4
-    waves per job, strip-major with 1/2/3/4/7/8/16 pipelined waves per job, and the
-    strip-major kernel with its pool in global memory."""
+    waves per job, strip-major with 1/2/3/4/7/8/16 pipelined waves per job, the
+    strip-major kernel with its pool in global memory, and the strip kernel's
+    exact pruning off, at its tightest slack, and with a bound above the
+    optimum (every pruned job retried unpruned)."""
     import os
     from svscope_amd import synth
     from svscope_amd.poa import poa_batch
@@ -120,3 +127,29 @@ def test_kernel_variants_match_oracle(env):
                 os.environ[k] = v
     for seqs, g in zip(cases, got):
         assert g == oracle_poa(seqs, 1)
+
+
+@pytest.mark.parametrize("slack,retries", [("0.05", None), ("-0.3", True)])
+def test_pruning_stats_and_exactness(slack, retries):
+    """The strip kernel's exact pruning on config-3-like windows: the oracle's
+    MSA and consensus, fewer cells evaluated than the full matrix, and with a
+    bound above every optimum (negative slack) every pruned job retried."""
+    import os
+    from svscope_amd import synth
+    from svscope_amd.poa import poa_batch
+    wins = [synth.make_window(w, 10, 3000)[0] for w in range(3)]
+    old = os.environ.get("SVS_POA_PRUNE_SLACK")
+    os.environ["SVS_POA_PRUNE_SLACK"] = slack
+    try:
+        got, st = poa_batch(wins, return_stats=True)
+    finally:
+        if old is None:
+            os.environ.pop("SVS_POA_PRUNE_SLACK", None)
+        else:
+            os.environ["SVS_POA_PRUNE_SLACK"] = old
+    for seqs, g in zip(wins, got):
+        assert g == oracle_poa(seqs, 1)
+    if retries:
+        assert st["prune_retries"] > 0
+    else:
+        assert st["cells_computed"] < 0.6 * st["dp_cells"], st

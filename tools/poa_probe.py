@@ -24,6 +24,8 @@ out, st = poa_batch([w[0] for w in wins], return_stats=True)
 wall = time.time() - t
 st["windows_per_s"] = a.windows / wall
 st["gcups_kernel"] = st["dp_cells"] / (st["kernel_ms"] * 1e-3) / 1e9
+st["gcups_computed"] = st["cells_computed"] / (st["kernel_ms"] * 1e-3) / 1e9
+st["computed_frac"] = st["cells_computed"] / max(1, st["dp_cells"])
 st["wall_s"] = wall
 print(json.dumps(st), flush=True)
 if a.check:
