@@ -126,42 +126,61 @@ void PoaGraph::add_alignment_nodes(const std::vector<std::pair<int32_t, int32_t>
 }
 
 void PoaGraph::sort_ranks() {
+  // spoa's DFS topological sort (aligned groups kept contiguous), with the
+  // mark / ignored flags in one byte array and a raw stack: the same visit
+  // order as the textbook form, fewer instructions per visit
   const uint32_t n = num_nodes();
-  rank_to_node_.clear();
-  rank_to_node_.reserve(n);
-  std::vector<uint8_t> mark(n, 0), ignored(n, 0);
-  std::vector<uint32_t> stack;
+  rank_to_node_.resize(n);
+  uint32_t* __restrict__ order = rank_to_node_.data();
+  uint32_t cnt = 0;
+  static thread_local std::vector<uint8_t> flags;  // bits 0-1: 0 new, 1 open, 2 done; bit 2: ignored
+  static thread_local std::vector<uint32_t> stack;
+  flags.assign(n, 0);
+  if (stack.size() < e_tail_.size() + 2 * static_cast<size_t>(n) + 64) stack.resize(e_tail_.size() + 2 * n + 64);
+  uint8_t* __restrict__ fl = flags.data();
+  uint32_t* stk = stack.data();
+  const uint32_t* __restrict__ etail = e_tail_.data();
   for (uint32_t root = 0; root < n; ++root) {
-    if (mark[root] != 0) continue;
-    stack.push_back(root);
-    while (!stack.empty()) {
-      const uint32_t cur = stack.back();
+    if (fl[root] != 0) continue;
+    size_t sp = 0;
+    stk[sp++] = root;
+    while (sp != 0) {
+      const uint32_t cur = stk[sp - 1];
+      if ((fl[cur] & 3) == 2) {
+        --sp;
+        continue;
+      }
       bool ready = true;
-      if (mark[cur] != 2) {
-        for (uint32_t e : in_[cur]) {
-          const uint32_t t = e_tail_[e];
-          if (mark[t] != 2) { stack.push_back(t); ready = false; }
-        }
-        if (!ignored[cur]) {
-          for (uint32_t a : aligned_[cur]) {
-            if (mark[a] != 2) { stack.push_back(a); ignored[a] = 1; ready = false; }
-          }
-        }
-        if (ready) {
-          mark[cur] = 2;
-          if (!ignored[cur]) {
-            rank_to_node_.push_back(cur);
-            for (uint32_t a : aligned_[cur]) rank_to_node_.push_back(a);
-          }
-        } else {
-          mark[cur] = 1;
+      const NodeList& al = aligned_[cur];
+      if (sp + in_[cur].size() + al.size() + 1 > stack.size()) {
+        stack.resize(2 * stack.size());
+        stk = stack.data();
+      }
+      for (uint32_t e : in_[cur]) {
+        const uint32_t t = etail[e];
+        if ((fl[t] & 3) != 2) { stk[sp++] = t; ready = false; }
+      }
+      if (!(fl[cur] & 4)) {
+        for (uint32_t a : al) {
+          if ((fl[a] & 3) != 2) { stk[sp++] = a; fl[a] |= 4; ready = false; }
         }
       }
-      if (ready) stack.pop_back();
+      if (ready) {
+        fl[cur] = static_cast<uint8_t>((fl[cur] & 4) | 2);
+        if (!(fl[cur] & 4)) {
+          order[cnt++] = cur;
+          for (uint32_t a : al) order[cnt++] = a;
+        }
+        --sp;
+      } else {
+        fl[cur] = static_cast<uint8_t>((fl[cur] & 4) | 1);
+      }
     }
   }
-  node_to_rank_.assign(n, 0);
-  for (uint32_t r = 0; r < rank_to_node_.size(); ++r) node_to_rank_[rank_to_node_[r]] = r;
+  rank_to_node_.resize(cnt);
+  node_to_rank_.resize(n);
+  uint32_t* __restrict__ n2r = node_to_rank_.data();
+  for (uint32_t r = 0; r < cnt; ++r) n2r[order[r]] = r;
 }
 
 void PoaGraph::export_rows(RowTables* t) const {
@@ -216,85 +235,115 @@ void PoaGraph::export_rows(RowTables* t) const {
   t->n_slots = next;
 }
 
-void PoaGraph::export_strip_rows(RowTables* t) const {
+void PoaGraph::export_strip_rows(RowTables* t) const { export_strip_rows(t, nullptr); }
+
+void PoaGraph::export_strip_rows(RowTables* t, const int32_t* gaps) const {
   const uint32_t V = num_nodes();
+  const uint32_t E = static_cast<uint32_t>(e_tail_.size());  // every edge is one in-edge entry
   t->info.clear();
   t->slot.clear();
   t->pstart.resize(V + 1);
-  t->pred_row.clear();
-  t->max_preds = 0;
-  t->rec.assign(static_cast<size_t>(V) * kRecWords, 0);
-  static thread_local std::vector<uint32_t> lds_last, slot;
-  static thread_local std::vector<uint32_t> free_slots;
+  t->pred_row.resize(E);
+  t->pred_slot.resize(E);
+  t->rec.resize(static_cast<size_t>(V) * kRecWords);
+  static thread_local std::vector<uint32_t> lds_last, slot, free_slots, dmin, dmax;
   lds_last.assign(V, 0);
-  slot.assign(V, kNoSlot);
+  slot.resize(V);
   free_slots.clear();
-  uint32_t np_total = 0;
+  uint32_t* __restrict__ pred_row = t->pred_row.data();
+  uint32_t* __restrict__ pstart = t->pstart.data();
+  uint32_t* __restrict__ last = lds_last.data();
+  const uint32_t* __restrict__ n2r = node_to_rank_.data();
+  const uint32_t* __restrict__ etail = e_tail_.data();
+  // pass 1 (ranks forward): in-edge rows (CSR), per row the last row that
+  // reads it through the pool (an in-edge from the row just above does not),
+  // and with gaps = {g, e, q, c} the column-0 values (fill_col0, fused)
+  if (gaps) t->col0.resize(3 * static_cast<size_t>(V));
+  int32_t* __restrict__ c0 = gaps ? t->col0.data() : nullptr;
+  uint32_t k = 0, max_preds = 0;
   for (uint32_t r = 0; r < V; ++r) {
-    const uint32_t node = rank_to_node_[r];
-    t->pstart[r] = np_total;
-    for (uint32_t e : in_[node]) {
-      const uint32_t pr = node_to_rank_[e_tail_[e]];
-      t->pred_row.push_back(pr + 1);
-      if (pr + 1 != r) lds_last[pr] = std::max(lds_last[pr], r + 1);  // read through the pool
-      ++np_total;
+    const NodeList& in = in_[rank_to_node_[r]];
+    pstart[r] = k;
+    max_preds = std::max(max_preds, in.size());
+    int32_t F0 = INT32_MIN + 1024, O0 = INT32_MIN + 1024;
+    for (uint32_t e : in) {
+      const uint32_t pr = n2r[etail[e]];
+      pred_row[k++] = pr + 1;
+      if (pr + 1 != r && last[pr] < r + 1) last[pr] = r + 1;
+      if (c0) {
+        F0 = std::max(F0, c0[3 * pr + 1]);
+        O0 = std::max(O0, c0[3 * pr + 2]);
+      }
     }
-    t->max_preds = std::max<uint32_t>(t->max_preds, static_cast<uint32_t>(in_[node].size()));
+    if (c0) {
+      if (in.empty()) {
+        F0 = gaps[0];
+        O0 = gaps[2];
+      } else {
+        F0 += gaps[1];
+        O0 += gaps[3];
+      }
+      c0[3 * r] = std::max(F0, O0);
+      c0[3 * r + 1] = F0;
+      c0[3 * r + 2] = O0;
+    }
   }
-  t->pstart[V] = np_total;
-  t->pred_slot.assign(np_total, kNoSlot);
+  pstart[V] = k;
+  t->max_preds = max_preds;
+  // pass 2 (forward): pool slots (a slot is free again after its row's last
+  // reader) and row records w0, w1, w3
+  uint32_t* __restrict__ pslot = t->pred_slot.data();
+  uint32_t* __restrict__ rec = t->rec.data();
   uint32_t next = 1;  // slot 0: virtual row 0
   for (uint32_t r = 0; r < V; ++r) {
     const uint32_t node = rank_to_node_[r];
-    const bool store = lds_last[r] != 0;
+    const bool store = last[r] != 0;
+    uint32_t own = kNoSlot;
     if (store) {
       if (free_slots.empty()) {
-        slot[r] = next++;
+        own = next++;
       } else {
-        slot[r] = free_slots.back();
+        own = free_slots.back();
         free_slots.pop_back();
       }
     }
-    const uint32_t a = t->pstart[r], b = t->pstart[r + 1];
-    uint32_t* w = t->rec.data() + static_cast<size_t>(r) * kRecWords;
+    slot[r] = own;
+    const uint32_t a = pstart[r], b = pstart[r + 1];
+    uint32_t* w = rec + static_cast<size_t>(r) * kRecWords;
     w[0] = static_cast<uint8_t>(base_[node]) | (out_[node].empty() ? 0x100u : 0u) | (store ? 0x200u : 0u) |
-           ((b - a) << 10) | ((store ? slot[r] : kNoSlot) << 16);
-    w[1] = 0;  // a source's in-edge comes from the virtual row 0 (slot 0)
-    for (uint32_t k = a; k < b; ++k) {
-      const uint32_t pr = t->pred_row[k] - 1;
+           ((b - a) << 10) | (own << 16);
+    uint32_t w1 = 0, w3 = 0;  // a source's in-edge comes from the virtual row 0 (slot 0)
+    for (uint32_t x = a; x < b; ++x) {
+      const uint32_t pr = pred_row[x] - 1;
       const uint32_t ps = (pr + 1 == r) ? kNoSlot : slot[pr];
-      t->pred_slot[k] = ps;
-      const uint32_t i = k - a;
-      if (i < kInlinePreds) w[1] |= ps << (16 * i);
-    }
-    w[3] = 0;
-    for (uint32_t k = a; k < b; ++k) {
-      const uint32_t pr = t->pred_row[k] - 1;
-      if (pr + 1 != r && lds_last[pr] == r + 1) {
-        free_slots.push_back(slot[pr]);
-        if (slot[pr] < 32) w[3] |= 1u << slot[pr];  // the pruning kernel's liveness bits
+      pslot[x] = ps;
+      if (x - a < kInlinePreds) w1 |= ps << (16 * (x - a));
+      if (pr + 1 != r && last[pr] == r + 1) {
+        free_slots.push_back(ps);
+        if (ps < 32) w3 |= 1u << ps;  // the pruning kernel's liveness bits
       }
     }
-  }
-  // path lengths to a sink, over the rank order backwards (every out-edge
-  // leads to a higher rank)
-  static thread_local std::vector<uint32_t> dmin, dmax;
-  dmin.assign(V, 0);
-  dmax.assign(V, 0);
-  for (uint32_t r = V; r-- > 0;) {
-    const uint32_t node = rank_to_node_[r];
-    uint32_t lo = 0xFFFFFFFFu, hi = 0;
-    for (uint32_t e : out_[node]) {
-      const uint32_t h = node_to_rank_[e_head_[e]];
-      lo = std::min(lo, dmin[h] + 1);
-      hi = std::max(hi, dmax[h] + 1);
-    }
-    if (out_[node].empty()) lo = 0;
-    dmin[r] = lo;
-    dmax[r] = hi;
-    t->rec[static_cast<size_t>(r) * kRecWords + 2] = std::min(lo, 0xFFFFu) | (std::min(hi, 0xFFFFu) << 16);
+    w[1] = w1;
+    w[3] = w3;
   }
   t->n_slots = next;
+  // pass 3 (backward): fewest / most nodes on a path to a sink; every out-edge
+  // leads to a higher rank, so a row is final when the scan reaches it and
+  // pushes its values to its in-edge rows
+  dmin.assign(V, 0xFFFFFFFFu);
+  dmax.assign(V, 0);
+  uint32_t* __restrict__ lo = dmin.data();
+  uint32_t* __restrict__ hi = dmax.data();
+  for (uint32_t r = V; r-- > 0;) {
+    if (lo[r] == 0xFFFFFFFFu) lo[r] = 0;  // a sink
+    const uint32_t l1 = lo[r] + 1, h1 = hi[r] + 1;
+    for (uint32_t x = pstart[r]; x < pstart[r + 1]; ++x) {
+      const uint32_t p = pred_row[x] - 1;
+      lo[p] = std::min(lo[p], l1);
+      hi[p] = std::max(hi[p], h1);
+    }
+    rec[static_cast<size_t>(r) * kRecWords + 2] = std::min(lo[r], 0xFFFFu) | (std::min(hi[r], 0xFFFFu) << 16);
+  }
 }
 
 void fill_col0(RowTables* t, int32_t g, int32_t e, int32_t q, int32_t c) {

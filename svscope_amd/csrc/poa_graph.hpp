@@ -145,6 +145,8 @@ class PoaGraph {
   // above is served from registers.  Fills rec, pstart, pred_row, pred_slot,
   // n_slots, max_preds (info/slot are left empty).
   void export_strip_rows(RowTables* t) const;
+  // the same, also filling col0 as fill_col0(t, gaps[0..3] = g, e, q, c) does
+  void export_strip_rows(RowTables* t, const int32_t* gaps) const;
   std::vector<std::string> msa() const;
   std::string consensus(int32_t min_coverage);
 

@@ -540,8 +540,16 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     // the rows it passes, and returns the first row with such an input (or V).
     auto fast_forward = [&](uint32_t r) -> uint32_t {
       while (r < V) {
+        uint32_t lim = min(64u, V - r);  // rows this step may look at
+        if (!FIRST && WPJ > 1) {
+          // only rows strip s-1 has finished (whole 8-row lines); a full chunk
+          // is not waited for, so the scan keeps pace with its producer
+          const int32_t least = need0 + static_cast<int32_t>(min(V, r + 8));
+          if (avail < least) avail = strip_wait_ge(&prog[pw], least, &s_err);
+          lim = min(lim, static_cast<uint32_t>(min(static_cast<int32_t>(V), avail - need0)) - r);
+        }
         const uint32_t rr = r + static_cast<uint32_t>(lane);
-        const bool in = rr < V;
+        const bool in = static_cast<uint32_t>(lane) < lim;
         bool cand = false;
         if (FIRST) {
           if (in) {
@@ -549,15 +557,11 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
             cand = rc0[3 * rr] + ub_of(w2, L, P.m * L) >= lb;
           }
         } else {
-          if (WPJ > 1) {
-            const int32_t need = need0 + static_cast<int32_t>(min(V, r + 64));
-            if (avail < need) avail = strip_wait_ge(&prog[pw], need, &s_err);
-          }
           if (in) cand = __builtin_nontemporal_load(bin + 4ull * rr + 3) > SVS_VNEG / 2;
         }
         if (slot0_alive && in) cand = cand || ((rec[static_cast<uint64_t>(rr) * kRecWords] >> 10) & 31u) == 0;
         const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
-        const uint32_t n = m ? static_cast<uint32_t>(__builtin_ctzll(m)) : min(64u, V - r);
+        const uint32_t n = m ? static_cast<uint32_t>(__builtin_ctzll(m)) : lim;
         if (write_bnd && static_cast<uint32_t>(lane) < n)
           *reinterpret_cast<int4*>(bout + 4ull * rr) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
         r += n;

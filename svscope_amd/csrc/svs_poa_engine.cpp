@@ -584,9 +584,13 @@ struct PoaScheduler::Impl {
         }
         if (t.next < t.seqs.size()) {
           needs[i] = 1;
-          if (use_strip_kernel()) t.graph.export_strip_rows(&t.rows);
-          else t.graph.export_rows(&t.rows);
-          fill_col0(&t.rows, cfg.g, cfg.e, cfg.q, cfg.c);
+          if (use_strip_kernel()) {
+            const int32_t gaps[4] = {cfg.g, cfg.e, cfg.q, cfg.c};
+            t.graph.export_strip_rows(&t.rows, gaps);
+          } else {
+            t.graph.export_rows(&t.rows);
+            fill_col0(&t.rows, cfg.g, cfg.e, cfg.q, cfg.c);
+          }
         } else {
           t.consensus = t.graph.consensus(cfg.min_coverage);
           if (t.genmsa) t.msa = t.graph.msa();

@@ -579,6 +579,17 @@ void* emu_poa(int n, const char* const* seqs, const int* lens, int m, int mis, i
         aln = strip ? emu_align_strip(T, seq, P) : emu_align(T, seq, P);
       }
       auto t2 = std::chrono::steady_clock::now();
+      if (const char* rec = std::getenv("EMU_RECORD")) {
+        // alignments for tests/cpp/host_bench.cpp: length-prefixed sequence and rank pairs
+        if (FILE* f = std::fopen(rec, "ab")) {
+          const uint32_t ls = static_cast<uint32_t>(seq.size()), la = static_cast<uint32_t>(aln.size());
+          std::fwrite(&ls, 4, 1, f);
+          std::fwrite(seq.data(), 1, ls, f);
+          std::fwrite(&la, 4, 1, f);
+          std::fwrite(aln.data(), 4, la, f);
+          std::fclose(f);
+        }
+      }
       graph.add_alignment_ranks(aln, seq);
       auto t3 = std::chrono::steady_clock::now();
       r->graph_ms += std::chrono::duration<double, std::milli>((t1 - t0) + (t3 - t2)).count();

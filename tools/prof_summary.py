@@ -56,9 +56,11 @@ def pmc(d, cells_json=None):
                 st = json.loads(line)
         if st:
             res["dp_cells"] = st["dp_cells"]
+            # per cell the kernel evaluated (its exact pruning skips the rest)
+            res["cells_computed"] = st.get("cells_computed", st["dp_cells"])
             res["launches"] = st["launches"]
             if "write_bytes" in res:
-                res["hbm_bytes_per_cell"] = (res["fetch_bytes_corrected"] + res["write_bytes"]) / st["dp_cells"]
+                res["hbm_bytes_per_cell"] = (res["fetch_bytes_corrected"] + res["write_bytes"]) / res["cells_computed"]
     return res
 
 
@@ -68,16 +70,17 @@ def merge(out_json, *pmc_jsons):
     for p in pmc_jsons:
         d = json.load(open(p))
         if "FETCH_SIZE" in d.get("counter_sums", {}):
-            fetch = d["fetch_bytes_corrected"] / d["dp_cells"]
-            fetch_raw = d["fetch_bytes_raw"] / d["dp_cells"]
+            fetch = d["fetch_bytes_corrected"] / d["cells_computed"]
+            fetch_raw = d["fetch_bytes_raw"] / d["cells_computed"]
         if "WRITE_SIZE" in d.get("counter_sums", {}):
-            write = d["write_bytes"] / d["dp_cells"]
-        cells = d.get("dp_cells", cells)
+            write = d["write_bytes"] / d["cells_computed"]
+        cells = d.get("cells_computed", cells)
     res = {"kernel": "poa_strip_kernel",
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; kB x 1024; "
                      "FETCH_SIZE doubled (gfx950 under-count, MI355X_MICROARCH.md HBM section)",
            "fetch_bytes_per_cell": fetch, "fetch_bytes_per_cell_raw": fetch_raw, "write_bytes_per_cell": write,
-           "hbm_bytes_per_cell": fetch + write, "dp_cells_profiled": cells}
+           "hbm_bytes_per_cell": fetch + write, "per": "DP cell evaluated by the kernel (cells_computed)",
+           "cells_computed_profiled": cells}
     json.dump(res, open(out_json, "w"), indent=1)
     print(json.dumps(res))
 
