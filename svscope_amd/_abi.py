@@ -7,7 +7,7 @@ import ctypes
 import os
 import threading
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libsvscope_hip.so")
+LIB_PATH = os.environ.get("SVS_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libsvscope_hip.so")  # SVS_LIB_PATH: development variants
 
 SVS_OK = 0
 _ERRNAMES = {-1: "SVS_E_INVALID", -2: "SVS_E_NOMEM", -3: "SVS_E_HIP", -4: "SVS_E_UNSUPPORTED",

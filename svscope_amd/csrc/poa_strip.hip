@@ -126,7 +126,7 @@ __device__ __forceinline__ void strip_gaps_nf(const PoaScore& P, int32_t j0, int
 // Prefetched inputs of one row: its record and its carries into this strip
 // (strip 0: column-0 values H0, F0, O0 from fill_col0).
 struct RowIn {
-  uint32_t w0, w1, w2, w3;
+  uint32_t w0, w1;
   int32_t b0, b1, b2, b3;
 };
 
@@ -137,6 +137,16 @@ __device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, con
 
 }  // namespace
 
+#ifdef SVS_STRIP_PROF
+// development build only: per-wave cycle attribution summed over the launch
+// [0] sweep cycles, [1] producer waits in fetch, [2] fast_forward cycles,
+// [3] producer waits inside fast_forward, [4] computed strip rows, [5] ff calls,
+// [6] rows skipped one by one, [7] waves
+__device__ unsigned long long svs_strip_prof[8];
+#define SVS_PROF_T() __builtin_amdgcn_s_memtime()
+#define SVS_PROF_ADD(i, v) do { if (lane == 0) atomicAdd(&svs_strip_prof[i], (unsigned long long)(v)); } while (0)
+#endif
+
 // Bounded LDS-flag wait (workgroup scope); sets *err after kStripSpinLimit polls.
 constexpr long kStripSpinLimit = 1l << 26;
 __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, int32_t* err) {
@@ -144,7 +154,10 @@ __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, 
   int32_t v;
   while ((v = __builtin_amdgcn_readfirstlane(
               __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))) < target) {
-    __builtin_amdgcn_s_sleep(1);
+    // short naps first, then longer ones: a wave far behind its producer
+    // should not take issue slots from the waves that are computing
+    if (n < 8) __builtin_amdgcn_s_sleep(1);
+    else __builtin_amdgcn_s_sleep(4);
     if (++n > kStripSpinLimit) {
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return target;
@@ -158,7 +171,14 @@ __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, 
 // it publishes every 8 rows through an LDS progress counter (workgroup-scope
 // release / acquire), so the waves form a row-skewed pipeline over strips.
 template <bool LDSP, int WPJ, bool PRUNE>
-__global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
+// The pruning variant is held to 80 VGPRs (6 waves per SIMD; a few spills to
+// scratch in cold paths): measured faster than its natural 86 (5 waves),
+// profiles/r01_v36.  SVS_PRUNE_OCC overrides it in development builds.
+#ifndef SVS_PRUNE_OCC
+#define SVS_PRUNE_OCC 6
+#endif
+#define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? SVS_PRUNE_OCC : 1)))
+__global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore P, const uint32_t* __restrict__ rec_all,
     const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
     const uint32_t* __restrict__ pred_slot, const int32_t* __restrict__ col0, const uint8_t* __restrict__ seqs,
@@ -222,10 +242,16 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
   // was computed and the traceback is spoa's; otherwise the job returns
   // kPruneRetry and the host runs it again with no bound.
   const int32_t lb = J.lb;
-  const bool prune = PRUNE && lb != kNoPrune;
+  // the pruning variant prunes every job of its launch (a job without a bound
+  // gets kPruneAll, a bound below every real score: nothing is pruned)
+  constexpr bool prune = PRUNE;
   const int32_t cg = imax(imax(P.g, P.e), imax(P.q, P.c));  // best per-base gap score (<= 0, host-checked)
   uint32_t rows_done = 0;
 
+#ifdef SVS_STRIP_PROF
+  uint64_t pr_wait = 0, pr_ff = 0, pr_ffwait = 0, pr_ffn = 0, pr_slow = 0;
+  const uint64_t pr_t0 = SVS_PROF_T();
+#endif
   auto sweep = [&](auto first_tag, int32_t s) {
     constexpr bool FIRST = decltype(first_tag)::value;
     const int32_t j0 = s << 6;
@@ -242,9 +268,10 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     // slot 0 = the virtual row 0, alive when row0_h + m (L - j) reaches lb at
     // some column j0-1 .. j0+63, i.e. at j0-1: it decreases along j), and the
     // register row's liveness
-    const bool slot0_alive = FIRST || !prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb;
-    uint32_t alive = slot0_alive ? 1u : 0u;  // bit p: slot p alive (pruning: < 32 slots, host-checked)
-    bool reg_alive = false;
+    // bit p < 31: slot p alive (pruning: < 31 slots, host-checked); bit 31: the
+    // register row (the row just above) alive
+    constexpr uint32_t kRegBit = 1u << 31;
+    uint32_t alive = (FIRST || !prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb) ? 1u : 0u;
     const int32_t rrem = L - j;              // read bases after column j
     const int32_t mrr = P.m * rrem;
     // m rr + cg max(0, dmin - rr) - (m - cg) max(0, rr - dmax) as
@@ -278,12 +305,8 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     auto fetch = [&](RowIn& d, uint32_t r) {
       const uint32_t rr = r < V ? r : V - 1;
       const uint32_t* w = rec + static_cast<uint64_t>(rr) * kRecWords;
-      if constexpr (PRUNE) {
-        const uint4 v = *reinterpret_cast<const uint4*>(w);
-        d.w0 = v.x; d.w1 = v.y; d.w2 = v.z; d.w3 = v.w;
-      } else {
-        d.w0 = w[0]; d.w1 = w[1]; d.w2 = 0; d.w3 = 0;
-      }
+      d.w0 = w[0];
+      d.w1 = w[1];
       if (FIRST) {
         d.b0 = rc0[3 * rr];
         d.b1 = rc0[3 * rr + 1];
@@ -292,7 +315,15 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       } else {
         if (WPJ > 1) {
           const int32_t need = need0 + static_cast<int32_t>(rr) + 1;
-          if (avail < need) avail = strip_wait_ge(&prog[pw], need, &s_err);
+          if (avail < need) {
+#ifdef SVS_STRIP_PROF
+            const uint64_t tw = SVS_PROF_T();
+            avail = strip_wait_ge(&prog[pw], need, &s_err);
+            pr_wait += SVS_PROF_T() - tw;
+#else
+            avail = strip_wait_ge(&prog[pw], need, &s_err);
+#endif
+          }
         }
         const int4 v = *reinterpret_cast<const int4*>(bin + 4ull * rr);
         d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
@@ -308,8 +339,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       const uint32_t np = (w0 >> 10) & 31u;
       const uint32_t own = w0 >> 16;
       auto slot_alive = [&](uint32_t ps) -> bool {
-        if (ps == kNoSlot) return reg_alive;
-        return ((alive >> ps) & 1u) != 0;
+        return ((alive >> (ps == kNoSlot ? 31u : ps)) & 1u) != 0;
       };
       auto publish = [&]() {
         if (WPJ > 1 && write_bnd && ((r & 7u) == 7u || r + 1 == V) && lane == 0)
@@ -322,7 +352,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         bool live;
         if (FIRST) {
           const int32_t h0 = __builtin_amdgcn_readfirstlane(d.b0);
-          live = h0 + ub_of(__builtin_amdgcn_readfirstlane(d.w2), L, P.m * L) >= lb;
+          live = h0 + ub_of(rec[static_cast<uint64_t>(r) * kRecWords + 2], L, P.m * L) >= lb;
         } else {
           live = cH_in > SVS_VNEG / 2;
         }
@@ -344,9 +374,11 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
             reinterpret_cast<uint16_t*>(q + 65)[lane] = 0;  // F = O = H = VNEG
           }
           // own slot dead, slots whose last reader this row is (w3) released
-          alive &= ~(__builtin_amdgcn_readfirstlane(d.w3) | (store ? 1u << own : 0u));
+          alive &= ~(rec[static_cast<uint64_t>(r) * kRecWords + 3] | (store ? 1u << own : 0u) | kRegBit);
           pH = pF = pO = pHm = SVS_VNEG;
-          reg_alive = false;
+#ifdef SVS_STRIP_PROF
+          pr_slow += 1;
+#endif
           if (write_bnd && lane == 0)
             *reinterpret_cast<int4*>(bout + 4ull * r) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
           publish();
@@ -354,6 +386,9 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         }
       }
       if constexpr (PRUNE) ++rows_done;
+      // the row's path lengths (w2) and released slots (w3), needed after the DP
+      uint2 w2w3 = make_uint2(0, 0);
+      if constexpr (PRUNE) w2w3 = *reinterpret_cast<const uint2*>(rec + static_cast<uint64_t>(r) * kRecWords + 2);
       int32_t H0 = 0, F0 = 0, O0 = 0;
       StripCarry cr;
       if (FIRST) {
@@ -506,12 +541,11 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
       bool any_alive = true;
       if (prune) {
-        const int32_t ub = ub_of(__builtin_amdgcn_readfirstlane(d.w2), rrem, mrr);
+        const int32_t ub = ub_of(w2w3.x, rrem, mrr);
         any_alive = __builtin_amdgcn_ballot_w64(rrem >= 0 && H + ub >= lb) != 0;
         const bool out_alive = any_alive || cH_in > SVS_VNEG / 2;
-        reg_alive = out_alive;
-        const uint32_t ob = store ? 1u << own : 0u;
-        alive = ((alive & ~ob) | (out_alive ? ob : 0u)) & ~__builtin_amdgcn_readfirstlane(d.w3);
+        const uint32_t ob = (store ? 1u << own : 0u) | kRegBit;
+        alive = ((alive & ~ob) | (out_alive ? ob : 0u)) & ~w2w3.y;
       }
       if (store) {
         // Hx[l+1] = H[l], then Hx[l] = prevH[l] (= H[l-1], lane 0: H[j0-1]);
@@ -539,13 +573,25 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
     // Scans 64 rows per step with one load per lane, hands VNEG carries on for
     // the rows it passes, and returns the first row with such an input (or V).
     auto fast_forward = [&](uint32_t r) -> uint32_t {
+#ifdef SVS_STRIP_PROF
+      const uint64_t tf = SVS_PROF_T();
+      pr_ffn += 1;
+#endif
       while (r < V) {
         uint32_t lim = min(64u, V - r);  // rows this step may look at
         if (!FIRST && WPJ > 1) {
           // only rows strip s-1 has finished (whole 8-row lines); a full chunk
           // is not waited for, so the scan keeps pace with its producer
           const int32_t least = need0 + static_cast<int32_t>(min(V, r + 8));
-          if (avail < least) avail = strip_wait_ge(&prog[pw], least, &s_err);
+          if (avail < least) {
+#ifdef SVS_STRIP_PROF
+            const uint64_t tw = SVS_PROF_T();
+            avail = strip_wait_ge(&prog[pw], least, &s_err);
+            pr_ffwait += SVS_PROF_T() - tw;
+#else
+            avail = strip_wait_ge(&prog[pw], least, &s_err);
+#endif
+          }
           lim = min(lim, static_cast<uint32_t>(min(static_cast<int32_t>(V), avail - need0)) - r);
         }
         const uint32_t rr = r + static_cast<uint32_t>(lane);
@@ -559,7 +605,7 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         } else {
           if (in) cand = __builtin_nontemporal_load(bin + 4ull * rr + 3) > SVS_VNEG / 2;
         }
-        if (slot0_alive && in) cand = cand || ((rec[static_cast<uint64_t>(rr) * kRecWords] >> 10) & 31u) == 0;
+        if ((alive & 1u) && in) cand = cand || ((rec[static_cast<uint64_t>(rr) * kRecWords] >> 10) & 31u) == 0;
         const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
         const uint32_t n = m ? static_cast<uint32_t>(__builtin_ctzll(m)) : lim;
         if (write_bnd && static_cast<uint32_t>(lane) < n)
@@ -581,9 +627,12 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
         __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(done),
                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+#ifdef SVS_STRIP_PROF
+      pr_ff += SVS_PROF_T() - tf;
+#endif
       return r;
     };
-    auto dead_strip = [&]() { return (alive & ~1u) == 0 && !reg_alive; };
+    auto dead_strip = [&]() { return (alive & ~1u) == 0; };
 
     // rows in pairs with two statically named prefetch sets (no waits on
     // loads still in flight when a set is refilled)
@@ -632,6 +681,16 @@ __global__ __launch_bounds__(64 * WPJ) void poa_strip_kernel(
       else sweep(FalseT{}, s);
     }
   }
+#ifdef SVS_STRIP_PROF
+  SVS_PROF_ADD(0, SVS_PROF_T() - pr_t0);
+  SVS_PROF_ADD(1, pr_wait);
+  SVS_PROF_ADD(2, pr_ff);
+  SVS_PROF_ADD(3, pr_ffwait);
+  SVS_PROF_ADD(4, rows_done);
+  SVS_PROF_ADD(5, pr_ffn);
+  SVS_PROF_ADD(6, pr_slow);
+  SVS_PROF_ADD(7, 1);
+#endif
 
   // the owner of column L's strip holds the sink maximum; every wave's
   // traceback-code stores must be visible to wave 0's lane 0
@@ -784,6 +843,17 @@ int choose_strip_wpj(int device, size_t n_jobs, uint32_t lds_slots, uint32_t min
   }
   return best;
 }
+
+#ifdef SVS_STRIP_PROF
+extern "C" int svs_debug_strip_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(svs_strip_prof), sizeof(svs_strip_prof)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(svs_strip_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   if (a.n_jobs <= 0) return hipSuccess;

@@ -30,6 +30,9 @@ struct PoaJob {
 
 // PoaJob::lb value that turns the strip kernel's exact pruning off.
 constexpr int32_t kNoPrune = INT32_MIN;
+// The same for a job in a launch of the pruning variant: a bound below every
+// real score (and above the VNEG of a skipped input), so no cell is pruned.
+constexpr int32_t kPruneAll = INT32_MIN / 4;
 // aln_len[job] for a pruned job whose best sink score fell below its bound
 // (the bound was not a lower bound of the optimum: run it again unpruned).
 constexpr int32_t kPruneRetry = -2;

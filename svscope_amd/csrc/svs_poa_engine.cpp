@@ -225,7 +225,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     J.pool_off = n_pool;
     J.aln_off = n_aln;
     J.lb = prune_bound(tasks[la.ids[k]], score, J.n_rows, J.len);
-    if (J.n_slots > 32) J.lb = kNoPrune;  // the kernel tracks slot liveness in 32 bits
+    if (J.n_slots > 31) J.lb = kNoPrune;  // the kernel tracks slot liveness in 31 bits
     any_prune = any_prune || J.lb != kNoPrune;
     n_rows += J.n_rows;
     n_pstart += J.n_rows + 1;
@@ -240,6 +240,10 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   }
   if (max_preds > 31)
     throw SvsError(SVS_E_UNSUPPORTED, "a graph node has more than 31 in-edges (traceback code limit)");
+  // the pruning variant prunes every job of its launch: the others get no bound
+  if (any_prune)
+    for (PoaJob& J : la.jobs)
+      if (J.lb == kNoPrune) J.lb = kPruneAll;
   if (n_rows * kRecWords > 0xFFFFFFFFull || n_pred > 0xFFFFFFFFull || n_seq > 0xFFFFFFFFull)
     throw SvsError(SVS_E_UNSUPPORTED, "batch too large for 32-bit table offsets");
   la.n_aln = n_aln;

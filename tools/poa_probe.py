@@ -27,6 +27,14 @@ st["gcups_kernel"] = st["dp_cells"] / (st["kernel_ms"] * 1e-3) / 1e9
 st["gcups_computed"] = st["cells_computed"] / (st["kernel_ms"] * 1e-3) / 1e9
 st["computed_frac"] = st["cells_computed"] / max(1, st["dp_cells"])
 st["wall_s"] = wall
+if os.environ.get("SVS_STRIP_PROF"):
+    import ctypes
+    from svscope_amd import _abi
+    lib = _abi.load_library()
+    buf = (ctypes.c_ulonglong * 8)()
+    lib.svs_debug_strip_prof(buf, 0)
+    names = ["sweep_cyc", "fetch_wait_cyc", "ff_cyc", "ff_wait_cyc", "rows_computed", "ff_calls", "slow_skips", "waves"]
+    st["strip_prof"] = dict(zip(names, list(buf)))
 print(json.dumps(st), flush=True)
 if a.check:
     from oracle.spoa_oracle import poa as oracle_poa
