@@ -43,6 +43,7 @@ struct PoaTask {
   double rate = 0.0;      // best score / read length of the last alignment that needed no retry
   bool have_rate = false;
   bool retry = false;     // the current sequence's pruned run missed its bound: run it unpruned
+  uint8_t prepped = 0;    // next step already readied after the fold: 1 export done, 2 complete
   uint8_t n_retries = 0;
 
   std::string consensus;

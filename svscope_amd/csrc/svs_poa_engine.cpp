@@ -438,11 +438,39 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, c
   st.d2h_bytes += n_aln * 8 + nj * 4;
 }
 
-// Waits for the launch and folds its alignments back into the graphs.  While
+// Readies a task's next step: sequences landing on an empty graph become a
+// fresh chain (no DP), empty ones are skipped; then either the row tables of
+// the next alignment are exported (returns 1) or, with every sequence in, the
+// consensus and MSA are computed (returns 2).
+uint8_t prep_task(PoaTask& t, const svs_poa_config& cfg) {
+  while (t.next < t.seqs.size()) {
+    const std::string& s = t.seqs[t.next];
+    if (s.empty()) { ++t.next; continue; }
+    if (t.graph.empty()) { t.graph.add_alignment_nodes({}, s); ++t.next; continue; }
+    break;
+  }
+  if (t.next < t.seqs.size()) {
+    if (use_strip_kernel()) {
+      const int32_t gaps[4] = {cfg.g, cfg.e, cfg.q, cfg.c};
+      t.graph.export_strip_rows(&t.rows, gaps);
+    } else {
+      t.graph.export_rows(&t.rows);
+      fill_col0(&t.rows, cfg.g, cfg.e, cfg.q, cfg.c);
+    }
+    return 1;
+  }
+  t.consensus = t.graph.consensus(cfg.min_coverage);
+  if (t.genmsa) t.msa = t.graph.msa();
+  return 2;
+}
+
+// Waits for the launch and folds its alignments back into the graphs, each
+// task's next step readied right after its fold while its graph is in cache
+// (prep_task; PoaTask::prepped).  While
 // the launch is still running, `idle` (if given) is called for host work that
 // is off the critical path until it returns false.
 void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_stats& st, double& host_ms,
-            const std::function<bool()>& idle = nullptr) {
+            const svs_poa_config& cfg, const std::function<bool()>& idle = nullptr) {
   PoaArena& A = *la.arena;
   const auto tw0 = Clock::now();
   if (idle) {
@@ -480,8 +508,10 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
     auto& t = tasks[la.ids[k]];
     if (strip && n == kPruneRetry) {
       // the bound was above the optimum: the same sequence again, unpruned
+      // (its row tables are still those of this step)
       t.retry = true;
       t.n_retries += 1;
+      t.prepped = 1;
       return;
     }
     if (n < 0) throw SvsError(SVS_E_INTERNAL, "GPU traceback reported an inconsistent path");
@@ -501,6 +531,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
     }
     t.graph.add_alignment_ranks(fwd, t.seqs[t.next]);
     ++t.next;
+    t.prepped = prep_task(t, cfg);
   });
   host_ms += ms_since(th0);
   g_trace.host("fold", la.gid, th0, la.ids.size());
@@ -580,25 +611,9 @@ struct PoaScheduler::Impl {
       // sequences landing on an empty graph become a fresh chain (no DP)
       ctx->pool->parallel_for(g.active.size(), [&](size_t i) {
         PoaTask& t = tasks[g.active[i]];
-        while (t.next < t.seqs.size()) {
-          const std::string& s = t.seqs[t.next];
-          if (s.empty()) { ++t.next; continue; }
-          if (t.graph.empty()) { t.graph.add_alignment_nodes({}, s); ++t.next; continue; }
-          break;
-        }
-        if (t.next < t.seqs.size()) {
-          needs[i] = 1;
-          if (use_strip_kernel()) {
-            const int32_t gaps[4] = {cfg.g, cfg.e, cfg.q, cfg.c};
-            t.graph.export_strip_rows(&t.rows, gaps);
-          } else {
-            t.graph.export_rows(&t.rows);
-            fill_col0(&t.rows, cfg.g, cfg.e, cfg.q, cfg.c);
-          }
-        } else {
-          t.consensus = t.graph.consensus(cfg.min_coverage);
-          if (t.genmsa) t.msa = t.graph.msa();
-        }
+        const uint8_t state = t.prepped ? t.prepped : prep_task(t, cfg);
+        t.prepped = 0;
+        needs[i] = state == 1 ? 1 : 0;
       });
       std::vector<uint32_t> ids, fin;
       for (size_t i = 0; i < g.active.size(); ++i) (needs[i] ? ids : fin).push_back(g.active[i]);
@@ -642,7 +657,7 @@ struct PoaScheduler::Impl {
         sub.arena = g.arena;
         sub.gid = gid(g);
         pack_and_launch(ctx, sub, tasks, score, st, host_ms);
-        finish(ctx, sub, tasks, st, host_ms);
+        finish(ctx, sub, tasks, st, host_ms, cfg);
         first = last;
       }
     }
@@ -675,7 +690,7 @@ struct PoaScheduler::Impl {
       bool progressed = false;
       for (Group& g : groups) {
         if (!g.pending) continue;
-        finish(ctx, g.la, tasks, st, host_ms, [this] { return reap(); });
+        finish(ctx, g.la, tasks, st, host_ms, cfg, [this] { return reap(); });
         g.pending = false;
         advance(g, done);
         progressed = true;
