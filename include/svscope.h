@@ -204,6 +204,36 @@ int svs_msa_features(int32_t n_rows, int32_t width, const char* msa, const char*
                      int32_t n_ids, int32_t hcutoff, double scutoff, int32_t* rows, int32_t* n_feat,
                      uint8_t* feat, int64_t feat_cap, int32_t* id_map, int32_t* n_map, int64_t id_cap);
 
+/* ---------------------------------------------------------------- MisScore
+ * PairwiseCompare.AligmentScore (PairwiseCompare.py:19-30) for many pairs:
+ *   alignment = Bio.pairwise2.align.globalms(som, ger, 1, 0, -1, -1)[0]
+ *   alig      = format_alignment(*alignment).split('\n')[1][cutoff:len-cutoff]
+ *   MisScore  = len(alig) - alig.count('|')
+ * Pair p aligns sequence pair_a[p] (SomConsensus) against pair_b[p]
+ * (GerConsensus); sequence s is seq_bytes[seq_byte_start[s] .. seq_byte_start[s+1]).
+ * Writes out_len[p] = len(alig), out_match[p] = count('|') and out_status[p]:
+ * SVS_MS_OK, or SVS_MS_EMPTY when a sequence is empty (pairwise2 returns no
+ * alignment and the reference's [0] raises IndexError).  cutoff 0..64.
+ * Replaces the per-pair Biopython call made by CalculateMisscore
+ * (PairwiseCompare.py:54-64) over the rows of MisScorePipe (:76-86). */
+#define SVS_MS_OK 0
+#define SVS_MS_EMPTY 4
+
+typedef struct svs_misscore_stats {
+  uint64_t pairs;       /* pairs aligned on the GPU (non-empty) */
+  uint64_t dp_cells;    /* sum of len(som) * len(ger) */
+  uint64_t nib_bytes;   /* 4-bit score-difference bytes written (HBM) */
+  uint64_t launches;
+  uint64_t tb_steps;    /* traceback DFS steps */
+  double fill_ms;       /* DP kernel time (HIP events) */
+  double traceback_ms;  /* traceback kernel time */
+  double wall_ms;
+} svs_misscore_stats;
+
+int svs_aligment_score_batch(svs_context* ctx, int32_t n_pairs, const int32_t* pair_a, const int32_t* pair_b,
+                             int32_t n_seqs, const int64_t* seq_byte_start, const char* seq_bytes, int32_t cutoff,
+                             int32_t* out_len, int32_t* out_match, int32_t* out_status, svs_misscore_stats* stats);
+
 /* Wave-primitive self test (GPU tests): per 64-lane wave, inclusive prefix max
  * and shift-right-by-one (lane 0 <- -7). */
 int svs_wave_selftest(svs_context* ctx, const int32_t* in, int32_t* scan, int32_t* shift,

@@ -71,6 +71,18 @@ class DecisionStats(ctypes.Structure):
 
 DEC_NO_EM, DEC_EM, DEC_EMOUTPUT, DEC_INDEX_ERROR = 0, 1, 2, 3
 
+
+class MisscoreStats(ctypes.Structure):
+    _fields_ = [("pairs", ctypes.c_uint64), ("dp_cells", ctypes.c_uint64), ("nib_bytes", ctypes.c_uint64),
+                ("launches", ctypes.c_uint64), ("tb_steps", ctypes.c_uint64), ("fill_ms", ctypes.c_double),
+                ("traceback_ms", ctypes.c_double), ("wall_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+MS_OK, MS_EMPTY = 0, 4
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -149,6 +161,8 @@ def _declare_em(lib):
     lib.svs_em_result_get.restype = ctypes.c_int
     lib.svs_em_result_free.argtypes = [P]
     lib.svs_em_result_free.restype = None
+    lib.svs_aligment_score_batch.argtypes = [P, I32, P, P, I32, P, P, I32, P, P, P, ctypes.POINTER(MisscoreStats)]
+    lib.svs_aligment_score_batch.restype = ctypes.c_int
 
 
 def check(rc, what="svscope call"):

@@ -24,6 +24,7 @@ SOURCES = [
     "poa_kernels.hip",
     "poa_strip.hip",
     "em_kernels.hip",
+    "misscore_kernels.hip",
     "poa_graph.cpp",
     "svs_threadpool.cpp",
     "ward.cpp",
@@ -31,6 +32,7 @@ SOURCES = [
     "svs_decision.cpp",
     "svs_poa_engine.cpp",
     "svs_em_engine.cpp",
+    "svs_misscore_engine.cpp",
     "svs_abi.cpp",
 ]
 

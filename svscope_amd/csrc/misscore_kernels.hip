@@ -1,0 +1,176 @@
+// MisScore on gfx950: Biopython pairwise2.align.globalms(som, ger, 1, 0, -1, -1)[0]
+// and its match-line counts for many (somatic, germline) consensus pairs
+// (reference: /root/reference/src/PairwiseCompare.py:19-30 AligmentScore,
+// called by CalculateMisscore :54-64 for every pair of a Raw.bed row).
+//
+// Two kernels per launch:
+//
+// misscore_fill_kernel — one wave per pair.  The DP matrix (rows = som,
+// columns = ger) is swept in 64-column strips; inside a strip lane k owns
+// column c0 + k and works one row behind lane k - 1 (a diagonal wavefront),
+// so each step is one DPP lane shift plus a max3:
+//   H[r][c] = max(H[r-1][c-1] + (a == b), max(H[r-1][c], H[r][c-1]) - 1)
+// (linear gaps: pairwise2's row/col scores equal H - 1 of the left/upper
+// cell, see misscore_tb.hpp).  Only the two score differences
+// dh = H[r][c] - H[r][c-1] and dv = H[r][c] - H[r-1][c] leave the kernel, two
+// bits each, eight rows of one column per 32-bit word:
+//   word index = (strip * n_groups + (t - 1) / 8) * 64 + lane,
+//   nibble     = (t - 1) % 8,  t = r + lane (the step that computed the cell),
+// so all 64 lanes close a word on the same step: one coalesced 256-B store
+// every 8 steps.
+// 0.5 B per cell of HBM writes instead of pairwise2's int score + trace.
+// The H column at a strip's right edge is handed to the next strip through a
+// per-pair carry vector (one int32 per row, in place, 64 rows per coalesced
+// load/store, loaded one 64-step chunk ahead); the A characters stream in the
+// same way.  The 64 steps of a chunk are unrolled, so lane selects are
+// immediates and stores sit at fixed positions.
+//
+// misscore_traceback_kernel — one lane per pair replays pairwise2's DFS
+// (misscore_tb.hpp) over the nibbles with an explicit stack in HBM.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#define SVS_MS_FN __device__ __forceinline__
+#include "misscore_device.hpp"
+
+namespace svs {
+
+namespace {
+
+// lane l <- x[l-1]; lane 0 <- fill.  DPP wave_shr:1 (bound_ctrl off keeps old).
+__device__ __forceinline__ int32_t shr1(int32_t x, int32_t fill) {
+  return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xF, 0xF, false);
+}
+// lane l <- x[l+1] (lane 63 keeps x).  DPP wave_shl:1.
+__device__ __forceinline__ int32_t shl1(int32_t x) { return __builtin_amdgcn_update_dpp(x, x, 0x130, 0xF, 0xF, false); }
+// lane l <- x[l-1], lane 0 <- x[63].  DPP wave_ror:1.
+__device__ __forceinline__ int32_t ror1(int32_t x) { return __builtin_amdgcn_update_dpp(x, x, 0x13C, 0xF, 0xF, false); }
+
+__global__ __launch_bounds__(256) void misscore_fill_kernel(const MsPair* __restrict__ pairs, int n_pairs,
+                                                            const uint8_t* __restrict__ seqs,
+                                                            uint32_t* __restrict__ nib, int32_t* __restrict__ carry) {
+  const int pid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pid >= n_pairs) return;
+  const int lane = threadIdx.x & 63;
+  const MsPair P = pairs[pid];
+  const int32_t la = P.la, lb = P.lb;
+  const int32_t n_chunks = ms_chunks(la);
+  const int32_t n_strips = (lb + 63) >> 6;
+  const uint8_t* A = seqs + P.a_off;
+  const uint8_t* B = seqs + P.b_off;
+  int32_t* cr = carry + P.carry_off;  // cr[r - 1] = H[r][c0 - 1] of the current strip
+  for (int32_t s = 0; s < n_strips; ++s) {
+    const int32_t c = s * 64 + lane + 1;
+    const bool col_ok = c <= lb;
+    const int32_t bc = col_ok ? static_cast<int32_t>(B[c - 1]) : -1;
+    const bool last = s == n_strips - 1;
+    int32_t h = -c;           // H[r-1][c]: row 0 is -c
+    int32_t diag = -(c - 1);  // H[r-1][c-1]
+    int32_t ach = 0;          // A[r-1] of this lane's row
+    int32_t cout = 0;         // H of lane 63's rows in this chunk (lane j: step 63 - j)
+    uint32_t* out = nib + P.nib_off + static_cast<uint64_t>(s) * n_chunks * 8 * 64 + lane;
+    // chunk 0: rows 1..64 (lane j holds row 1 + j)
+    int32_t nxt_c, nxt_a;
+    {
+      const int32_t rr = 1 + lane;
+      const bool ok = rr <= la;
+      nxt_c = s == 0 ? -rr : (ok ? cr[rr - 1] : 0);
+      nxt_a = ok ? static_cast<int32_t>(A[rr - 1]) : 0;
+    }
+    for (int32_t ch = 0; ch < n_chunks; ++ch) {
+      int32_t cc = nxt_c, ca = nxt_a;  // lane 0 holds this step's left H / A character
+      {  // prefetch the next chunk's left column and A characters
+        const int32_t rr = 64 * (ch + 1) + 1 + lane;
+        const bool ok = rr <= la;
+        nxt_c = s == 0 ? -rr : (ok ? cr[rr - 1] : 0);
+        nxt_a = ok ? static_cast<int32_t>(A[rr - 1]) : 0;
+      }
+      // step t = 64 ch + u + 1; lane k is at row r = t - k
+      const int32_t rm1_base = 64 * ch - lane;  // r - 1 at u = 0
+      uint32_t acc = 0;
+#pragma unroll
+      for (int32_t u = 0; u < 64; ++u) {
+        const int32_t left = shr1(h, cc);  // lane 0 keeps cc (its left neighbour)
+        ach = shr1(ach, ca);
+        cc = shl1(cc);
+        ca = shl1(ca);
+        const int32_t sc = ach == bc ? 1 : 0;
+        const int32_t hn = max(diag + sc, max(h, left) - 1);
+        const bool act = static_cast<uint32_t>(rm1_base + u) < static_cast<uint32_t>(la);
+        const uint32_t code = static_cast<uint32_t>(hn - left + 1) | (static_cast<uint32_t>(hn - h + 1) << 2);
+        acc |= (act ? code : 0u) << ((u & 7) * 4);
+        diag = act ? left : diag;
+        h = act ? hn : h;
+        if ((u & 7) == 7) {  // every lane closes an 8-step group together
+          if (col_ok) out[static_cast<uint64_t>(ch * 8 + (u >> 3)) * 64] = acc;
+          acc = 0;
+        }
+        // history of lane 63's H: lane j ends with the value of step 63 - j
+        cout = shr1(cout, ror1(h));
+      }
+      if (!last) {  // lane 63's rows of this chunk: step u = 63 - lane, row t - 63 = 64 ch + u - 62
+        const int32_t row = 64 * ch + 1 - lane;
+        if (row >= 1 && row <= la) cr[row - 1] = cout;
+      }
+    }
+    // the next strip reads the carries this wave just wrote
+    __threadfence_block();
+  }
+}
+
+struct DevEnv {
+  const uint32_t* nibs;
+  const uint8_t* A;
+  const uint8_t* B;
+  MsState* stack;
+  uint32_t cap;
+  uint32_t top;
+  int32_t n_groups;
+  int32_t max_depth;
+  __device__ __forceinline__ uint32_t nib(int32_t r, int32_t c) const {
+    // lane k of strip s holds row r at step t = r + k: word (s, (t-1)/8, k), nibble (t-1)%8
+    const int32_t k = (c - 1) & 63, t1 = r - 1 + k;
+    const uint32_t w = nibs[(static_cast<uint64_t>((c - 1) >> 6) * n_groups + (t1 >> 3)) * 64 + k];
+    return (w >> ((t1 & 7) * 4)) & 15u;
+  }
+  __device__ __forceinline__ uint8_t a(int32_t i) const { return A[i]; }
+  __device__ __forceinline__ uint8_t b(int32_t j) const { return B[j]; }
+  __device__ __forceinline__ bool push(const MsState& s) {
+    if (top >= cap) return false;
+    stack[top++] = s;
+    return true;
+  }
+  __device__ __forceinline__ void pop(MsState& s) { s = stack[--top]; }
+};
+
+__global__ __launch_bounds__(64) void misscore_traceback_kernel(const MsPair* __restrict__ pairs, int n_pairs,
+                                                                const uint8_t* __restrict__ seqs,
+                                                                const uint32_t* __restrict__ nib,
+                                                                MsState* __restrict__ stack, int32_t cutoff,
+                                                                MsResult* __restrict__ out) {
+  const int pid = blockIdx.x * 64 + threadIdx.x;
+  if (pid >= n_pairs) return;
+  const MsPair P = pairs[pid];
+  DevEnv env{nib + P.nib_off, seqs + P.a_off, seqs + P.b_off, stack + P.stack_off, P.stack_cap, 0,
+             ms_chunks(P.la) * 8, 0};
+  const int64_t max_steps = 8ll * (P.la + P.lb) + 4096;
+  out[P.out_idx] = ms_first_alignment(env, P.la, P.lb, cutoff, max_steps);
+}
+
+}  // namespace
+
+hipError_t launch_misscore(const MsPair* pairs, int n_pairs, const uint8_t* seqs, uint32_t* nib, int32_t* carry,
+                           MsState* stack, int32_t cutoff, MsResult* out, hipStream_t stream,
+                           hipEvent_t ev_fill_start, hipEvent_t ev_fill_end) {
+  if (n_pairs <= 0) return hipSuccess;
+  if (ev_fill_start) (void)hipEventRecord(ev_fill_start, stream);
+  misscore_fill_kernel<<<(n_pairs + 3) / 4, 256, 0, stream>>>(pairs, n_pairs, seqs, nib, carry);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (ev_fill_end) (void)hipEventRecord(ev_fill_end, stream);
+  misscore_traceback_kernel<<<(n_pairs + 63) / 64, 64, 0, stream>>>(pairs, n_pairs, seqs, nib, stack, cutoff, out);
+  return hipGetLastError();
+}
+
+}  // namespace svs

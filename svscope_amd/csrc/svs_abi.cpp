@@ -108,7 +108,9 @@ void svs_release(svs_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->em_stream) (void)hipStreamSynchronize(ctx->em_stream);
   ctx->poa_arenas.clear();
-  for (svs::DeviceBuf* b : {&ctx->d_em_in, &ctx->d_em_ws, &ctx->d_em_out, &ctx->d_rng}) b->release();
+  for (svs::DeviceBuf* b : {&ctx->d_em_in, &ctx->d_em_ws, &ctx->d_em_out, &ctx->d_rng, &ctx->d_ms_pairs,
+                            &ctx->d_ms_seq, &ctx->d_ms_nib, &ctx->d_ms_carry, &ctx->d_ms_stack, &ctx->d_ms_out})
+    b->release();
   for (svs::PinnedBuf* b : {&ctx->h_em_in, &ctx->h_em_out}) b->release();
   if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
   if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
@@ -352,6 +354,29 @@ int svs_wave_selftest(svs_context* ctx, const int32_t* in, int32_t* scan, int32_
     if (e == hipSuccess) e = hipMemcpy(shift, d + 2 * n_waves * 64, bytes, hipMemcpyDeviceToHost);
     (void)hipFree(d);
     SVS_HIP(e);
+  });
+}
+
+int svs_aligment_score_batch(svs_context* ctx, int32_t n_pairs, const int32_t* pair_a, const int32_t* pair_b,
+                             int32_t n_seqs, const int64_t* seq_byte_start, const char* seq_bytes, int32_t cutoff,
+                             int32_t* out_len, int32_t* out_match, int32_t* out_status, svs_misscore_stats* stats) {
+  if (!ctx || n_pairs < 0 || n_seqs < 0 ||
+      (n_pairs > 0 && (!pair_a || !pair_b || !seq_byte_start || !out_len || !out_match || !out_status)))
+    return fail(SVS_E_INVALID, "svs_aligment_score_batch: invalid argument");
+  if (cutoff < 0 || cutoff > 64)
+    return fail(SVS_E_UNSUPPORTED, "svs_aligment_score_batch: cutoff must be 0..64");
+  return guarded([&] {
+    for (int32_t s = 0; s < n_seqs; ++s)
+      if (seq_byte_start[s] < 0 || seq_byte_start[s + 1] < seq_byte_start[s])
+        throw svs::SvsError(SVS_E_INVALID, "seq_byte_start not monotone");
+    if (n_seqs > 0 && seq_byte_start[n_seqs] > seq_byte_start[0] && !seq_bytes)
+      throw svs::SvsError(SVS_E_INVALID, "null seq_bytes");
+    for (int32_t p = 0; p < n_pairs; ++p)
+      if (pair_a[p] < 0 || pair_a[p] >= n_seqs || pair_b[p] < 0 || pair_b[p] >= n_seqs)
+        throw svs::SvsError(SVS_E_INVALID, "pair " + std::to_string(p) + ": sequence index out of range");
+    SVS_HIP(hipSetDevice(ctx->device));
+    svs::run_misscore(ctx, n_pairs, pair_a, pair_b, seq_byte_start, seq_bytes, cutoff, out_len, out_match,
+                      out_status, stats);
   });
 }
 

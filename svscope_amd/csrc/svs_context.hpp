@@ -123,6 +123,8 @@ struct svs_context {
   // EM arenas
   svs::DeviceBuf d_em_in, d_em_ws, d_em_out, d_rng;
   svs::PinnedBuf h_em_in, h_em_out;
+  // MisScore arenas (svs_misscore_engine.cpp)
+  svs::DeviceBuf d_ms_pairs, d_ms_seq, d_ms_nib, d_ms_carry, d_ms_stack, d_ms_out;
   size_t rng_len = 0;
   uint32_t rng_seed = 0;
 };

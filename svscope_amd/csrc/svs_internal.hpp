@@ -91,6 +91,10 @@ class ThreadPool;
 svs_em_result* run_em_cluster(svs_context* ctx, int32_t n, const svs_em_window* wins, const uint8_t* X,
                               const svs_em_config& cfg, ThreadPool* pool);
 
+void run_misscore(svs_context* ctx, int32_t n_pairs, const int32_t* pair_a, const int32_t* pair_b,
+                  const int64_t* seq_byte_start, const char* seq_bytes, int32_t cutoff, int32_t* out_len,
+                  int32_t* out_match, int32_t* out_status, svs_misscore_stats* st);
+
 svs_decision_result* run_decision(svs_context* ctx, int32_t n, const svs_decision_window* wins,
                                   const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
                                   const uint8_t* is_tlabel, const svs_decision_config& cfg);
