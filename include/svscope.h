@@ -14,6 +14,9 @@
  *              M-step 162-188, loglik 104-122, BIC 211-219)
  *              -> svs_similarity_batch (pariwiseDistance, :52-59) and
  *                 svs_em_batch (everything after scipy's ward/fcluster init)
+ *   MisScore   PairwiseCompare.AligmentScore / CalculateMisscore
+ *              PairwiseCompare.py:19-30,54-64 (Bio.pairwise2 globalms, AlnFeature
+ *              via SVscope.py:282) -> svs_aligment_score_batch
  */
 #ifndef SVSCOPE_H
 #define SVSCOPE_H
