@@ -154,7 +154,7 @@ def main():
     if rank == 0:
         cpu = None
         n_cpu = args.cpu_sample
-        if n_cpu != 0:
+        if n_cpu != 0 and world == 1:  # the CPU baseline is an N=1 figure
             cores = min(16, os.cpu_count() or 1)
             if n_cpu < 0:
                 n_cpu = cores

@@ -83,12 +83,23 @@ struct PinnedBuf {
 struct PoaArena {
   DeviceBuf d_in, d_tb, d_pool, d_aln, d_alen;
   PinnedBuf h_in, h_aln, h_alen;
-  hipStream_t stream = nullptr;       // shared kernel stream
+  hipStream_t stream = nullptr;       // kernel stream (shared, or this group's own)
   hipStream_t copy_stream = nullptr;  // this group's copies
+  bool own = false;                   // stream is this group's, copies ride on it too
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr, h2d = nullptr;
+  // s == nullptr: the group gets one stream of its own for copies and kernels,
+  // so its kernel can start while the other group's launch is still draining
+  // (its last, longest jobs leave most CUs idle); otherwise kernels of both
+  // groups alternate on the shared stream s and copies go to a copy stream.
   PoaArena(int device, hipStream_t s) : stream(s) {
     SVS_HIP(hipSetDevice(device));
-    SVS_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+    if (!s) {
+      own = true;
+      SVS_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+      copy_stream = stream;
+    } else {
+      SVS_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+    }
     SVS_HIP(hipEventCreate(&ev0));
     SVS_HIP(hipEventCreate(&ev1));
     SVS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
@@ -103,7 +114,7 @@ struct PoaArena {
     if (ev1) (void)hipEventDestroy(ev1);
     if (done) (void)hipEventDestroy(done);
     if (h2d) (void)hipEventDestroy(h2d);
-    if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);  // == stream when own
   }
   PoaArena(const PoaArena&) = delete;
   PoaArena& operator=(const PoaArena&) = delete;

@@ -572,7 +572,14 @@ struct PoaScheduler::Impl {
   Impl(svs_context* c, const svs_poa_config& k, svs_poa_stats& s)
       : ctx(c), cfg(k), score{k.m, k.n, k.g, k.e, k.q, k.c}, st(s), cap(active_jobs_per_group()),
         budget(c->device_budget / 2) {
-    while (ctx->poa_arenas.size() < 2) ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
+    // Both groups' kernels alternate on the context's one stream.
+    // SVS_POA_STREAMS=2 gives each group a stream of its own so the next
+    // launch can overlap the other's tail: measured no faster (196.9 vs 202.0
+    // windows/s, profiles/r01_v40), so it stays a development option.
+    const char* ns = std::getenv("SVS_POA_STREAMS");
+    const bool shared = !(ns && std::atoi(ns) == 2);
+    while (ctx->poa_arenas.size() < 2)
+      ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, shared ? ctx->stream : nullptr));
     for (int g = 0; g < 2; ++g) groups[g].arena = ctx->poa_arenas[g].get();
   }
 
