@@ -25,6 +25,16 @@ struct MsPair {
   int32_t pad;
 };
 
+// Two pairs swept together by the packed int16 fill kernel (y = -1: x alone).
+struct MsDuo {
+  int32_t x, y;        // indices into the launch's MsPair array
+  uint32_t carry_off;  // int32 (two int16 halves) into the carry buffer, max(la) entries
+  int32_t pad;
+};
+
+// Longest sequence the packed int16 fill takes (|H| <= max(la, lb) < 2^15).
+constexpr int32_t kMsPackedMaxLen = 30000;
+
 // 64-step chunks of one strip: la + 63 steps (lane 63 trails lane 0 by 63 rows)
 __host__ __device__ inline int32_t ms_chunks(int32_t la) { return (la + 63 + 63) / 64; }
 inline uint64_t ms_nib_words(int32_t la, int32_t lb) {
@@ -32,8 +42,11 @@ inline uint64_t ms_nib_words(int32_t la, int32_t lb) {
 }
 inline uint32_t ms_stack_cap(int32_t la, int32_t lb) { return 2u * static_cast<uint32_t>(la + lb) + 256u; }
 
-hipError_t launch_misscore(const MsPair* pairs, int n_pairs, const uint8_t* seqs, uint32_t* nib, int32_t* carry,
-                           MsState* stack, int32_t cutoff, MsResult* out, hipStream_t stream,
-                           hipEvent_t ev_fill_start, hipEvent_t ev_fill_end);
+// Fills the duos with the packed int16 kernel and the pairs listed in solo
+// with the int32 kernel, then runs the traceback of every pair.
+hipError_t launch_misscore(const MsPair* pairs, int n_pairs, const MsDuo* duos, int n_duos, const int32_t* solo,
+                           int n_solo, const uint8_t* seqs, uint32_t* nib, int32_t* carry, MsState* stack,
+                           int32_t cutoff, MsResult* out, hipStream_t stream, hipEvent_t ev_fill_start,
+                           hipEvent_t ev_fill_end);
 
 }  // namespace svs

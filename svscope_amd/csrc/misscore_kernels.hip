@@ -47,13 +47,14 @@ __device__ __forceinline__ int32_t shl1(int32_t x) { return __builtin_amdgcn_upd
 // lane l <- x[l-1], lane 0 <- x[63].  DPP wave_ror:1.
 __device__ __forceinline__ int32_t ror1(int32_t x) { return __builtin_amdgcn_update_dpp(x, x, 0x13C, 0xF, 0xF, false); }
 
-__global__ __launch_bounds__(256) void misscore_fill_kernel(const MsPair* __restrict__ pairs, int n_pairs,
+__global__ __launch_bounds__(256) void misscore_fill_kernel(const MsPair* __restrict__ pairs,
+                                                            const int32_t* __restrict__ solo, int n_solo,
                                                             const uint8_t* __restrict__ seqs,
                                                             uint32_t* __restrict__ nib, int32_t* __restrict__ carry) {
-  const int pid = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (pid >= n_pairs) return;
+  const int sid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (sid >= n_solo) return;
   const int lane = threadIdx.x & 63;
-  const MsPair P = pairs[pid];
+  const MsPair P = pairs[solo[sid]];
   const int32_t la = P.la, lb = P.lb;
   const int32_t n_chunks = ms_chunks(la);
   const int32_t n_strips = (lb + 63) >> 6;
@@ -119,6 +120,109 @@ __global__ __launch_bounds__(256) void misscore_fill_kernel(const MsPair* __rest
   }
 }
 
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_s(int32_t x) { return __builtin_bit_cast(s16x2, x); }
+__device__ __forceinline__ int32_t as_i(s16x2 v) { return __builtin_bit_cast(int32_t, v); }
+__device__ __forceinline__ int32_t as_i(u16x2 v) { return __builtin_bit_cast(int32_t, v); }
+__device__ __forceinline__ int32_t pack2(int32_t lo, int32_t hi) {
+  return static_cast<int32_t>((static_cast<uint32_t>(lo) & 0xFFFFu) | (static_cast<uint32_t>(hi) << 16));
+}
+
+// misscore_fill_kernel for two pairs at once (a "duo"): the low 16-bit half of
+// every register belongs to pair X, the high half to pair Y, and the step runs
+// on packed VOP3P math (v_pk_add/sub/max/min_*16), so one VALU instruction
+// advances two cells.  Both pairs sweep max(la) x max(lb); cells outside a
+// pair's own matrix are computed but never stored, and they only ever feed
+// cells further right or down, outside it too.  Scores fit in 16 bits:
+// |H| <= max(la, lb) <= kMsPackedMaxLen (host-checked).  Each 8-step group's
+// two 4-step accumulators are split into X's and Y's 32-bit words with
+// v_perm, so the nibble layout is the 32-bit kernel's.
+__global__ __launch_bounds__(256) void misscore_fill2_kernel(const MsPair* __restrict__ pairs,
+                                                             const MsDuo* __restrict__ duos, int n_duos,
+                                                             const uint8_t* __restrict__ seqs,
+                                                             uint32_t* __restrict__ nib, int32_t* __restrict__ carry) {
+  const int did = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (did >= n_duos) return;
+  const int lane = threadIdx.x & 63;
+  const MsDuo D = duos[did];
+  const MsPair X = pairs[D.x];
+  const bool has_y = D.y >= 0;
+  const MsPair Y = pairs[has_y ? D.y : D.x];
+  const int32_t la = max(X.la, Y.la), lb = max(X.lb, Y.lb);
+  const int32_t n_chunks = ms_chunks(la);
+  const int32_t gx = ms_chunks(X.la) * 8, gy = ms_chunks(Y.la) * 8;  // each pair's own word rows per strip
+  const int32_t n_strips = (lb + 63) >> 6;
+  const uint8_t* AX = seqs + X.a_off;
+  const uint8_t* AY = seqs + Y.a_off;
+  const uint8_t* BX = seqs + X.b_off;
+  const uint8_t* BY = seqs + Y.b_off;
+  int32_t* cr = carry + D.carry_off;  // packed H[r][c0 - 1]
+  const u16x2 one = {1, 1};
+  for (int32_t s = 0; s < n_strips; ++s) {
+    const int32_t c = s * 64 + lane + 1;
+    const bool okx = c <= X.lb, oky = has_y && c <= Y.lb;
+    // 0x100 never equals a character
+    const int32_t bc = pack2(okx ? BX[c - 1] : 0x100, oky ? BY[c - 1] : 0x100);
+    const bool last = s == n_strips - 1;
+    int32_t h = pack2(-c, -c);
+    int32_t diag = pack2(-(c - 1), -(c - 1));
+    int32_t ach = 0, cout = 0;
+    uint32_t* outx = nib + X.nib_off + static_cast<uint64_t>(s) * gx * 64 + lane;
+    uint32_t* outy = nib + Y.nib_off + static_cast<uint64_t>(s) * gy * 64 + lane;
+    auto chunk_in = [&](int32_t rr, int32_t& vc, int32_t& va) {
+      const bool ok = rr <= la;
+      vc = s == 0 ? pack2(-rr, -rr) : (ok ? cr[rr - 1] : 0);
+      va = pack2(rr <= X.la ? AX[rr - 1] : 0x200, has_y && rr <= Y.la ? AY[rr - 1] : 0x200);
+    };
+    int32_t nxt_c, nxt_a;
+    chunk_in(1 + lane, nxt_c, nxt_a);
+    for (int32_t ch = 0; ch < n_chunks; ++ch) {
+      int32_t cc = nxt_c, ca = nxt_a;
+      chunk_in(64 * (ch + 1) + 1 + lane, nxt_c, nxt_a);
+      const int32_t rm1_base = 64 * ch - lane;
+      uint32_t acc0 = 0, acc1 = 0;  // steps 0-3 and 4-7 of the current group, both pairs
+#pragma unroll
+      for (int32_t u = 0; u < 64; ++u) {
+        const int32_t left = shr1(h, cc);
+        ach = shr1(ach, ca);
+        cc = shl1(cc);
+        ca = shl1(ca);
+        // per half: 1 where the characters differ, 0 where they match (asm keeps
+        // it one v_pk_min_u16: the compiler would otherwise split it into
+        // two 16-bit compares and selects)
+        int32_t ne;
+        asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(ne) : "v"(ach ^ bc));
+        const s16x2 dmatch = as_s(diag) + as_s(as_i(one)) - as_s(ne);  // H[r-1][c-1] + (a == b)
+        const s16x2 hn = __builtin_elementwise_max(dmatch,
+                                                   __builtin_elementwise_max(as_s(h), as_s(left)) - as_s(as_i(one)));
+        const bool act = static_cast<uint32_t>(rm1_base + u) < static_cast<uint32_t>(la);
+        const s16x2 hn1 = hn + as_s(as_i(one));
+        const uint32_t dh1 = static_cast<uint32_t>(as_i(hn1 - as_s(left)));  // 0..3 per half
+        const uint32_t dv1 = static_cast<uint32_t>(as_i(hn1 - as_s(h)));
+        const uint32_t code = act ? (dh1 | (dv1 << 2)) : 0u;
+        if ((u & 4) == 0) acc0 |= code << ((u & 3) * 4);
+        else acc1 |= code << ((u & 3) * 4);
+        diag = act ? left : diag;
+        h = act ? as_i(hn) : h;
+        if ((u & 7) == 7) {
+          const int32_t g = ch * 8 + (u >> 3);
+          if (okx && g < gx) outx[static_cast<uint64_t>(g) * 64] = __builtin_amdgcn_perm(acc1, acc0, 0x05040100u);
+          if (oky && g < gy) outy[static_cast<uint64_t>(g) * 64] = __builtin_amdgcn_perm(acc1, acc0, 0x07060302u);
+          acc0 = 0;
+          acc1 = 0;
+        }
+        cout = shr1(cout, ror1(h));
+      }
+      if (!last) {
+        const int32_t row = 64 * ch + 1 - lane;
+        if (row >= 1 && row <= la) cr[row - 1] = cout;
+      }
+    }
+    __threadfence_block();
+  }
+}
+
 struct DevEnv {
   const uint32_t* nibs;
   const uint8_t* A;
@@ -160,13 +264,17 @@ __global__ __launch_bounds__(64) void misscore_traceback_kernel(const MsPair* __
 
 }  // namespace
 
-hipError_t launch_misscore(const MsPair* pairs, int n_pairs, const uint8_t* seqs, uint32_t* nib, int32_t* carry,
-                           MsState* stack, int32_t cutoff, MsResult* out, hipStream_t stream,
-                           hipEvent_t ev_fill_start, hipEvent_t ev_fill_end) {
+hipError_t launch_misscore(const MsPair* pairs, int n_pairs, const MsDuo* duos, int n_duos, const int32_t* solo,
+                           int n_solo, const uint8_t* seqs, uint32_t* nib, int32_t* carry, MsState* stack,
+                           int32_t cutoff, MsResult* out, hipStream_t stream, hipEvent_t ev_fill_start,
+                           hipEvent_t ev_fill_end) {
   if (n_pairs <= 0) return hipSuccess;
   if (ev_fill_start) (void)hipEventRecord(ev_fill_start, stream);
-  misscore_fill_kernel<<<(n_pairs + 3) / 4, 256, 0, stream>>>(pairs, n_pairs, seqs, nib, carry);
+  if (n_duos > 0) misscore_fill2_kernel<<<(n_duos + 3) / 4, 256, 0, stream>>>(pairs, duos, n_duos, seqs, nib, carry);
   hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (n_solo > 0) misscore_fill_kernel<<<(n_solo + 3) / 4, 256, 0, stream>>>(pairs, solo, n_solo, seqs, nib, carry);
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev_fill_end) (void)hipEventRecord(ev_fill_end, stream);
   misscore_traceback_kernel<<<(n_pairs + 63) / 64, 64, 0, stream>>>(pairs, n_pairs, seqs, nib, stack, cutoff, out);

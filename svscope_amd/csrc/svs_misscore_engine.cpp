@@ -5,13 +5,16 @@
 //
 // Pairs are sorted by DP size (largest first) and packed into launches that
 // fit the context's device budget.  A launch uploads the sequences its pairs
-// use once, runs misscore_fill_kernel (one wave per pair, 4-bit score
-// differences to HBM) and misscore_traceback_kernel (one lane per pair,
-// pairwise2's DFS), and downloads one MsResult per pair.
+// use once, runs the fill (misscore_fill2_kernel: two neighbouring pairs per
+// wave in packed int16; misscore_fill_kernel: one pair per wave in int32 for
+// pairs over kMsPackedMaxLen), writing 4-bit score differences to HBM, then
+// misscore_traceback_kernel (one lane per pair, pairwise2's DFS), and
+// downloads one MsResult per pair.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -100,9 +103,12 @@ void run_misscore(svs_context* ctx, int32_t n_pairs, const int32_t* pair_a, cons
     }
     const int32_t n = static_cast<int32_t>(j - i);
     std::vector<MsPair> pairs(n);
+    std::vector<MsDuo> duos;
+    std::vector<int32_t> solo;
     std::vector<uint8_t> seqbuf(seq_total, 0);
     for (const auto& kv : seq_at) std::memcpy(seqbuf.data() + kv.second, seq_bytes + seq_byte_start[kv.first], seq_len(kv.first));
     uint64_t nib_w = 0, carry_w = 0, stack_e = 0;
+    auto carry_entries = [](int32_t la) { return (static_cast<uint64_t>(la) + 63) / 64 * 64; };
     for (int32_t k = 0; k < n; ++k) {
       const int32_t p = order[i + k];
       MsPair& P = pairs[k];
@@ -117,20 +123,51 @@ void run_misscore(svs_context* ctx, int32_t n_pairs, const int32_t* pair_a, cons
       P.out_idx = k;
       P.pad = 0;
       nib_w += ms_nib_words(P.la, P.lb);
-      carry_w += (static_cast<uint64_t>(P.la) + 63) / 64 * 64;
       stack_e += P.stack_cap;
       stats.dp_cells += static_cast<uint64_t>(P.la) * P.lb;
     }
+    // Fill work: neighbours in the size order share a wave of the packed
+    // int16 kernel; pairs longer than it takes (or SVS_MS_FILL=32) get the
+    // int32 kernel.
+    const char* fe = std::getenv("SVS_MS_FILL");
+    const bool packed = !(fe && std::atoi(fe) == 32);
+    int32_t pend = -1;  // a packable pair waiting for a partner
+    for (int32_t k = 0; k < n; ++k) {
+      const MsPair& P = pairs[k];
+      if (!packed || P.la > kMsPackedMaxLen || P.lb > kMsPackedMaxLen) {
+        pairs[k].carry_off = static_cast<uint32_t>(carry_w);
+        carry_w += carry_entries(P.la);
+        solo.push_back(k);
+      } else if (pend < 0) {
+        pend = k;
+      } else {
+        duos.push_back(MsDuo{pend, k, static_cast<uint32_t>(carry_w), 0});
+        carry_w += carry_entries(std::max(pairs[pend].la, P.la));
+        pend = -1;
+      }
+    }
+    if (pend >= 0) {
+      duos.push_back(MsDuo{pend, -1, static_cast<uint32_t>(carry_w), 0});
+      carry_w += carry_entries(pairs[pend].la);
+    }
     if (carry_w > 0xFFFFFFFFull) throw SvsError(SVS_E_UNSUPPORTED, "carry buffer over 2^32 entries");
-    ctx->d_ms_pairs.ensure(n * sizeof(MsPair));
+    const size_t off_duo = align256(n * sizeof(MsPair)), off_solo = off_duo + align256(duos.size() * sizeof(MsDuo));
+    std::vector<uint8_t> desc(off_solo + solo.size() * sizeof(int32_t) + 4);
+    std::memcpy(desc.data(), pairs.data(), n * sizeof(MsPair));
+    if (!duos.empty()) std::memcpy(desc.data() + off_duo, duos.data(), duos.size() * sizeof(MsDuo));
+    if (!solo.empty()) std::memcpy(desc.data() + off_solo, solo.data(), solo.size() * sizeof(int32_t));
+    ctx->d_ms_pairs.ensure(desc.size());
     ctx->d_ms_seq.ensure(std::max<uint64_t>(seq_total, 64));
     ctx->d_ms_nib.ensure(nib_w * 4);
     ctx->d_ms_carry.ensure(carry_w * 4);
     ctx->d_ms_stack.ensure(stack_e * sizeof(MsState));
     ctx->d_ms_out.ensure(n * sizeof(MsResult));
-    SVS_HIP(hipMemcpyAsync(ctx->d_ms_pairs.ptr, pairs.data(), n * sizeof(MsPair), hipMemcpyHostToDevice, ctx->stream));
+    SVS_HIP(hipMemcpyAsync(ctx->d_ms_pairs.ptr, desc.data(), desc.size(), hipMemcpyHostToDevice, ctx->stream));
     SVS_HIP(hipMemcpyAsync(ctx->d_ms_seq.ptr, seqbuf.data(), seq_total, hipMemcpyHostToDevice, ctx->stream));
-    SVS_HIP(launch_misscore(ctx->d_ms_pairs.as<MsPair>(), n, ctx->d_ms_seq.as<uint8_t>(), ctx->d_ms_nib.as<uint32_t>(),
+    uint8_t* dd = ctx->d_ms_pairs.as<uint8_t>();
+    SVS_HIP(launch_misscore(ctx->d_ms_pairs.as<MsPair>(), n, reinterpret_cast<const MsDuo*>(dd + off_duo),
+                            static_cast<int>(duos.size()), reinterpret_cast<const int32_t*>(dd + off_solo),
+                            static_cast<int>(solo.size()), ctx->d_ms_seq.as<uint8_t>(), ctx->d_ms_nib.as<uint32_t>(),
                             ctx->d_ms_carry.as<int32_t>(), ctx->d_ms_stack.as<MsState>(), cutoff,
                             ctx->d_ms_out.as<MsResult>(), ctx->stream, ev[0], ev[1]));
     SVS_HIP(hipEventRecord(ev[2], ctx->stream));

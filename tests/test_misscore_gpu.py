@@ -98,3 +98,21 @@ def test_calculate_misscore_and_pipe(gpu_ctx, tmp_path):
     assert list(res["MisScore"]) == exp
     one = [r for r in rows if r[9] == "NormalOutput|EMOutput"][0]
     assert PC.CalculateMisscore({"somSeqList": one[3], "germSeqList": one[6]}) == exp[0]
+
+
+def test_int32_fill_and_long_pairs(gpu_ctx, monkeypatch):
+    """The int32 fill kernel (forced with SVS_MS_FILL=32, and taken by pairs
+    longer than the packed kernel's 30000) gives the same counts; an odd
+    number of packable pairs leaves one duo with a single pair."""
+    PC = _pc()
+    rng = random.Random(25)
+    pairs = [random_pair(rng, max_len=200) for _ in range(501)]
+    exp = [P2.AligmentScore_c(a, b) for a, b in pairs]
+    assert PC.aligment_score_batch(pairs, context=gpu_ctx) == exp
+    monkeypatch.setenv("SVS_MS_FILL", "32")
+    assert PC.aligment_score_batch(pairs, context=gpu_ctx) == exp
+    monkeypatch.delenv("SVS_MS_FILL")
+    base = "".join(rng.choice("ACGT") for _ in range(150))
+    long_pairs = [("".join(rng.choice("ACGT") for _ in range(31000)), base), (base, mutate(rng, base, 0.1)),
+                  ("ACGT" * 7600, "ACGA" * 50)]
+    assert PC.aligment_score_batch(long_pairs, context=gpu_ctx) == [P2.AligmentScore_c(a, b) for a, b in long_pairs]
