@@ -116,3 +116,23 @@ def test_int32_fill_and_long_pairs(gpu_ctx, monkeypatch):
     long_pairs = [("".join(rng.choice("ACGT") for _ in range(31000)), base), (base, mutate(rng, base, 0.1)),
                   ("ACGT" * 7600, "ACGA" * 50)]
     assert PC.aligment_score_batch(long_pairs, context=gpu_ctx) == [P2.AligmentScore_c(a, b) for a, b in long_pairs]
+
+
+def test_misscore_on_local_graph_output(gpu_ctx, tmp_path):
+    """AlnFeature's MisScore over a Raw.bed that this build's localGraph wrote
+    (synthetic windows with somatic insertions): MisScorePipe on the GPU equals
+    the oracle's CalculateMisscore over the same records."""
+    PC = _pc()
+    from svscope_amd import synth
+    from svscope_amd.local_graph import record_line
+    from svscope_amd.som_td_detector import TDscope_npz_batch
+    rows = [synth.make_window(w, 16, 700) for w in range(24)]
+    recs = TDscope_npz_batch(rows, context=gpu_ctx)
+    f = tmp_path / "T.vs.N.TandemRepeat.Raw.bed"
+    f.write_text("\n".join(record_line(r) for r in recs) + "\n")
+    em = [r for r in recs if str(r[-1]) == "NormalOutput|EMOutput"]
+    assert em, "no EMOutput window in the sample"
+    res = PC.MisScorePipe(str(f), context=gpu_ctx)
+    exp = [P2.CalculateMisscore({"somSeqList": str(r[3]), "germSeqList": str(r[6])}, score_fn=P2.AligmentScore_c)
+           for r in em]
+    assert list(res["MisScore"]) == exp
