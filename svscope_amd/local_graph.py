@@ -120,14 +120,18 @@ def localGraph_npz(args):
         import torch
         import torch.distributed as dist
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        os.environ.setdefault("SVS_DEVICE", str(local))
+        # RCCL between GPUs; gloo only for CPU rehearsals of the plumbing (the
+        # windows themselves still need the HIP engine)
+        gpu = torch.cuda.is_available()
+        if gpu:
+            torch.cuda.set_device(local)
+            os.environ.setdefault("SVS_DEVICE", str(local))
         if not dist.is_initialized():
-            dist.init_process_group("nccl")
+            dist.init_process_group("nccl" if gpu else "gloo")
         owner = shard_lpt(rows, world)
         mine = [r for r, o in zip(rows, owner) if o == rank]
         lines = [record_line(x) for x in run_windows(mine, args.batch)]
-        lines = gather_lines(lines, torch.device("cuda", local))
+        lines = gather_lines(lines, torch.device("cuda", local) if gpu else torch.device("cpu"))
     else:
         lines = [record_line(x) for x in run_windows(rows, args.batch)]
     if rank == 0:
