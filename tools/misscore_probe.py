@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-sample", type=int, default=16)
     ap.add_argument("--check", type=int, default=64, help="pairs checked against the oracle")
+    ap.add_argument("--warmup", type=int, default=1)
     a = ap.parse_args()
     rng = random.Random(7)
     pairs = []
@@ -45,7 +46,8 @@ def main():
     from svscope_amd import _abi
     from svscope_amd.pairwise_compare import aligment_score_batch
     ctx = _abi.default_context()
-    aligment_score_batch(pairs[:64], context=ctx)  # warm-up
+    if a.warmup:
+        aligment_score_batch(pairs[:64], context=ctx)
     best = None
     for _ in range(a.reps):
         st = []
