@@ -62,3 +62,22 @@ def test_local_graph_npz_end_to_end(tmp_path):
     # --Continue skips everything already written
     main(["-t", "T1", "-n", "N1", "-s", str(tmp_path), "-C"])
     assert open(tmp_path / "T1.vs.N1.TandemRepeat.Raw.bed").read().splitlines() == exp
+
+
+def _oracle_record(r):
+    return decision_oracle.record_line(decision_oracle.tdscope_npz(r[4], r[0], np.asarray(r[1]), r[2], r[3]))
+
+
+def test_config3_windows_match_oracle():
+    """configs[2] at full size: two 64-read x 3 kb windows (one somatic
+    insertion, one deletion) through the whole GPU pipeline (MSA POA with exact
+    pruning, features, EM, consensus POA) against the CPU oracle, record for
+    record (the oracle runs in two processes, about 25 s each)."""
+    import multiprocessing as mp
+    from svscope_amd import synth
+    from svscope_amd.som_td_detector import TDscope_npz_batch
+    rows = [synth.make_window(w, 64, 3000) for w in (0, 1)]
+    got = [decision_oracle.record_line(g) for g in TDscope_npz_batch(rows)]
+    with mp.get_context("fork").Pool(2) as pool:
+        exp = pool.map(_oracle_record, rows)
+    assert got == exp
