@@ -63,9 +63,19 @@ def cpu_baseline(rows, cores):
     with mp.get_context("fork").Pool(cores) as pool:
         pool.map(_oracle_window, rows, chunksize=1)
     wall = time.time() - t
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": len(rows) / wall, "unit": "windows/s", "cores": cores, "kind": "port",
             "sample": f"{len(rows)} config-3 windows (64 reads x 3 kb), one per process; CPU oracle "
-                      f"(C++ spoa-NW-convex restatement, numpy EM, literal Decision); wall {wall:.1f}s"}
+                      f"(C++ spoa-NW-convex restatement standing in for pyspoa, numpy EM, literal Decision); "
+                      f"wall {wall:.1f}s",
+            "cpu_model": model, "nproc": os.cpu_count()}
 
 
 def pmc_traffic_per_cell():
