@@ -95,7 +95,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("SVS_BENCH_BATCH", "2048")))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("SVS_BENCH_BATCH", "4096")))
     ap.add_argument("--cpu-sample", type=int, default=-1, help="windows for the CPU baseline (-1 auto, 0 off)")
     ap.add_argument("--gen-procs", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cstring>
 #include <future>
@@ -79,6 +80,19 @@ svs_decision_result* run_decision(svs_context* ctx, int32_t n, const svs_decisio
   std::vector<int32_t> em_ready;
   std::unique_ptr<EmBatch> em;
   std::vector<ConsRef> cons_ref;  // consensus task id - n -> cluster
+  // Pruning prior of a window's consensus tasks: their first alignment (read
+  // against a one-read graph) has no score rate of its own yet, so it starts
+  // from the window's last MSA rate less SVS_POA_CONS_PRIOR (score per read
+  // base, default 1.5): two reads differ about twice as much as a read and
+  // the reference.  Exact for any value: a bound above the optimum is retried
+  // unpruned.  A negative value turns the prior off (the first alignment runs
+  // unpruned).
+  std::vector<double> msa_rate(static_cast<size_t>(n), 0.0);
+  std::vector<uint8_t> msa_has_rate(static_cast<size_t>(n), 0);
+  const double cons_prior = [] {
+    const char* e = std::getenv("SVS_POA_CONS_PRIOR");
+    return e ? std::atof(e) : 1.5;
+  }();
   svs_em_config ecfg = cfg.em;
   ecfg.want_params = 0;
 
@@ -150,6 +164,10 @@ svs_decision_result* run_decision(svs_context* ctx, int32_t n, const svs_decisio
         t.genmsa = false;
         t.tag = static_cast<uint32_t>(cons_ref.size());
         t.seqs = std::move(p.reads);
+        if (cons_prior >= 0.0 && msa_has_rate[w]) {
+          t.rate = msa_rate[w] - cons_prior;
+          t.have_rate = true;
+        }
         sched.add(std::move(t));
         cons_ref.push_back(ConsRef{w, c});
         st.consensus_tasks += 1;
@@ -165,6 +183,8 @@ svs_decision_result* run_decision(svs_context* ctx, int32_t n, const svs_decisio
       PoaTask& t = sched.task(id);
       if (t.genmsa) {
         msa_ids.push_back(id);
+        msa_rate[t.tag] = t.rate;
+        msa_has_rate[t.tag] = t.have_rate ? 1 : 0;
       } else {
         const ConsRef& cr = cons_ref[t.tag];
         auto& out = res->w[cr.window];
