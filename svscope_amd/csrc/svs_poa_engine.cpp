@@ -146,11 +146,20 @@ bool strip_pool_forced_global() {
 // alignment of a task, for a retry, after two retries of one task, for graphs
 // too long for the 16-bit path lengths of the row records, and for score
 // parameters the kernel's upper bound does not cover (SVS_POA_PRUNE=0: off).
-int32_t prune_bound(const PoaTask& t, const PoaScore& P, uint32_t n_rows, uint32_t len) {
-  const char* pe = std::getenv("SVS_POA_PRUNE");
-  const bool on = !(pe && std::string(pe) == "0");
-  const char* se = std::getenv("SVS_POA_PRUNE_SLACK");
-  const double slack = se ? std::atof(se) : 0.05;
+struct PruneEnv {
+  bool on = true;
+  double slack = 0.05;
+  PruneEnv() {  // read once per launch, not once per job
+    const char* pe = std::getenv("SVS_POA_PRUNE");
+    on = !(pe && std::string(pe) == "0");
+    const char* se = std::getenv("SVS_POA_PRUNE_SLACK");
+    if (se) slack = std::atof(se);
+  }
+};
+
+int32_t prune_bound(const PoaTask& t, const PoaScore& P, uint32_t n_rows, uint32_t len, const PruneEnv& pv) {
+  const bool on = pv.on;
+  const double slack = pv.slack;
   const int32_t cg = std::max(std::max(P.g, P.e), std::max(P.q, P.c));
   if (!on || !t.have_rate || t.retry || t.n_retries >= 2 || n_rows > 0xFFFFu || len > (1u << 20)) return kNoPrune;
   if (cg > 0 || P.m < P.n || P.m < 0) return kNoPrune;
@@ -159,12 +168,19 @@ int32_t prune_bound(const PoaTask& t, const PoaScore& P, uint32_t n_rows, uint32
   return static_cast<int32_t>(lb);
 }
 
-uint64_t job_bytes(const RowTables& tt, uint64_t L) {
+// Kernel selection flags read from the environment once per call site
+// (not once per job: getenv scans the whole environment).
+struct KernelEnv {
+  bool strip = use_strip_kernel();
+  bool global_pool = strip_pool_forced_global();
+};
+
+uint64_t job_bytes(const RowTables& tt, uint64_t L, const KernelEnv& ke) {
   const uint64_t ls = round_up(L + 1, 64), V = tt.pstart.size() - 1;
-  if (use_strip_kernel()) {
+  if (ke.strip) {
     // traceback codes + two strip-boundary carry buffers (+ a global pool when
     // the graph needs more slots than the LDS pool holds)
-    const uint64_t pool = (tt.n_slots > kStripMaxLdsSlots || strip_pool_forced_global())
+    const uint64_t pool = (tt.n_slots > kStripMaxLdsSlots || ke.global_pool)
                               ? 8ull * round_up(static_cast<uint64_t>(tt.n_slots) * 97, 64) * 4 : 0;
     return V * ls * 2 + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
   }
@@ -207,6 +223,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   // the per-wave LDS pools of one workgroup must fit the CU's LDS
   while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * kStripSlotBytes > kStripLdsBytes) wpj /= 2;
   if (std::getenv("SVS_POA_DEBUG")) std::fprintf(stderr, "[svs] strip launch: %zu jobs, wpj %d, slots %u\n", nj, wpj, max_slots);
+  const PruneEnv penv;
   for (size_t k = 0; k < nj; ++k) {
     const auto& tt = tasks[la.ids[k]].rows;
     const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];
@@ -224,7 +241,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     J.bnd_off = n_bnd;
     J.pool_off = n_pool;
     J.aln_off = n_aln;
-    J.lb = prune_bound(tasks[la.ids[k]], score, J.n_rows, J.len);
+    J.lb = prune_bound(tasks[la.ids[k]], score, J.n_rows, J.len, penv);
     if (J.n_slots > 31) J.lb = kNoPrune;  // the kernel tracks slot liveness in 31 bits
     any_prune = any_prune || J.lb != kNoPrune;
     n_rows += J.n_rows;
@@ -637,7 +654,8 @@ struct PoaScheduler::Impl {
         if (ids.empty()) continue;  // refill and try again
       }
       uint64_t total = 0;
-      for (uint32_t id : ids) total += job_bytes(tasks[id].rows, tasks[id].seqs[tasks[id].next].size());
+      const KernelEnv ke;
+      for (uint32_t id : ids) total += job_bytes(tasks[id].rows, tasks[id].seqs[tasks[id].next].size(), ke);
       if (total <= budget) {
         g.la.ids = std::move(ids);
         g.la.arena = g.arena;
@@ -654,7 +672,7 @@ struct PoaScheduler::Impl {
         size_t last = first;
         uint64_t bytes = 0;
         while (last < ids.size()) {
-          const uint64_t b = job_bytes(tasks[ids[last]].rows, tasks[ids[last]].seqs[tasks[ids[last]].next].size());
+          const uint64_t b = job_bytes(tasks[ids[last]].rows, tasks[ids[last]].seqs[tasks[ids[last]].next].size(), ke);
           if (last > first && bytes + b > budget) break;
           bytes += b;
           ++last;
