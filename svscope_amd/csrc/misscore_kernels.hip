@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #define SVS_MS_FN __device__ __forceinline__
 #include "misscore_device.hpp"
@@ -262,6 +263,109 @@ __global__ __launch_bounds__(64) void misscore_traceback_kernel(const MsPair* __
   out[P.out_idx] = ms_first_alignment(env, P.la, P.lb, cutoff, max_steps);
 }
 
+// The same DFS with one wave per pair.  Every value the DFS branches on is
+// wave-uniform; the wave's lanes only serve as a register cache.  Nibbles come
+// from a 32-column x 32-step tile (two words per lane: lane l holds column
+// tc - (l & 31), words g0 - (l >> 5) and g0 - 2 - (l >> 5) of that column,
+// g0 the word holding row tr), so a path pays one HBM round trip per ~16-32
+// steps instead of two or three dependent loads per step.  Characters come
+// from 64-wide register windows the same way.  Stack entries are written and
+// read back by lane 0 only (a thread sees its own stores) and broadcast.
+struct WaveEnv {
+  const uint32_t* nibs;
+  const uint8_t* A;
+  const uint8_t* B;
+  MsState* stack;
+  uint32_t cap;
+  uint32_t top;
+  int32_t n_groups;
+  int32_t max_depth;
+  int32_t lane;
+  int32_t tr = -1000000, tc = -1000000;  // tile anchor (row, column)
+  uint32_t tw0 = 0, tw1 = 0;
+  int32_t ta = -1000000, tb = -1000000;  // character windows: lane l holds A[ta-1-l], B[tb-1-l]
+  int32_t wa = 0, wb = 0;
+  __device__ __forceinline__ uint32_t word_at(int32_t c, int32_t g) const {
+    const int32_t k = (c - 1) & 63;
+    return nibs[(static_cast<uint64_t>((c - 1) >> 6) * n_groups + g) * 64 + k];
+  }
+  __device__ __forceinline__ void load_tile(int32_t r, int32_t c) {
+    tr = r;
+    tc = c;
+    const int32_t cc = c - (lane & 31);
+    const int32_t g0 = (r - 1 + ((cc - 1) & 63)) >> 3;
+    const int32_t ga = g0 - (lane >> 5), gb = ga - 2;
+    tw0 = (cc >= 1 && ga >= 0) ? word_at(cc, ga) : 0u;
+    tw1 = (cc >= 1 && gb >= 0) ? word_at(cc, gb) : 0u;
+  }
+  __device__ __forceinline__ uint32_t nib(int32_t r, int32_t c) {
+    const int32_t k = (c - 1) & 63, t1 = r - 1 + k;
+    int32_t d = tc - c, dg = ((tr - 1 + k) >> 3) - (t1 >> 3);
+    if (static_cast<uint32_t>(d) >= 32u || static_cast<uint32_t>(dg) >= 4u) {
+      load_tile(r, c);
+      d = 0;
+      dg = 0;
+    }
+    const int32_t l = d + 32 * (dg & 1);
+    const uint32_t w = (dg >> 1) ? __builtin_amdgcn_readlane(tw1, l) : __builtin_amdgcn_readlane(tw0, l);
+    return (w >> ((t1 & 7) * 4)) & 15u;
+  }
+  __device__ __forceinline__ uint8_t a(int32_t i) {
+    int32_t d = ta - 1 - i;
+    if (static_cast<uint32_t>(d) >= 64u) {
+      ta = i + 1;
+      wa = i - lane >= 0 ? A[i - lane] : 0;
+      d = 0;
+    }
+    return static_cast<uint8_t>(__builtin_amdgcn_readlane(wa, d));
+  }
+  __device__ __forceinline__ uint8_t b(int32_t j) {
+    int32_t d = tb - 1 - j;
+    if (static_cast<uint32_t>(d) >= 64u) {
+      tb = j + 1;
+      wb = j - lane >= 0 ? B[j - lane] : 0;
+      d = 0;
+    }
+    return static_cast<uint8_t>(__builtin_amdgcn_readlane(wb, d));
+  }
+  __device__ __forceinline__ bool push(const MsState& s) {
+    if (top >= cap) return false;
+    if (lane == 0) stack[top] = s;
+    ++top;
+    return true;
+  }
+  __device__ __forceinline__ void pop(MsState& s) {
+    --top;
+    MsState v{};
+    if (lane == 0) v = stack[top];
+    s.row = __builtin_amdgcn_readfirstlane(v.row);
+    s.col = __builtin_amdgcn_readfirstlane(v.col);
+    s.trace = __builtin_amdgcn_readfirstlane(v.trace);
+    s.col_gap = __builtin_amdgcn_readfirstlane(v.col_gap);
+    s.nc = __builtin_amdgcn_readfirstlane(v.nc);
+    s.nm = __builtin_amdgcn_readfirstlane(v.nm);
+    s.front = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int32_t>(v.front >> 32)))) << 32) |
+              static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int32_t>(v.front)));
+    s.recent = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int32_t>(v.recent >> 32)))) << 32) |
+               static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int32_t>(v.recent)));
+  }
+};
+
+__global__ __launch_bounds__(64) void misscore_traceback_wave_kernel(const MsPair* __restrict__ pairs, int n_pairs,
+                                                                     const uint8_t* __restrict__ seqs,
+                                                                     const uint32_t* __restrict__ nib,
+                                                                     MsState* __restrict__ stack, int32_t cutoff,
+                                                                     MsResult* __restrict__ out) {
+  const int pid = blockIdx.x;
+  if (pid >= n_pairs) return;
+  const MsPair P = pairs[pid];
+  WaveEnv env{nib + P.nib_off, seqs + P.a_off, seqs + P.b_off, stack + P.stack_off, P.stack_cap, 0,
+              ms_chunks(P.la) * 8, 0, static_cast<int32_t>(threadIdx.x)};
+  const int64_t max_steps = 8ll * (P.la + P.lb) + 4096;
+  const MsResult r = ms_first_alignment(env, P.la, P.lb, cutoff, max_steps);
+  if (threadIdx.x == 0) out[P.out_idx] = r;
+}
+
 }  // namespace
 
 hipError_t launch_misscore(const MsPair* pairs, int n_pairs, const MsDuo* duos, int n_duos, const int32_t* solo,
@@ -277,7 +381,12 @@ hipError_t launch_misscore(const MsPair* pairs, int n_pairs, const MsDuo* duos, 
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev_fill_end) (void)hipEventRecord(ev_fill_end, stream);
-  misscore_traceback_kernel<<<(n_pairs + 63) / 64, 64, 0, stream>>>(pairs, n_pairs, seqs, nib, stack, cutoff, out);
+  // SVS_MS_TB=lane: one lane per pair (the first version; kept as a tested variant)
+  const char* tbe = std::getenv("SVS_MS_TB");
+  if (tbe && tbe[0] == 'l')
+    misscore_traceback_kernel<<<(n_pairs + 63) / 64, 64, 0, stream>>>(pairs, n_pairs, seqs, nib, stack, cutoff, out);
+  else
+    misscore_traceback_wave_kernel<<<n_pairs, 64, 0, stream>>>(pairs, n_pairs, seqs, nib, stack, cutoff, out);
   return hipGetLastError();
 }
 

@@ -136,3 +136,20 @@ def test_misscore_on_local_graph_output(gpu_ctx, tmp_path):
     exp = [P2.CalculateMisscore({"somSeqList": str(r[3]), "germSeqList": str(r[6])}, score_fn=P2.AligmentScore_c)
            for r in em]
     assert list(res["MisScore"]) == exp
+
+
+def test_traceback_variants_agree(gpu_ctx, monkeypatch):
+    """The wave-per-pair tiled traceback (default) and the lane-per-pair one
+    (SVS_MS_TB=lane) give the oracle's counts, cutoffs included."""
+    PC = _pc()
+    rng = random.Random(26)
+    pairs = [random_pair(rng, max_len=120) for _ in range(600)]
+    for _ in range(6):
+        a = "".join(rng.choice("ACGT") for _ in range(3000))
+        pairs.append((a, mutate(rng, a, 0.08, ins=rng.choice([0, 500]))))
+    for cut in (0, 5):
+        exp = [P2.AligmentScore_c(a, b, cut) for a, b in pairs]
+        assert PC.aligment_score_batch(pairs, cutoff=cut, context=gpu_ctx) == exp
+        monkeypatch.setenv("SVS_MS_TB", "lane")
+        assert PC.aligment_score_batch(pairs, cutoff=cut, context=gpu_ctx) == exp
+        monkeypatch.delenv("SVS_MS_TB")
