@@ -153,3 +153,12 @@ def test_traceback_variants_agree(gpu_ctx, monkeypatch):
         monkeypatch.setenv("SVS_MS_TB", "lane")
         assert PC.aligment_score_batch(pairs, cutoff=cut, context=gpu_ctx) == exp
         monkeypatch.delenv("SVS_MS_TB")
+
+
+def test_unsupported_cutoff_fails_loudly(gpu_ctx):
+    """cutoff > 64 is outside the kernel's flag window: an error, never a
+    silently different count (the reference only calls cutoff=0)."""
+    from svscope_amd import _abi
+    PC = _pc()
+    with pytest.raises(_abi.SvsError):
+        PC.AligmentScore("ACGT" * 50, "ACGA" * 50, cutoff=65)
