@@ -81,3 +81,33 @@ def test_config3_windows_match_oracle():
     with mp.get_context("fork").Pool(2) as pool:
         exp = pool.map(_oracle_record, rows)
     assert got == exp
+
+
+def test_config3_batch_invariants():
+    """Size-independent properties at full config-3 size (64 reads x 3 kb):
+    the continuous-batching engine gives the same records whatever the batch
+    composition and order (32 windows at once, again, then reversed in two
+    halves), and every EMOutput record's read ids are window read ids, each
+    in at most one cluster."""
+    from svscope_amd import synth
+    from svscope_amd.som_td_detector import TDscope_npz_batch
+    rows = [synth.make_window(w, 64, 3000) for w in range(100, 132)]
+    first = [decision_oracle.record_line(g) for g in TDscope_npz_batch(rows)]
+    again = [decision_oracle.record_line(g) for g in TDscope_npz_batch(rows)]
+    assert first == again
+    rev = rows[::-1]
+    split = TDscope_npz_batch(rev[:11]) + TDscope_npz_batch(rev[11:])
+    assert [decision_oracle.record_line(g) for g in split][::-1] == first
+    n_em = 0
+    for r, line in zip(rows, first):
+        f = line.split("\t")
+        if not f[-1].endswith("|EMOutput"):
+            continue
+        n_em += 1
+        ids = set(map(str, r[1]))
+        seen = []
+        for field in (f[4], f[7]):
+            for cluster in field.split(";"):
+                seen += [x for x in cluster.split(",") if x]
+        assert set(seen) <= ids and len(seen) == len(set(seen)), line[:200]
+    assert n_em > 0
