@@ -103,6 +103,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    # synthetic windows first: the generator pool forks before this process
+    # touches the GPU
+    B, K, W = args.batch, args.steps, args.warmup
+    per_rank = (W + K) * B
+    ids = list(range(rank * per_rank, (rank + 1) * per_rank))
+    rows = generate(ids, max(1, args.gen_procs))
+    batches = [rows[s * B:(s + 1) * B] for s in range(W + K)]
+
     dist = None
     if world > 1:
         import torch
@@ -110,12 +119,6 @@ def main():
         torch.cuda.set_device(local)
         os.environ["SVS_DEVICE"] = str(local)
         dist.init_process_group("nccl")
-
-    B, K, W = args.batch, args.steps, args.warmup
-    per_rank = (W + K) * B
-    ids = list(range(rank * per_rank, (rank + 1) * per_rank))
-    rows = generate(ids, max(1, args.gen_procs))
-    batches = [rows[s * B:(s + 1) * B] for s in range(W + K)]
 
     from svscope_amd import _abi
     from svscope_amd.som_td_detector import TDscope_npz_batch
