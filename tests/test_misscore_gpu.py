@@ -162,3 +162,23 @@ def test_unsupported_cutoff_fails_loudly(gpu_ctx):
     PC = _pc()
     with pytest.raises(_abi.SvsError):
         PC.AligmentScore("ACGT" * 50, "ACGA" * 50, cutoff=65)
+
+
+def test_misscore_on_config3_local_graph_output(gpu_ctx, tmp_path):
+    """Full size: the consensus pairs of 8 config-3 windows (64 reads x 3 kb)
+    written by this build's localGraph, through MisScorePipe on the GPU,
+    equal the oracle's CalculateMisscore."""
+    PC = _pc()
+    from svscope_amd import synth
+    from svscope_amd.local_graph import record_line
+    from svscope_amd.som_td_detector import TDscope_npz_batch
+    rows = [synth.make_window(w, 64, 3000) for w in range(200, 208)]
+    recs = TDscope_npz_batch(rows, context=gpu_ctx)
+    f = tmp_path / "T.vs.N.TandemRepeat.Raw.bed"
+    f.write_text("\n".join(record_line(r) for r in recs) + "\n")
+    em = [r for r in recs if str(r[-1]) == "NormalOutput|EMOutput"]
+    assert em
+    res = PC.MisScorePipe(str(f), context=gpu_ctx)
+    exp = [P2.CalculateMisscore({"somSeqList": str(r[3]), "germSeqList": str(r[6])}, score_fn=P2.AligmentScore_c)
+           for r in em]
+    assert list(res["MisScore"]) == exp
