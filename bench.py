@@ -1,28 +1,45 @@
 #!/usr/bin/env python3
 """Benchmark of the SVScope localGraph hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--depth D]
 
-One step = one pass of the hot path (window MSA POA -> feature selection ->
-EM over K=1..9 -> per-cluster consensus POA -> 10-field record) over a batch of
-B synthetic config-3 windows (64 reads x 3 kb, BASELINE.json configs[2],
-generator of SURVEY.md §8(d)) per GPU.  For N > 1 the script runs as one
-process per GPU under torch.distributed.run; every rank processes its own
-windows (weak scaling), time = max over ranks.  Rank 0 prints one JSON line.
+Workload: BASELINE.json configs[2] ("config 3"): candidate windows of 64 reads
+x 3 kb, synthetic (SURVEY.md §8(d) generator), run end to end through the
+localGraph per-window path (window MSA POA -> feature selection -> EM over
+K=1..9 -> per-cluster consensus POA -> 10-field record).
+
+One step = one batch of B windows (default 512) submitted to the engine's
+streaming decision session.  K steps = K*B windows (default 20 x 512 = 10,240,
+i.e. config 3's 10,000 windows) are all submitted and completed inside the
+timed region; the session keeps up to D batches in flight (continuous
+batching: batch b+1's window MSAs fill the GPU while batch b finishes), the
+way localGraph_npz streams its windows.  Warmup steps run W batches of a
+separate, reused set of B windows through the same session before timing.
+
+For --gpus N > 1 the script re-launches itself under torch.distributed.run
+(one process per GPU, before anything touches a GPU); each rank processes its
+own K*B windows (weak scaling, no data-path collective: windows are
+independent), time = max over ranks, value = all ranks' windows / that time.
 
 roofline: the dominant kernel is the POA DP (poa_strip_kernel); achieved =
-algorithmic bytes (20 B per DP cell: the int32 H,E,F,O,Q planes of convex NW,
-SURVEY.md §8(d)) x cells per launch / mean launch time, from HIP events on the
-engine's POA stream.  traffic = measured HBM bytes per DP cell from the
-committed rocprofv3 PMC summary (profiles/pmc_poa_traffic.json) x cells per
-launch, else null.
-cpu_baseline: the CPU oracle (C++ spoa restatement + numpy EM + literal
-Decision) on a bounded sample of the same windows, one process per core.
+algorithmic bytes (20 B per evaluated DP cell: the int32 H,E,F,O,Q planes of
+convex NW) per launch / mean launch time, from HIP events on
+the engine's POA stream.  traffic = measured HBM bytes per evaluated cell from
+the committed rocprofv3 PMC summary (profiles/pmc_poa_traffic.json) x cells
+per launch, else null.
+
+cpu_baseline: the CPU oracle (C++ spoa restatement standing in for pyspoa, the
+numpy EM restatement of ReadsCluster.py, the literal Decision) on a bounded
+sample of the same windows, timed before the GPU is touched, in the two modes
+of SURVEY.md §8(d): as shipped (min(6, cores) worker processes,
+SVscope.py:158-161) and all cores of this job's CPU share, BLAS threads 1.
 """
 import argparse
 import json
 import multiprocessing as mp
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +50,7 @@ METRIC = "candidate-windows/sec (64 reads × 3 kb) localGraph, 1/2/4/8 MI355X; %
 HBM_PEAK_GBS = 8000.0
 BYTES_PER_CELL = 20
 N_READS, REF_LEN = 64, 3000
+WARMUP_ID_BASE = 1 << 30  # warmup windows never share a seed with timed ones
 
 
 def _gen(ws):
@@ -41,6 +59,8 @@ def _gen(ws):
 
 
 def generate(ids, procs):
+    if procs <= 1 or len(ids) < 2:
+        return _gen(ids)
     chunks = [ids[i::procs] for i in range(procs)]
     with mp.get_context("fork").Pool(procs) as pool:
         parts = pool.map(_gen, chunks)
@@ -51,18 +71,48 @@ def generate(ids, procs):
     return [by_id[w] for w in ids]
 
 
+def host_cores():
+    """CPUs this job may use: its affinity mask, capped by the box's CPU share
+    (OMP_NUM_THREADS is set to the share on the GPU boxes)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
+
+
+def _baseline_init():
+    from threadpoolctl import threadpool_limits
+    threadpool_limits(1)  # BLAS threads = 1 per worker (SURVEY.md §8(d))
+
+
 def _oracle_window(row):
+    import numpy as np
     from oracle import decision_oracle
-    return decision_oracle.tdscope_npz(row[4], row[0], row[1], row[2], row[3])
+    return decision_oracle.tdscope_npz(row[4], row[0], np.asarray(row[1]), row[2], row[3])
+
+
+def _time_pool(rows, workers):
+    t = time.time()
+    with mp.get_context("fork").Pool(workers, initializer=_baseline_init) as pool:
+        pool.map(_oracle_window, rows, chunksize=1)
+    return time.time() - t
 
 
 def cpu_baseline(rows, cores):
+    """Both §8(d) modes, one window per worker each, before any GPU call."""
     from oracle import spoa_oracle
-    spoa_oracle._load()  # build/load before timing
-    t = time.time()
-    with mp.get_context("fork").Pool(cores) as pool:
-        pool.map(_oracle_window, rows, chunksize=1)
-    wall = time.time() - t
+    spoa_oracle._load()  # build/load the C++ oracle before timing
+    shipped = min(6, cores)
+    modes = {}
+    for name, workers in (("as_shipped", shipped), ("all_cores", cores)):
+        sample = rows[:workers]
+        wall = _time_pool(sample, workers)
+        modes[name] = {"value": round(len(sample) / wall, 5), "workers": workers, "windows": len(sample),
+                       "wall_s": round(wall, 2)}
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -71,16 +121,18 @@ def cpu_baseline(rows, cores):
                 break
     except OSError:
         pass
-    return {"value": len(rows) / wall, "unit": "windows/s", "cores": cores, "kind": "port",
-            "sample": f"{len(rows)} config-3 windows (64 reads x 3 kb), one per process; CPU oracle "
-                      f"(C++ spoa-NW-convex restatement standing in for pyspoa, numpy EM, literal Decision); "
-                      f"wall {wall:.1f}s",
-            "cpu_model": model, "nproc": os.cpu_count()}
+    best = modes["all_cores"]
+    return {"value": best["value"], "unit": "windows/s", "cores": best["workers"], "kind": "port",
+            "sample": (f"one config-3 window (64 reads x 3 kb) per worker process; as shipped "
+                       f"{modes['as_shipped']['workers']} workers (SVscope.py:158-161), all cores "
+                       f"{best['workers']} workers (this job's CPU share); BLAS threads 1; POA is a proxy: "
+                       f"the C++ spoa-NW-convex restatement (pyspoa is not installed), numpy EM, literal Decision"),
+            "modes": modes, "cpu_model": model, "nproc": os.cpu_count()}
 
 
 def pmc_traffic_per_cell():
-    """Measured HBM bytes per DP cell of the POA kernel from the committed
-    rocprofv3 PMC summary (FETCH_SIZE and WRITE_SIZE passes), or None."""
+    """Measured HBM bytes per evaluated DP cell of the POA kernel from the
+    committed rocprofv3 PMC summary (FETCH_SIZE and WRITE_SIZE passes), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_poa_traffic.json")
     if not os.path.exists(path):
         return None
@@ -90,27 +142,88 @@ def pmc_traffic_per_cell():
         return None
 
 
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Runs this script as n ranks under torch.distributed.run (a child process:
+    nothing here has touched the GPU) and returns its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    return subprocess.call(cmd)
+
+
+def diff_stats(a, b):
+    out = {}
+    for k, v in b.items():
+        if isinstance(v, dict):
+            out[k] = diff_stats(a.get(k, {}), v)
+        else:
+            out[k] = v - a.get(k, 0)
+    return out
+
+
+def run_steps(session, batches, depth):
+    """Submits every batch, at most `depth` in flight; returns the records."""
+    from collections import deque
+    tickets, out = deque(), []
+    for b in batches:
+        tickets.append(session.submit(b))
+        if len(tickets) >= depth:
+            out.extend(session.wait(tickets.popleft()))
+    while tickets:
+        out.extend(session.wait(tickets.popleft()))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("SVS_BENCH_BATCH", "4096")))
-    ap.add_argument("--cpu-sample", type=int, default=-1, help="windows for the CPU baseline (-1 auto, 0 off)")
-    ap.add_argument("--gen-procs", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("SVS_BENCH_BATCH", "512")))
+    ap.add_argument("--depth", type=int, default=int(os.environ.get("SVS_BENCH_DEPTH", "4")),
+                    help="batches in flight in the streaming session")
+    ap.add_argument("--cpu-sample", type=int, default=-1, help="CPU baseline: -1 both modes, 0 off")
+    ap.add_argument("--gen-procs", type=int, default=0, help="window generator processes (0: all host cores)")
+    ap.add_argument("--probe-env", default="", help=argparse.SUPPRESS)  # launcher test: record rank env, exit
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.probe_env:
+        with open(os.path.join(args.probe_env, f"rank{rank}.json"), "w") as fh:
+            json.dump({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}, fh)
+        return
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
 
-    # synthetic windows first: the generator pool forks before this process
-    # touches the GPU
-    B, K, W = args.batch, args.steps, args.warmup
-    per_rank = (W + K) * B
-    ids = list(range(rank * per_rank, (rank + 1) * per_rank))
-    rows = generate(ids, max(1, args.gen_procs))
-    batches = [rows[s * B:(s + 1) * B] for s in range(W + K)]
+    # Everything that forks (window generation, the CPU baseline) runs before
+    # this process touches the GPU.
+    B, K, W = max(1, args.batch), max(1, args.steps), max(0, args.warmup)
+    cores = host_cores()
+    gen_procs = args.gen_procs or max(1, cores // max(1, world) if world > 1 else cores)
+    t_gen = time.time()
+    timed_ids = list(range(rank * K * B, (rank + 1) * K * B))
+    rows = generate(timed_ids, gen_procs)
+    warm = generate(list(range(WARMUP_ID_BASE + rank * B, WARMUP_ID_BASE + (rank + 1) * B)), gen_procs) if W else []
+    # bundle rows [sequenceList, ReadIDs, flank_5, flank_3, TDRecord] -> the
+    # TDscope_npz arguments, as localGraph_npz passes them (SVscope.py:212-217)
+    from svscope_amd.local_graph import _window
+    batches = [[_window(r) for r in rows[s * B:(s + 1) * B]] for s in range(K)]
+    warm = [_window(r) for r in warm]
+    gen_s = time.time() - t_gen
+
+    cpu = None
+    if args.cpu_sample != 0 and world == 1 and rank == 0:  # the CPU baseline is an N=1 figure
+        cpu = cpu_baseline(rows, cores)
 
     dist = None
     if world > 1:
@@ -118,60 +231,45 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         os.environ["SVS_DEVICE"] = str(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from svscope_amd import _abi
-    from svscope_amd.som_td_detector import TDscope_npz_batch
-    ctx = _abi.default_context()
+    from svscope_amd.decision_maker import DecisionSession
+    ctx = _abi.default_context(local if world > 1 else None)
+    session = DecisionSession(ctx)
 
-    for s in range(W):
-        TDscope_npz_batch(batches[s], context=ctx)
+    t_warm = time.time()
+    if W:
+        run_steps(session, [warm] * W, args.depth)
+    warm_s = time.time() - t_warm
+    st0 = session.stats()
 
-    stats = []
     if dist is not None:
         import torch
         dist.barrier()
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n_em = 0
-    for s in range(W, W + K):
-        recs = TDscope_npz_batch(batches[s], context=ctx, stats=stats)
-        n_em += sum(1 for r in recs if str(r[-1]).endswith("|EMOutput"))
+    recs = run_steps(session, batches, args.depth)
     if dist is not None:
         dist.barrier()
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    st = diff_stats(st0, session.stats())
+    session.close()
+    n_em = sum(1 for r in recs if str(r[-1]).endswith("|EMOutput"))
+    assert len(recs) == K * B, (len(recs), K * B)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    poa_stats = [st for name, st in stats if name in ("msa_poa", "consensus_poa", "decision_poa")]
-    cells = sum(st["dp_cells"] for st in poa_stats)
-    # cells the kernel evaluated (its exact pruning skips strip rows that cannot
-    # reach the alignment's bound): the roofline is priced on these
-    cells_done = sum(st.get("cells_computed", st["dp_cells"]) for st in poa_stats)
-    retries = sum(st.get("prune_retries", 0) for st in poa_stats)
-    kms = sum(st["kernel_ms"] for st in poa_stats)
-    launches = sum(st["launches"] for st in poa_stats)
-    host_ms = sum(st["host_graph_ms"] for st in poa_stats)
-    wait_ms = sum(st.get("gpu_wait_ms", 0.0) for st in poa_stats)
-    phases = {}
-    for name, st in stats:
-        if name == "phases":
-            for k, v in st.items():
-                phases[k] = round(phases.get(k, 0.0) + v, 3)
+    poa = st["poa"]
+    cells, cells_done = poa["dp_cells"], poa["cells_computed"]
+    kms, launches = poa["kernel_ms"], poa["launches"]
     achieved = cells_done * BYTES_PER_CELL / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     total_windows = B * K * world
 
     if rank == 0:
-        cpu = None
-        n_cpu = args.cpu_sample
-        if n_cpu != 0 and world == 1:  # the CPU baseline is an N=1 figure
-            cores = min(16, os.cpu_count() or 1)
-            if n_cpu < 0:
-                n_cpu = cores
-            cpu = cpu_baseline(batches[W][:n_cpu], min(cores, n_cpu))
         value = total_windows / elapsed
         per_cell = pmc_traffic_per_cell()
         traffic = round(per_cell * cells_done / max(1, launches)) if per_cell is not None else None
@@ -188,9 +286,10 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (SURVEY.md §8(d) generator: ONT-like 8% error, somatic INS/DEL, seeded)",
-            "config": {"workload": "config3: 64 reads x 3 kb candidate windows, localGraph end-to-end "
-                                   "(MSA POA + features + EM K=1..9 + consensus POA)",
-                       "windows_per_step_per_gpu": B, "reads_per_window": N_READS, "ref_len": REF_LEN,
+            "config": {"workload": f"config3: {K * B} candidate windows per GPU (64 reads x 3 kb), {B} per step, "
+                                   f"localGraph end to end (MSA POA + features + EM K=1..9 + consensus POA)",
+                       "windows_per_step_per_gpu": B, "windows_per_gpu": K * B, "reads_per_window": N_READS,
+                       "ref_len": REF_LEN, "batches_in_flight": args.depth,
                        "parallelism": f"window shards x{world}"},
             "roofline": {"bound": "hbm", "kernel": "poa_strip_kernel",
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -199,13 +298,22 @@ def main():
                          "algorithmic_bytes_per_launch": int(cells_done * BYTES_PER_CELL / max(1, launches)),
                          "mean_launch_ms": round(kms / max(1, launches), 4)},
             "cpu_baseline": cpu,
-            "breakdown": {"poa_cells": cells, "poa_cells_computed": cells_done, "prune_retries": retries,
+            "breakdown": {"poa_cells": cells, "poa_cells_computed": cells_done,
+                          "prune_retries": poa["prune_retries"],
                           "poa_kernel_ms": round(kms, 2), "poa_launches": launches,
                           "gcups": round(cells_done / (kms * 1e-3) / 1e9, 3) if kms else None,
                           "gcups_full_matrix_equivalent": round(cells / (kms * 1e-3) / 1e9, 3) if kms else None,
-                          "host_graph_ms": round(host_ms, 1), "host_wait_for_gpu_ms": round(wait_ms, 1),
+                          "host_graph_ms": round(poa["host_graph_ms"], 1),
+                          "host_wait_for_gpu_ms": round(poa["gpu_wait_ms"], 1),
+                          "h2d_bytes": poa["h2d_bytes"], "d2h_bytes": poa["d2h_bytes"],
                           "em_output_windows": n_em,
-                          "phases_s": phases,
+                          "em_kernel_s": round(st["em_kernel_ms"] / 1e3, 3),
+                          "em_wall_s": round(st["em_wall_ms"] / 1e3, 3),
+                          "em_launches": st["em_launches"], "em_windows": st["em_windows"],
+                          "consensus_tasks": st["consensus_tasks"],
+                          "features_s": round(st["features_ms"] / 1e3, 3),
+                          "labelling_s": round(st["labelling_ms"] / 1e3, 3),
+                          "generate_s": round(gen_s, 1), "warmup_s": round(warm_s, 1),
                           "em_dtype": "f64"},
         }
         print(json.dumps(out), flush=True)

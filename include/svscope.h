@@ -187,6 +187,30 @@ typedef struct svs_decision_result svs_decision_result;
 int svs_decision_batch(svs_context* ctx, int32_t n_windows, const svs_decision_window* wins,
                        const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
                        const uint8_t* is_tlabel, const svs_decision_config* cfg, svs_decision_result** out);
+/* Streaming form of svs_decision_batch: a session owns one worker thread and
+ * one POA scheduler for every batch submitted to it, so the MSA jobs of batch
+ * b+1 fill the GPU while batch b's EM and consensus jobs finish (no drain
+ * between batches).  submit() queues a batch and returns a ticket at once; the
+ * input arrays are read by the worker and must stay valid and unchanged until
+ * wait() for that ticket has returned.  wait() blocks until the batch is
+ * complete and returns its result (free with svs_decision_result_free); its
+ * stats are the session's cumulative statistics at the batch's completion.
+ * Batches complete in any order.  While a session is open the context must not
+ * be used for other calls.  close() finishes every submitted batch, joins the
+ * worker and frees the session; it returns the worker's error, if any (after
+ * an error every submit/wait of the session fails with it).
+ * Replaces the Pool.imap_unordered fan-out of localGraph_npz (SVscope.py:220-233)
+ * over TDscope_npz / Decision. */
+typedef struct svs_decision_session svs_decision_session;
+int svs_decision_session_open(svs_context* ctx, const svs_decision_config* cfg, svs_decision_session** out);
+int svs_decision_session_submit(svs_decision_session* s, int32_t n_windows, const svs_decision_window* wins,
+                                const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
+                                const uint8_t* is_tlabel, int64_t* ticket);
+int svs_decision_session_wait(svs_decision_session* s, int64_t ticket, svs_decision_result** out);
+/* cumulative statistics of the session as of its last completed batch */
+int svs_decision_session_stats(svs_decision_session* s, svs_decision_stats* out);
+int svs_decision_session_close(svs_decision_session* s);
+
 int svs_decision_result_window(const svs_decision_result* r, int32_t window, int32_t* status, int32_t* K,
                                int32_t* n_som, int32_t* n_germ);
 /* cluster c of a window: somatic clusters first (c < n_som), then germline;

@@ -145,6 +145,17 @@ def _declare_em(lib):
                                        ctypes.POINTER(DecisionConfig), ctypes.POINTER(ctypes.c_void_p)]
     lib.svs_decision_batch.restype = ctypes.c_int
     PI32 = ctypes.POINTER(ctypes.c_int32)
+    lib.svs_decision_session_open.argtypes = [P, ctypes.POINTER(DecisionConfig), ctypes.POINTER(ctypes.c_void_p)]
+    lib.svs_decision_session_open.restype = ctypes.c_int
+    lib.svs_decision_session_submit.argtypes = [P, I32, ctypes.POINTER(DecisionWindow), P, P, P, P,
+                                                ctypes.POINTER(ctypes.c_int64)]
+    lib.svs_decision_session_submit.restype = ctypes.c_int
+    lib.svs_decision_session_wait.argtypes = [P, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]
+    lib.svs_decision_session_wait.restype = ctypes.c_int
+    lib.svs_decision_session_stats.argtypes = [P, ctypes.POINTER(DecisionStats)]
+    lib.svs_decision_session_stats.restype = ctypes.c_int
+    lib.svs_decision_session_close.argtypes = [P]
+    lib.svs_decision_session_close.restype = ctypes.c_int
     lib.svs_decision_result_window.argtypes = [P, I32, PI32, PI32, PI32, PI32]
     lib.svs_decision_result_window.restype = ctypes.c_int
     lib.svs_decision_result_cluster.argtypes = [P, I32, I32, ctypes.POINTER(PI32), PI32,

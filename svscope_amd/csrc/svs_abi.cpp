@@ -254,20 +254,32 @@ int svs_em_cluster_batch(svs_context* ctx, int32_t n_windows, const svs_em_windo
   return rc;
 }
 
-int svs_decision_batch(svs_context* ctx, int32_t n_windows, const svs_decision_window* wins,
-                       const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
-                       const uint8_t* is_tlabel, const svs_decision_config* cfg, svs_decision_result** out) {
-  if (!ctx || !cfg || !out || n_windows < 0 || (n_windows > 0 && (!wins || !seq_byte_start)))
-    return fail(SVS_E_INVALID, "svs_decision_batch: invalid argument");
-  *out = nullptr;
+static int check_decision_windows(const char* fn, int32_t n_windows, const svs_decision_window* wins,
+                                  const int64_t* seq_byte_start, const char* text, const uint8_t* is_tlabel) {
+  if (n_windows < 0 || (n_windows > 0 && (!wins || !seq_byte_start)))
+    return fail(SVS_E_INVALID, std::string(fn) + ": invalid argument");
   for (int32_t w = 0; w < n_windows; ++w) {
     const svs_decision_window& W = wins[w];
     if (W.n_seqs < 1 || W.n_ids < 0 || W.seq_start < 0 || W.flank5_len < 0 || W.flank3_len < 0 || W.tag_off < 0 ||
         ((W.flank5_len || W.flank3_len) && !text) || (W.n_ids && !is_tlabel))
-      return fail(SVS_E_INVALID, "svs_decision_batch: window " + std::to_string(w) + " is malformed");
+      return fail(SVS_E_INVALID, std::string(fn) + ": window " + std::to_string(w) + " is malformed");
   }
-  if (cfg->readcutoff < 0 || cfg->em.max_c < 1 || cfg->em.n_step < 1)
-    return fail(SVS_E_INVALID, "svs_decision_batch: invalid config");
+  return SVS_OK;
+}
+
+static int check_decision_config(const char* fn, const svs_decision_config* cfg) {
+  if (!cfg || cfg->readcutoff < 0 || cfg->em.max_c < 1 || cfg->em.n_step < 1)
+    return fail(SVS_E_INVALID, std::string(fn) + ": invalid config");
+  return SVS_OK;
+}
+
+int svs_decision_batch(svs_context* ctx, int32_t n_windows, const svs_decision_window* wins,
+                       const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
+                       const uint8_t* is_tlabel, const svs_decision_config* cfg, svs_decision_result** out) {
+  if (!ctx || !cfg || !out) return fail(SVS_E_INVALID, "svs_decision_batch: invalid argument");
+  *out = nullptr;
+  if (int rc = check_decision_windows("svs_decision_batch", n_windows, wins, seq_byte_start, text, is_tlabel)) return rc;
+  if (int rc = check_decision_config("svs_decision_batch", cfg)) return rc;
   svs_decision_result* res = nullptr;
   const int rc = guarded([&] {
     SVS_HIP(hipSetDevice(ctx->device));
@@ -276,6 +288,54 @@ int svs_decision_batch(svs_context* ctx, int32_t n_windows, const svs_decision_w
   });
   if (rc == SVS_OK) *out = res;
   return rc;
+}
+
+int svs_decision_session_open(svs_context* ctx, const svs_decision_config* cfg, svs_decision_session** out) {
+  if (!ctx || !cfg || !out) return fail(SVS_E_INVALID, "svs_decision_session_open: invalid argument");
+  *out = nullptr;
+  if (int rc = check_decision_config("svs_decision_session_open", cfg)) return rc;
+  svs_decision_session* s = nullptr;
+  const int rc = guarded([&] {
+    SVS_HIP(hipSetDevice(ctx->device));
+    s = svs::open_decision_session(ctx, *cfg);
+  });
+  if (rc == SVS_OK) *out = s;
+  return rc;
+}
+
+int svs_decision_session_submit(svs_decision_session* s, int32_t n_windows, const svs_decision_window* wins,
+                                const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
+                                const uint8_t* is_tlabel, int64_t* ticket) {
+  if (!s || !ticket) return fail(SVS_E_INVALID, "svs_decision_session_submit: invalid argument");
+  if (int rc = check_decision_windows("svs_decision_session_submit", n_windows, wins, seq_byte_start, text,
+                                      is_tlabel))
+    return rc;
+  return guarded([&] {
+    *ticket = svs::submit_decision_batch(s, n_windows, wins, seq_byte_start, seq_bytes, text, is_tlabel);
+  });
+}
+
+int svs_decision_session_wait(svs_decision_session* s, int64_t ticket, svs_decision_result** out) {
+  if (!s || !out) return fail(SVS_E_INVALID, "svs_decision_session_wait: invalid argument");
+  *out = nullptr;
+  svs_decision_result* r = nullptr;
+  const int rc = guarded([&] { r = svs::wait_decision_batch(s, ticket); });
+  if (rc == SVS_OK) *out = r;
+  return rc;
+}
+
+int svs_decision_session_stats(svs_decision_session* s, svs_decision_stats* out) {
+  if (!s || !out) return fail(SVS_E_INVALID, "svs_decision_session_stats: invalid argument");
+  svs::session_stats(s, out);
+  return SVS_OK;
+}
+
+int svs_decision_session_close(svs_decision_session* s) {
+  if (!s) return SVS_OK;
+  return guarded([&] {
+    std::exception_ptr e = svs::close_decision_session(s);
+    if (e) std::rethrow_exception(e);
+  });
 }
 
 int svs_decision_result_window(const svs_decision_result* r, int32_t window, int32_t* status, int32_t* K,

@@ -1,5 +1,6 @@
 // Internal declarations shared by the engine translation units.
 #pragma once
+#include <exception>
 #include <functional>
 #include <string>
 #include <vector>
@@ -36,6 +37,7 @@ struct PoaTask {
   std::vector<std::string> seqs;
   bool genmsa = false;  // also produce the MSA rows when the task completes
   uint32_t tag = 0;     // caller's bookkeeping (window / cluster id)
+  uint32_t prio = 0;    // queue order: lower first (a session's batch number), then longest remaining
   size_t next = 0;      // index of the next sequence to align
   PoaGraph graph;
   RowTables rows;       // exported row tables of the current step (capacity reused across steps)
@@ -64,8 +66,10 @@ class PoaScheduler {
   using PollFn = std::function<bool(bool)>;
   PoaScheduler(svs_context* ctx, const svs_poa_config& cfg, svs_poa_stats& st);
   ~PoaScheduler();
+  // Queues a task; ids of finished, released tasks are reused.
   uint32_t add(PoaTask&& t);
   PoaTask& task(uint32_t id);
+  double host_ms() const;  // host graph work so far (fold, export, pack)
   // Runs until no task is queued or active and poll() reports no outside work.
   // done(ids) receives each batch of completed tasks (consensus / msa filled);
   // afterwards the scheduler drops their graphs.
@@ -95,8 +99,17 @@ void run_misscore(svs_context* ctx, int32_t n_pairs, const int32_t* pair_a, cons
                   const int64_t* seq_byte_start, const char* seq_bytes, int32_t cutoff, int32_t* out_len,
                   int32_t* out_match, int32_t* out_status, svs_misscore_stats* st);
 
+
 svs_decision_result* run_decision(svs_context* ctx, int32_t n, const svs_decision_window* wins,
                                   const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
                                   const uint8_t* is_tlabel, const svs_decision_config& cfg);
+
+svs_decision_session* open_decision_session(svs_context* ctx, const svs_decision_config& cfg);
+int64_t submit_decision_batch(svs_decision_session* s, int32_t n, const svs_decision_window* wins,
+                              const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
+                              const uint8_t* is_tlabel);
+svs_decision_result* wait_decision_batch(svs_decision_session* s, int64_t ticket);
+void session_stats(svs_decision_session* s, svs_decision_stats* out);
+std::exception_ptr close_decision_session(svs_decision_session* s);
 
 }  // namespace svs

@@ -584,6 +584,7 @@ struct PoaScheduler::Impl {
   size_t budget;
   double host_ms = 0.0;
   std::vector<uint32_t> graves;  // finished tasks whose storage is not yet released
+  std::vector<uint32_t> free_ids;  // released task slots, reused by add()
   bool queue_dirty = false;      // tasks were queued since the last sort
 
   Impl(svs_context* c, const svs_poa_config& k, svs_poa_stats& s)
@@ -609,7 +610,9 @@ struct PoaScheduler::Impl {
     // longest remaining task first, so the long tasks (germline-cluster
     // consensus) do not form a tail of small launches at the end
     if (queue_dirty) {
+      // (within a session: older batches first, so batches complete in order)
       std::stable_sort(queue.begin(), queue.end(), [this](uint32_t a, uint32_t b) {
+        if (tasks[a].prio != tasks[b].prio) return tasks[a].prio < tasks[b].prio;
         return tasks[a].seqs.size() - tasks[a].next > tasks[b].seqs.size() - tasks[b].next;
       });
       queue_dirty = false;
@@ -703,6 +706,8 @@ struct PoaScheduler::Impl {
       t.rows = RowTables();
       std::vector<std::string>().swap(t.seqs);
     });
+    // a long session reuses the slots of released tasks
+    free_ids.insert(free_ids.end(), graves.begin() + static_cast<std::ptrdiff_t>(base), graves.end());
     graves.resize(base);
     g_trace.host("reap", -1, t0, n);
     return true;
@@ -757,15 +762,24 @@ PoaScheduler::~PoaScheduler() {
 }
 
 uint32_t PoaScheduler::add(PoaTask&& t) {
-  const uint32_t id = static_cast<uint32_t>(impl_->tasks.size());
   t.next = 0;
-  impl_->tasks.push_back(std::move(t));
+  uint32_t id;
+  if (!impl_->free_ids.empty()) {
+    id = impl_->free_ids.back();
+    impl_->free_ids.pop_back();
+    impl_->tasks[id] = std::move(t);
+  } else {
+    id = static_cast<uint32_t>(impl_->tasks.size());
+    impl_->tasks.push_back(std::move(t));
+  }
   impl_->queue.push_back(id);
   impl_->queue_dirty = true;
   return id;
 }
 
 PoaTask& PoaScheduler::task(uint32_t id) { return impl_->tasks[id]; }
+
+double PoaScheduler::host_ms() const { return impl_->host_ms; }
 
 void PoaScheduler::run(const DoneFn& done, const PollFn& poll) { impl_->run(done, poll); }
 

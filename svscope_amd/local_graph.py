@@ -8,7 +8,11 @@ TDscope_npz on each window, write ``<T>.vs.<N>.TandemRepeat.Raw.bed`` (one
 ``sort -k1,1 -k2,2n`` (:236; C-locale byte order, whole-line tie-break).
 
 Differences, all deliberate:
-  * windows run in GPU batches (DecisionBatch) instead of a 6-process Pool;
+  * windows stream through one DecisionSession in GPU batches instead of a
+    6-process Pool; each batch's records are appended and flushed as soon as
+    the batch completes (the reference flushes per record), so --Continue
+    resumes after a crash (per-rank journals ``<out>.part<rank>`` on N > 1,
+    folded into the output by rank 0 on the next --Continue run);
   * ``--Continue`` skips windows whose first three fields are already in the
     output (the reference compares full records against 3-field keys and so
     never skips, SURVEY.md §5);
@@ -26,7 +30,6 @@ import time
 
 import numpy as np
 
-from .som_td_detector import TDscope_npz_batch
 
 log = logging.getLogger("svscope_amd")
 
@@ -72,11 +75,70 @@ def sort_lines(lines):
     return sorted(lines, key=key)
 
 
-def run_windows(rows, batch_size=512, context=None, stats=None):
+def _window(r):
+    """bundle row [sequenceList, ReadIDs, flank_5, flank_3, TDRecord] -> Decision arguments"""
+    return (r[4], list(r[0]), np.asarray(r[1]), r[2], r[3])
+
+
+def iter_batches(rows, batch_size=512, context=None, depth=4):
+    """Yields the records of each batch of ``rows``, in order, streamed through
+    one DecisionSession with up to ``depth`` batches in flight (the engine's
+    scheduler never drains between batches)."""
+    from collections import deque
+    from .decision_maker import DecisionSession
+    if not rows:
+        return
+    with DecisionSession(context) as session:
+        tickets = deque()
+        for k in range(0, len(rows), batch_size):
+            tickets.append(session.submit([_window(r) for r in rows[k:k + batch_size]]))
+            if len(tickets) >= depth:
+                yield session.wait(tickets.popleft())
+        while tickets:
+            yield session.wait(tickets.popleft())
+
+
+def run_windows(rows, batch_size=512, context=None):
     out = []
-    for s in range(0, len(rows), batch_size):
-        out.extend(TDscope_npz_batch(rows[s:s + batch_size], context=context, stats=stats))
+    for recs in iter_batches(rows, batch_size, context):
+        out.extend(recs)
     return out
+
+
+def write_journal(path, mode, rows, batch_size):
+    """Runs the windows and appends each batch's records to ``path`` as soon as
+    the batch completes, flushed (the reference writes and flushes every
+    record as it arrives, SVscope.py:227-233, which is what makes --Continue
+    resume after a crash).  Returns the record lines."""
+    lines = []
+    with open(path, mode) as fh:
+        for recs in iter_batches(rows, batch_size):
+            chunk = [record_line(x) for x in recs]
+            fh.write("".join(line + "\n" for line in chunk))
+            fh.flush()
+            lines.extend(chunk)
+    return lines
+
+
+def part_path(path, rank):
+    return "%s.part%d" % (path, rank)
+
+
+def merge_parts(path):
+    """Folds the per-rank journals of an interrupted multi-GPU run into the
+    output file (rank 0, before any window runs)."""
+    d, base = os.path.split(path)
+    parts = sorted(x for x in os.listdir(d or ".") if re.fullmatch(re.escape(base) + r"\.part\d+", x))
+    if not parts:
+        return
+    with open(path, "a") as out:
+        for name in parts:
+            with open(os.path.join(d, name)) as fh:
+                for line in fh:
+                    if line.endswith("\n"):  # a torn last line was never complete
+                        out.write(line)
+    for name in parts:
+        os.remove(os.path.join(d, name))
 
 
 def gather_lines(lines, device):
@@ -107,15 +169,10 @@ def localGraph_npz(args):
     nsid = args.NSampleID.split(",")
     rawoutput = "%s.vs.%s.TandemRepeat.Raw.bed" % ("-".join(tsid), "-".join(nsid))
     path = os.path.join(args.savedir, rawoutput)
-    rows = load_bundles(args.savedir)
-    finished = set()
-    if getattr(args, "Continue", False) and os.path.exists(path):
-        with open(path) as fh:
-            finished = {"\t".join(x.strip().split("\t")[0:3]) for x in fh if x.strip()}
-    rows = [r for r in rows if "\t".join(r[4].strip().split("\t")[0:3]) not in finished]
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    cont = getattr(args, "Continue", False)
+    dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
@@ -128,17 +185,33 @@ def localGraph_npz(args):
             os.environ.setdefault("SVS_DEVICE", str(local))
         if not dist.is_initialized():
             dist.init_process_group("nccl" if gpu else "gloo")
+        device = torch.device("cuda", local) if gpu else torch.device("cpu")
+    if rank == 0 and cont and os.path.exists(path):
+        merge_parts(path)
+    if dist is not None:
+        dist.barrier()
+    rows = load_bundles(args.savedir)
+    finished = set()
+    if cont and os.path.exists(path):
+        with open(path) as fh:
+            finished = {"\t".join(x.strip().split("\t")[0:3]) for x in fh if x.strip()}
+    rows = [r for r in rows if "\t".join(r[4].strip().split("\t")[0:3]) not in finished]
+
+    if dist is not None:
         owner = shard_lpt(rows, world)
         mine = [r for r, o in zip(rows, owner) if o == rank]
-        lines = [record_line(x) for x in run_windows(mine, args.batch)]
-        lines = gather_lines(lines, torch.device("cuda", local) if gpu else torch.device("cpu"))
+        # each rank journals its records as batches complete; rank 0 receives
+        # every rank's records with one RCCL all_gather and writes the output
+        lines = write_journal(part_path(path, rank), "w", mine, args.batch)
+        lines = gather_lines(lines, device)
+        if rank == 0:
+            with open(path, "a" if finished else "w") as fh:
+                fh.write("".join(line + "\n" for line in lines))
+        dist.barrier()
+        os.remove(part_path(path, rank))
     else:
-        lines = [record_line(x) for x in run_windows(rows, args.batch)]
+        write_journal(path, "a" if finished else "w", rows, args.batch)
     if rank == 0:
-        mode = "a" if finished else "w"
-        with open(path, mode) as fh:
-            for line in lines:
-                fh.write(line + "\n")
         with open(path) as fh:
             allines = [x.rstrip("\n") for x in fh if x.strip()]
         with open(path, "w") as fh:

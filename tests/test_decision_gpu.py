@@ -111,3 +111,59 @@ def test_config3_batch_invariants():
                 seen += [x for x in cluster.split(",") if x]
         assert set(seen) <= ids and len(seen) == len(set(seen)), line[:200]
     assert n_em > 0
+
+
+def test_decision_session_streams_batches_out_of_order():
+    """The streaming session (svs_decision_session_*): golden windows split
+    over several batches, one with no gated window, submitted back to back and
+    waited for out of order, give the reference's records; a closed session
+    refuses work and an unknown ticket fails loudly."""
+    from svscope_amd import _abi
+    from svscope_amd.decision_maker import DecisionSession
+    cases = json.load(open(GOLD))
+    wins = [(c["TDRecord"], c["sequenceList"], np.array(c["ReadIDs"]), c["flank_5"], c["flank_3"]) for c in cases]
+    lines = [c["line"] for c in cases]
+    gate = [k for k, c in enumerate(cases) if c["kind"] in ("one_tag", "few_reads")]
+    assert gate
+    # batch 2 holds only windows that fail the gate (never reach the engine)
+    order = [list(range(0, 5)), gate, [k for k in range(5, len(cases)) if k not in gate]]
+    s = DecisionSession()
+    tickets = [s.submit([wins[k] for k in part]) for part in order]
+    got = {}
+    for t in reversed(tickets):
+        got[t] = s.wait(t)
+    st = s.stats()
+    assert st["msa_tasks"] > 0 and st["poa"]["launches"] > 0
+    for t, part in zip(tickets, order):
+        assert ["\t".join(str(x) for x in r) for r in got[t]] == [lines[k] for k in part]
+    with pytest.raises(_abi.SvsError):
+        _abi.check(s.lib.svs_decision_session_wait(s.handle, 10 ** 6, ctypes_ptr()), "wait")
+    s.close()
+    s.close()  # idempotent
+
+
+def ctypes_ptr():
+    import ctypes
+    return ctypes.byref(ctypes.c_void_p())
+
+
+def test_decision_session_config3_matches_batch_path():
+    """Full-size config-3 windows through the session with batches in flight
+    (the bench's path) equal the one-call batch path record for record."""
+    from collections import deque
+    from svscope_amd import synth
+    from svscope_amd.decision_maker import DecisionSession
+    from svscope_amd.local_graph import _window
+    from svscope_amd.som_td_detector import TDscope_npz_batch
+    rows = [synth.make_window(w, 64, 3000) for w in range(200, 224)]
+    exp = [decision_oracle.record_line(g) for g in TDscope_npz_batch(rows)]
+    got = []
+    with DecisionSession() as s:
+        q = deque()
+        for k in range(0, len(rows), 5):
+            q.append(s.submit([_window(r) for r in rows[k:k + 5]]))
+            if len(q) >= 3:
+                got += s.wait(q.popleft())
+        while q:
+            got += s.wait(q.popleft())
+    assert [decision_oracle.record_line(g) for g in got] == exp

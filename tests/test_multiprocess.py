@@ -24,10 +24,15 @@ def _oracle_run(rows, batch_size=512, context=None, stats=None):
     return [decision_oracle.tdscope_npz(r[4], r[0], np.asarray(r[1]), r[2], r[3]) for r in rows]
 
 
+def _oracle_batches(rows, batch_size=512, context=None, depth=4):
+    for k in range(0, len(rows), batch_size):
+        yield _oracle_run(rows[k:k + batch_size])
+
+
 def _rank_main(rank, world, port, savedir, outdir):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
-    local_graph.run_windows = _oracle_run
+    local_graph.iter_batches = _oracle_batches
     args = argparse.Namespace(TSampleID="T1", NSampleID="N1", savedir=savedir, Continue=False, batch=4)
     path = local_graph.localGraph_npz(args)
     import torch.distributed as dist
