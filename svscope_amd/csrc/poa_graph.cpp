@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace svs {
@@ -294,7 +295,13 @@ void PoaGraph::export_strip_rows(RowTables* t, const int32_t* gaps) const {
   // reader) and row records w0, w1, w3
   uint32_t* __restrict__ pslot = t->pred_slot.data();
   uint32_t* __restrict__ rec = t->rec.data();
-  uint32_t next = 1;  // slot 0: virtual row 0
+  // slot 0: virtual row 0.  Test hook: SVS_POA_TEST_WIDE_SLOTS=<n> numbers the
+  // slots of graphs with >= n rows from 40 up, so that jobs with slot indices
+  // past the pruning kernel's 31 liveness bits share launches with pruned ones.
+  // (read per call, ~1 us against the export's ~0.3 ms: tests set it mid-process)
+  const char* wide_env = std::getenv("SVS_POA_TEST_WIDE_SLOTS");
+  const uint32_t wide_rows = wide_env ? static_cast<uint32_t>(std::strtoul(wide_env, nullptr, 10)) : 0u;
+  uint32_t next = (wide_rows != 0 && V >= wide_rows) ? 40 : 1;
   for (uint32_t r = 0; r < V; ++r) {
     const uint32_t node = rank_to_node_[r];
     const bool store = last[r] != 0;
@@ -320,7 +327,9 @@ void PoaGraph::export_strip_rows(RowTables* t, const int32_t* gaps) const {
       if (x - a < kInlinePreds) w1 |= ps << (16 * (x - a));
       if (pr + 1 != r && last[pr] == r + 1) {
         free_slots.push_back(ps);
-        if (ps < 32) w3 |= 1u << ps;  // the pruning kernel's liveness bits
+        // the pruning kernel's liveness bits: slots 0..30 (bit 31 is its
+        // register row; slots >= 31 have no bit and count as always alive)
+        if (ps < 31) w3 |= 1u << ps;
       }
     }
     w[1] = w1;

@@ -338,9 +338,13 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       const bool store = (w0 >> 9) & 1u;
       const uint32_t np = (w0 >> 10) & 31u;
       const uint32_t own = w0 >> 16;
+      // slots >= 31 have no liveness bit (only jobs without a bound of their
+      // own, kPruneAll, have them): always alive
       auto slot_alive = [&](uint32_t ps) -> bool {
-        return ((alive >> (ps == kNoSlot ? 31u : ps)) & 1u) != 0;
+        if (ps == kNoSlot) return (alive >> 31) != 0;
+        return ps >= 31u || ((alive >> ps) & 1u) != 0;
       };
+      const uint32_t own_bit = (store && own < 31u) ? 1u << own : 0u;
       auto publish = [&]() {
         if (WPJ > 1 && write_bnd && ((r & 7u) == 7u || r + 1 == V) && lane == 0)
           __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
@@ -374,7 +378,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
             reinterpret_cast<uint16_t*>(q + 65)[lane] = 0;  // F = O = H = VNEG
           }
           // own slot dead, slots whose last reader this row is (w3) released
-          alive &= ~(rec[static_cast<uint64_t>(r) * kRecWords + 3] | (store ? 1u << own : 0u) | kRegBit);
+          alive &= ~(rec[static_cast<uint64_t>(r) * kRecWords + 3] | own_bit | kRegBit);
           pH = pF = pO = pHm = SVS_VNEG;
 #ifdef SVS_STRIP_PROF
           pr_slow += 1;
@@ -544,7 +548,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const int32_t ub = ub_of(w2w3.x, rrem, mrr);
         any_alive = __builtin_amdgcn_ballot_w64(rrem >= 0 && H + ub >= lb) != 0;
         const bool out_alive = any_alive || cH_in > SVS_VNEG / 2;
-        const uint32_t ob = (store ? 1u << own : 0u) | kRegBit;
+        const uint32_t ob = own_bit | kRegBit;
         alive = ((alive & ~ob) | (out_alive ? ob : 0u)) & ~w2w3.y;
       }
       if (store) {

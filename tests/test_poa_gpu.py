@@ -153,3 +153,28 @@ def test_pruning_stats_and_exactness(slack, retries):
         assert st["prune_retries"] > 0
     else:
         assert st["cells_computed"] < 0.6 * st["dp_cells"], st
+
+
+def test_wide_slot_jobs_share_pruned_launches():
+    """Jobs whose pool slots go past the pruning kernel's 31 liveness bits get
+    no bound of their own (kPruneAll) yet run in the same pruning launches as
+    bounded jobs; both give the oracle's result.  The test hook numbers the
+    slots of graphs with >= 1500 rows from 40 up."""
+    import os
+    from svscope_amd import synth
+    from svscope_amd.poa import poa_batch
+    wide = [synth.make_window(w, 8, 2500)[0] for w in range(2)]
+    small = helpers.random_cases(77, 30, max_seqs=10, max_len=260, edits=20)
+    cases = [c for pair in zip(small[:2], wide) for c in pair] + small[2:]
+    old = os.environ.get("SVS_POA_TEST_WIDE_SLOTS")
+    os.environ["SVS_POA_TEST_WIDE_SLOTS"] = "1500"
+    try:
+        got, st = poa_batch(cases, return_stats=True)
+    finally:
+        if old is None:
+            os.environ.pop("SVS_POA_TEST_WIDE_SLOTS", None)
+        else:
+            os.environ["SVS_POA_TEST_WIDE_SLOTS"] = old
+    for seqs, g in zip(cases, got):
+        assert g == oracle_poa(seqs, 1)
+    assert st["cells_computed"] < st["dp_cells"], st
