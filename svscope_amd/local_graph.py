@@ -169,23 +169,8 @@ def localGraph_npz(args):
     nsid = args.NSampleID.split(",")
     rawoutput = "%s.vs.%s.TandemRepeat.Raw.bed" % ("-".join(tsid), "-".join(nsid))
     path = os.path.join(args.savedir, rawoutput)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     cont = getattr(args, "Continue", False)
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        # RCCL between GPUs; gloo only for CPU rehearsals of the plumbing (the
-        # windows themselves still need the HIP engine)
-        gpu = torch.cuda.is_available()
-        if gpu:
-            torch.cuda.set_device(local)
-            os.environ.setdefault("SVS_DEVICE", str(local))
-        if not dist.is_initialized():
-            dist.init_process_group("nccl" if gpu else "gloo")
-        device = torch.device("cuda", local) if gpu else torch.device("cpu")
+    world, rank, dist, device = _dist_setup()
     if rank == 0 and cont and os.path.exists(path):
         merge_parts(path)
     if dist is not None:
@@ -196,33 +181,144 @@ def localGraph_npz(args):
         with open(path) as fh:
             finished = {"\t".join(x.strip().split("\t")[0:3]) for x in fh if x.strip()}
     rows = [r for r in rows if "\t".join(r[4].strip().split("\t")[0:3]) not in finished]
-
     if dist is not None:
-        owner = shard_lpt(rows, world)
-        mine = [r for r, o in zip(rows, owner) if o == rank]
         # each rank journals its records as batches complete; rank 0 receives
         # every rank's records with one RCCL all_gather and writes the output
+        owner = shard_lpt(rows, world)
+        mine = [r for r, o in zip(rows, owner) if o == rank]
         lines = write_journal(part_path(path, rank), "w", mine, args.batch)
-        lines = gather_lines(lines, device)
+    else:
+        lines = write_journal(path, "a" if finished else "w", rows, args.batch)
+    return _finish(path, lines, rank, world, dist, device, finished, t0, "Local Graph")
+
+
+def _dist_setup():
+    """(world, rank, dist or None, device): one process per GPU, RCCL between
+    GPUs; gloo only for CPU rehearsals of the plumbing."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world <= 1:
+        return world, rank, None, None
+    import torch
+    import torch.distributed as dist
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = torch.cuda.is_available()
+    if gpu:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("SVS_DEVICE", str(local))
+    if not dist.is_initialized():
+        dist.init_process_group("nccl" if gpu else "gloo")
+    return world, rank, dist, torch.device("cuda", local) if gpu else torch.device("cpu")
+
+
+def _finish(path, lines_by_rank, rank, world, dist, device, finished, t0, what):
+    """Multi-rank: gather every rank's journalled lines to rank 0 (one RCCL
+    all_gather), then rank 0 sorts the output like sort -k1,1 -k2,2n."""
+    if dist is not None:
+        lines = gather_lines(lines_by_rank, device)
         if rank == 0:
             with open(path, "a" if finished else "w") as fh:
                 fh.write("".join(line + "\n" for line in lines))
         dist.barrier()
         os.remove(part_path(path, rank))
-    else:
-        write_journal(path, "a" if finished else "w", rows, args.batch)
     if rank == 0:
         with open(path) as fh:
             allines = [x.rstrip("\n") for x in fh if x.strip()]
         with open(path, "w") as fh:
             for line in sort_lines(allines):
                 fh.write(line + "\n")
-        log.info("Local Graph : work finished with %s hour", (time.time() - t0) / 3600)
+        log.info("%s : work finished with %s hour", what, (time.time() - t0) / 3600)
     return path
 
 
+def localGraph(args, readers=None):
+    """The BAM-reading localGraph (SVscope.py:118-183): window BED ->
+    DataMaker -> Decision (+ the DUP corner re-scan, TDscope) -> Raw.bed.
+
+    Extraction (data_maker.DataMaker / DataMaker2, BAM I/O) runs in a
+    process pool of min(6, -p) spawned workers, as the reference caps its
+    Pool (:158-161); each chunk of ``args.batch`` windows then goes through
+    TDscope_batch (DecisionBatch on the GPU), the next chunk's extraction
+    overlapping it.  Records are journalled per chunk (flushed), --Continue
+    skips windows already written (the reference's check never matches,
+    SURVEY.md §5), multi-GPU shards windows round-robin (their cost is unknown
+    before extraction) with the same single RCCL gather as localGraph_npz.
+    ``readers`` replaces pysam (data_maker's hook)."""
+    import functools
+    import multiprocessing as mp
+    import sys
+    from .data_maker import DataMaker, DataMaker2
+    from .som_td_detector import TDscope_batch
+    t0 = time.time()
+    tumor, normal = args.Tumorbam.split(","), args.Normalbam.split(",")
+    tsid, nsid = args.TSampleID.split(","), args.NSampleID.split(",")
+    if len(tsid) != len(tumor):
+        print("SampleID not meet tumor bam file, exit !")
+        sys.exit(1)
+    if len(nsid) != len(normal):
+        print("SampleID not meet normal bam file, exit !")
+        sys.exit(1)
+    bams = tumor + normal
+    labels = [x + "_tumor" for x in tsid] + [x + "_normal" for x in nsid]
+    rawoutput = "%s.vs.%s.TandemRepeat.Raw.bed" % ("-".join(tsid), "-".join(nsid))
+    if not os.path.exists(args.savedir):
+        os.mkdir(args.savedir)
+    path = os.path.join(args.savedir, rawoutput)
+    with open(args.windowBed) as fh:
+        records = ["\t".join(x.strip().split("\t")) for x in fh.readlines()]
+    cont = getattr(args, "Continue", False)
+    world, rank, dist, device = _dist_setup()
+    if rank == 0 and cont and os.path.exists(path):
+        merge_parts(path)
+    if dist is not None:
+        dist.barrier()
+    finished = set()
+    if cont and os.path.exists(path):
+        with open(path) as fh:
+            finished = {"\t".join(x.strip().split("\t")[0:3]) for x in fh if x.strip()}
+    records = [r for r in records if "\t".join(r.split("\t")[0:3]) not in finished]
+    mine = records[rank::world]
+    dm = functools.partial(DataMaker, refFile=args.Reference, bamFileList=bams, LabelList=labels,
+                           offset=int(args.offset), mapQ=int(args.mapQ), readers=readers)
+    dm2 = functools.partial(DataMaker2, refFile=args.Reference, bamFileList=bams, LabelList=labels,
+                            offset=int(args.offset), mapQ=int(args.mapQ), readers=readers)
+    procs = min(6, int(args.thread))
+    pool = mp.get_context("spawn").Pool(procs) if procs > 1 else None
+    map_fn = pool.map if pool else map
+    B = max(1, int(getattr(args, "batch", 512)))
+    chunks = [mine[k:k + B] for k in range(0, len(mine), B)]
+    out_path = part_path(path, rank) if dist is not None else path
+    lines = []
+    try:
+        with open(out_path, "w" if dist is not None else ("a" if finished else "w")) as fh:
+            nxt = pool.map_async(dm, chunks[0]) if (pool and chunks) else None
+            for k, chunk in enumerate(chunks):
+                bundles = nxt.get() if nxt is not None else [dm(r) for r in chunk]
+                nxt = pool.map_async(dm, chunks[k + 1]) if (pool and k + 1 < len(chunks)) else None
+                recs = TDscope_batch(chunk, dm, dm2, map_fn=map_fn, bundles=bundles)
+                chunk_lines = [record_line(x) for x in recs]
+                fh.write("".join(line + "\n" for line in chunk_lines))
+                fh.flush()
+                lines.extend(chunk_lines)
+    finally:
+        if pool:
+            pool.close()
+            pool.join()
+    return _finish(path, lines, rank, world, dist, device, finished, t0, "Local Graph")
+
+
 def main(argv=None):
-    ap = argparse.ArgumentParser(description="SVScope localGraph_npz on MI355X")
+    """python -m svscope_amd.local_graph [localGraph|localGraph_npz] ...
+    (the SVscope.py sub-commands of this path; localGraph_npz by default)."""
+    import sys
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd = argv.pop(0) if argv and argv[0] in ("localGraph", "localGraph_npz") else "localGraph_npz"
+    ap = argparse.ArgumentParser(description="SVScope %s on MI355X" % cmd)
+    if cmd == "localGraph":
+        ap.add_argument("-w", "--windowBed", required=True)
+        ap.add_argument("-T", "--Tumorbam", required=True)
+        ap.add_argument("-N", "--Normalbam", required=True)
+        ap.add_argument("-r", "--Reference", required=True)
     ap.add_argument("-t", "--TSampleID", required=True)
     ap.add_argument("-n", "--NSampleID", required=True)
     ap.add_argument("-s", "--savedir", required=True)
@@ -233,7 +329,7 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=512, help="windows per GPU batch")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
-    print(localGraph_npz(args))
+    print(localGraph(args) if cmd == "localGraph" else localGraph_npz(args))
 
 
 if __name__ == "__main__":

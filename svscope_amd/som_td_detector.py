@@ -6,7 +6,9 @@
 corner re-scan branch (:41-58); DataMaker/DataMaker2 are the caller's
 BAM readers (pysam, out of scope here) bound with functools.partial exactly as
 SVscope.py:152-154 does, so both stay picklable.
-``TDscope_npz_batch(rows)`` is the batched form used by localGraph_npz.
+``TDscope_npz_batch(rows)`` is the batched form used by localGraph_npz, and
+``TDscope_batch(records, DataMaker, DataMaker2)`` the batched form of TDscope
+used by localGraph (svscope_amd/data_maker.py holds the readers).
 """
 import logging
 import re
@@ -41,6 +43,47 @@ def TDscope(TDRecord, DataMaker, DataMaker2, DecisionMaker):
                 Record[-1] = flag3
     log.info("pipeline for region %s finished Take %ss", TDRecord, time.time() - start_time)
     return Record
+
+
+def _emoutput(rec):
+    return rec[-1].split("|")[-1] == "EMOutput"
+
+
+def TDscope_batch(TDRecords, DataMaker, DataMaker2, map_fn=map, context=None, Tlabel="tumor", readcutoff=3,
+                  hcutoff=3, scutoff=0.05, bundles=None):
+    """TDscope over many windows, each Decision round batched on the GPU.
+
+    Same records as ``[TDscope(r, DataMaker, DataMaker2, Decision) for r in
+    TDRecords]`` (SomTDDetector.py:26-61): DataMaker for every window
+    (through ``map_fn``, e.g. a process pool's map, since it is BAM I/O),
+    one DecisionBatch for all of them, then for the DUP windows without an
+    EMOutput one DataMaker2 each, one DecisionBatch for their 5' corners, one
+    for the 3' corners of those still without, and the flag rewrite of
+    :55-58.  ``bundles``, if given, is the precomputed DataMaker output."""
+    data = list(bundles) if bundles is not None else list(map_fn(DataMaker, TDRecords))
+    kw = dict(Tlabel=Tlabel, readcutoff=readcutoff, hcutoff=hcutoff, scutoff=scutoff, context=context)
+    # the window record's column 4 (IndexError on a 3-column record, as :39)
+    sv_types = [d[4].strip().split("\t")[3].split(",")[0] for d in data]
+    records = DecisionBatch([(d[4], d[0], d[1], d[2], d[3], d[5]) for d in data], **kw)
+    dup = [i for i, rec in enumerate(records) if not _emoutput(rec) and sv_types[i] == "DUP"]
+    if not dup:
+        return records
+    rescans = list(map_fn(DataMaker2, [data[i][4] for i in dup]))
+    rec5 = DecisionBatch([tuple(r[0][k] for k in (4, 0, 1, 2, 3, 5)) for r in rescans], **kw)
+    left = [j for j in range(len(dup)) if not _emoutput(rec5[j])]
+    rec3 = DecisionBatch([tuple(rescans[j][1][k] for k in (4, 0, 1, 2, 3, 5)) for j in left], **kw)
+    rec3 = dict(zip(left, rec3))
+    for j, i in enumerate(dup):
+        c5, c3 = rescans[j]
+        if _emoutput(rec5[j]):
+            records[i] = rec5[j]
+        elif _emoutput(rec3[j]):
+            records[i] = rec3[j]
+        elif len([x for x in np.setdiff1d(c5[1], data[i][1]) if re.search("_tumor", x)]) >= 3:
+            records[i][-1] = c5[5]
+        elif len([x for x in np.setdiff1d(c3[1], data[i][1]) if re.search("_tumor", x)]) >= 3:
+            records[i][-1] = c3[5]
+    return records
 
 
 def TDscope_npz(TDRecord, sequenceList, ReadIDs, flank_5, flank_3):
