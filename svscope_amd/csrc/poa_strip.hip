@@ -126,13 +126,66 @@ __device__ __forceinline__ void strip_gaps_nf(const PoaScore& P, int32_t j0, int
 // Prefetched inputs of one row: its record and its carries into this strip
 // (strip 0: column-0 values H0, F0, O0 from fill_col0).
 struct RowIn {
-  uint32_t w0, w1;
+  uint32_t w0, w1, w2, w3;
   int32_t b0, b1, b2, b3;
 };
 
 __device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, const uint32_t* __restrict__ spill) {
   if (k >= kInlinePreds) return spill[k];
   return (d.w1 >> (16 * k)) & 0xFFFFu;
+}
+
+// Traceback code of a one-in-edge cell off column 0 (the np <= 1 tests of
+// poa_strip_kernel) as 14 compares and 16 selects/shifts, all VALU: the
+// compares write three rotating SGPR pairs, each read as a v_cndmask mask three
+// instructions later (gfx950 needs two wait states between a VALU SGPR write
+// and a VALU mask read).  Written as one asm block because LLVM otherwise
+// merges the select chains into scalar mask logic (s_and/s_or_b64), which
+// competes with the row loop's bookkeeping for the scalar issue slots.
+//   code = dg ? 0 : up ? upc : lf ? lfc : 3,  upc = ua || (!ub && uc) ? 5 : 1,
+//   lfc = la || (!lb && lc) ? 6 : 2,  | lbit << 8  | vbit << 9
+__device__ __forceinline__ uint32_t code_np1(int32_t H, int32_t D, int32_t mFO, int32_t mEQ, int32_t fpe,
+                                             int32_t hpg, int32_t opc, int32_t hpq, int32_t prevEe,
+                                             int32_t prevHg, int32_t prevQc, int32_t prevHq, int32_t E, int32_t Q,
+                                             int32_t F, int32_t O) {
+  uint32_t r1, r2, c, t, v;
+  uint64_t m0, m1, m2;
+  asm("v_cmp_eq_u32_e64 %[m0], %[H], %[opc]\n\t"
+      "v_cmp_eq_u32_e64 %[m1], %[H], %[hpg]\n\t"
+      "v_cmp_eq_u32_e64 %[m2], %[H], %[fpe]\n\t"
+      "v_cndmask_b32_e64 %[r1], 1, 5, %[m0]\n\t"
+      "v_cmp_eq_u32_e64 %[m0], %[H], %[prevQc]\n\t"
+      "v_cndmask_b32_e64 %[r1], %[r1], 1, %[m1]\n\t"
+      "v_cmp_eq_u32_e64 %[m1], %[H], %[prevHg]\n\t"
+      "v_cndmask_b32_e64 %[r1], %[r1], 5, %[m2]\n\t"
+      "v_cmp_eq_u32_e64 %[m2], %[H], %[prevEe]\n\t"
+      "v_cndmask_b32_e64 %[r2], 2, 6, %[m0]\n\t"
+      "v_cmp_eq_u32_e64 %[m0], %[H], %[mEQ]\n\t"
+      "v_cndmask_b32_e64 %[r2], %[r2], 2, %[m1]\n\t"
+      "v_cmp_eq_u32_e64 %[m1], %[H], %[mFO]\n\t"
+      "v_cndmask_b32_e64 %[r2], %[r2], 6, %[m2]\n\t"
+      "v_cmp_eq_u32_e64 %[m2], %[H], %[D]\n\t"
+      "v_cndmask_b32_e64 %[c], 3, %[r2], %[m0]\n\t"
+      "v_cmp_eq_u32_e64 %[m0], %[E], %[prevHg]\n\t"
+      "v_cndmask_b32_e64 %[c], %[c], %[r1], %[m1]\n\t"
+      "v_cmp_eq_u32_e64 %[m1], %[Q], %[prevHq]\n\t"
+      "v_cndmask_b32_e64 %[c], %[c], 0, %[m2]\n\t"
+      "v_cmp_eq_u32_e64 %[m2], %[O], %[hpq]\n\t"
+      "v_cndmask_b32_e64 %[t], 0, 1, %[m0]\n\t"
+      "v_cmp_eq_u32_e64 %[m0], %[F], %[fpe]\n\t"
+      "v_cndmask_b32_e64 %[t], %[t], 1, %[m1]\n\t"
+      "v_cmp_eq_u32_e64 %[m1], %[F], %[hpg]\n\t"
+      "v_cndmask_b32_e64 %[v], 0, 1, %[m2]\n\t"
+      "v_lshl_or_b32 %[c], %[t], 8, %[c]\n\t"
+      "v_cndmask_b32_e64 %[v], %[v], 0, %[m0]\n\t"
+      "v_cndmask_b32_e64 %[v], %[v], 1, %[m1]\n\t"
+      "v_lshl_or_b32 %[c], %[v], 9, %[c]"
+      : [r1] "=&v"(r1), [r2] "=&v"(r2), [c] "=&v"(c), [t] "=&v"(t), [v] "=&v"(v), [m0] "=&s"(m0), [m1] "=&s"(m1),
+        [m2] "=&s"(m2)
+      : [H] "v"(H), [D] "v"(D), [mFO] "v"(mFO), [mEQ] "v"(mEQ), [fpe] "v"(fpe), [hpg] "v"(hpg), [opc] "v"(opc),
+        [hpq] "v"(hpq), [prevEe] "v"(prevEe), [prevHg] "v"(prevHg), [prevQc] "v"(prevQc), [prevHq] "v"(prevHq),
+        [E] "v"(E), [Q] "v"(Q), [F] "v"(F), [O] "v"(O));
+  return c;
 }
 
 }  // namespace
@@ -307,6 +360,12 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       const uint32_t* w = rec + static_cast<uint64_t>(rr) * kRecWords;
       d.w0 = w[0];
       d.w1 = w[1];
+      if constexpr (PRUNE) {
+        // path lengths and released slots, read after the DP: prefetched with
+        // the rest of the record instead of a dependent load in the row step
+        d.w2 = w[2];
+        d.w3 = w[3];
+      }
       if (FIRST) {
         d.b0 = rc0[3 * rr];
         d.b1 = rc0[3 * rr + 1];
@@ -356,7 +415,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         bool live;
         if (FIRST) {
           const int32_t h0 = __builtin_amdgcn_readfirstlane(d.b0);
-          live = h0 + ub_of(rec[static_cast<uint64_t>(r) * kRecWords + 2], L, P.m * L) >= lb;
+          live = h0 + ub_of(__builtin_amdgcn_readfirstlane(d.w2), L, P.m * L) >= lb;
         } else {
           live = cH_in > SVS_VNEG / 2;
         }
@@ -378,7 +437,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
             reinterpret_cast<uint16_t*>(q + 65)[lane] = 0;  // F = O = H = VNEG
           }
           // own slot dead, slots whose last reader this row is (w3) released
-          alive &= ~(rec[static_cast<uint64_t>(r) * kRecWords + 3] | own_bit | kRegBit);
+          alive &= ~(__builtin_amdgcn_readfirstlane(d.w3) | own_bit | kRegBit);
           pH = pF = pO = pHm = SVS_VNEG;
 #ifdef SVS_STRIP_PROF
           pr_slow += 1;
@@ -392,7 +451,8 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       if constexpr (PRUNE) ++rows_done;
       // the row's path lengths (w2) and released slots (w3), needed after the DP
       uint2 w2w3 = make_uint2(0, 0);
-      if constexpr (PRUNE) w2w3 = *reinterpret_cast<const uint2*>(rec + static_cast<uint64_t>(r) * kRecWords + 2);
+      if constexpr (PRUNE)
+        w2w3 = make_uint2(__builtin_amdgcn_readfirstlane(d.w2), __builtin_amdgcn_readfirstlane(d.w3));
       int32_t H0 = 0, F0 = 0, O0 = 0;
       StripCarry cr;
       if (FIRST) {
@@ -446,6 +506,18 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const uint32_t ps = __builtin_amdgcn_readfirstlane(d.w1) & 0xFFFFu;  // np == 0: slot 0 (virtual row)
         int32_t hp, fp, op, hpm;
         pred_vals(ps, hp, fp, op, hpm);
+#ifdef SVS_OPT_CODE
+        if constexpr (!FIRST) {
+          const int32_t hpg = hp + P.g, fpe = fp + P.e, hpq = hp + P.q, opc = op + P.c, D = hpm + mc;
+          F = imax(hpg, fpe);
+          O = imax(hpq, opc);
+          gaps(imax(D, imax(F, O)), true);
+          code = code_np1(H, D, imax(F, O), imax(E, Q), fpe, hpg, opc, hpq, prevEe, prevH + P.g, prevQc,
+                          prevH + P.q, E, Q, F, O);
+          if (np == 0) code = (code & 0x1FFu) | (31u << 10);
+        } else
+#endif
+        {
         F = imax(hp + P.g, fp + P.e);
         O = imax(hp + P.q, op + P.c);
         int32_t Hpre = imax(hpm + mc, imax(F, O));
@@ -474,6 +546,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         code |= lbit ? 0x100u : 0u;
         if (np != 0) code |= (va || (!vb && vc)) ? 0x200u : 0u;
         else code |= 31u << 10;
+        }
       } else if (!FIRST && np == 2) {
         // Two in-edges (the common merge row), both kept in registers between
         // the DP and the code tests.  Per in-edge k, Fk = max(hp+g, fp+e) and
@@ -543,6 +616,23 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k, uc_stop);
       }
       tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+#ifdef SVS_PROBE_SALU
+      // development probe: extra scalar work per computed row (issue-bound test)
+      {
+        uint32_t z = w0;
+#pragma unroll
+        for (int q = 0; q < SVS_PROBE_SALU; ++q) asm volatile("s_add_u32 %0, %0, 1" : "+s"(z));
+        asm volatile("" ::"s"(z));
+      }
+#endif
+#ifdef SVS_PROBE_VALU
+      {
+        uint32_t z = code;
+#pragma unroll
+        for (int q = 0; q < SVS_PROBE_VALU; ++q) asm volatile("v_add_u32 %0, %0, %0" : "+v"(z));
+        asm volatile("" ::"v"(z));
+      }
+#endif
       bool any_alive = true;
       if (prune) {
         const int32_t ub = ub_of(w2w3.x, rrem, mrr);
