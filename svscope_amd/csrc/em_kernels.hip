@@ -14,6 +14,7 @@
 // Rlik.sum() pairwise); the BLAS dot products are summed in feature order.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 #include "svs_em_device.hpp"
 
@@ -253,14 +254,68 @@ __device__ __forceinline__ void e_accumulate(const uint8_t* __restrict__ xi, con
   for (int k = 0; k < K; ++k) out[k] = acc[k];
 }
 
+// The same contraction on the matrix cores (SVS_EM_MFMA=1 variant):
+// A[i,k] = sum over the 5 nf one-hot columns (f, a) of [x_if == a] LT[(f,a), k],
+// a dense (N x 5nf) . (5nf x K) product of v_mfma_f64_16x16x4_f64 tiles, one
+// 16-read tile per wave at a time, K padded to 16 columns.  Operand maps
+// (gfx950, one f64 per lane): A[i = l&15][kk = l>>4], B[kk = l>>4][j = l&15];
+// result D[row = (l>>4) + 4 r][col = l&15], r = 0..3.  Four of every five
+// products are with a one-hot zero and K <= 9 of the 16 columns are real:
+// the work is ~9x the gather's, kept as the measured alternative
+// (DESIGN.md §4.3).
+typedef double svs_f64x4 __attribute__((ext_vector_type(4)));
+__device__ void e_accumulate_mfma(const EmWindow& W, int K, const uint8_t* __restrict__ xr,
+                                  const double* __restrict__ lt, double* __restrict__ out) {
+  const int N = W.n_reads, nf = W.n_feat, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int nfp = (nf + 15) & ~15;
+  const int kd = 5 * nf;                       // contraction length
+  const int kq = lane >> 4, col = lane & 15;   // this lane's k-slot and A row / B column
+  for (int tile = wave; tile * 16 < N; tile += 4) {
+    const int i = tile * 16 + col;             // A row (read) of this lane
+    const uint8_t* xi = xr + static_cast<int64_t>(i < N ? i : 0) * nfp;
+    svs_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int base = 0; base < kd; base += 4) {
+      const int kk = base + kq;                // one-hot column (f, a) = (kk / 5, kk % 5)
+      const int f = kk / 5, a = kk - 5 * f;
+      const double av = (i < N && kk < kd && xi[f] == a) ? 1.0 : 0.0;
+      const double bv = (col < K && kk < kd) ? lt[static_cast<int64_t>(kk) * K + col] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+    if (col < K) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = tile * 16 + kq + 4 * r;
+        if (row < N) out[row * K + col] = acc[r];
+      }
+    }
+  }
+}
+
 // E-step (gamma_updating :132-155) + the feature part of loglik,
 // A[i,k] = sum_f log theta'[k,f,x_if].  Lane = read, each of the 4 waves sums
 // a quarter of the features (gathers LT rows (f, x_if) of K contiguous
 // doubles), then the quarters are added in wave order.
+template <bool MFMA>
 __device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xr, const double* __restrict__ pi,
                        const double* __restrict__ lt, double* __restrict__ A, double* __restrict__ M,
                        double* __restrict__ g, EmLds* L) {
   const int N = W.n_reads, nf = W.n_feat, tid = threadIdx.x;
+  if constexpr (MFMA) {
+    e_accumulate_mfma(W, K, xr, lt, L->part);
+    __syncthreads();
+    for (int r = tid; r < N * K; r += blockDim.x) {
+      A[r] = L->part[r];
+      M[r] = L->part[r] + log(pi[r % K]);
+    }
+    __syncthreads();
+    for (int r = tid; r < N * K; r += blockDim.x) {
+      const int i = r / K, I = r % K;
+      g[r] = 1.0 / exp_row_sum(M + i * K, K, M[i * K + I]);
+    }
+    __syncthreads();
+    return;
+  }
   const int lane = tid & 63, wave = tid >> 6;
   const int NP = read_pad(N), chunks = NP >> 6;       // 64-read chunks (1..4)
   const int slices = 4 / chunks;                       // feature slices per chunk
@@ -298,6 +353,7 @@ __device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xr,
   __syncthreads();
 }
 
+template <bool MFMA>
 __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restrict__ wins,
                                                          const uint8_t* __restrict__ X,
                                                          const int32_t* __restrict__ labels,
@@ -355,10 +411,10 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
       for (int r = tid; r < N * K; r += blockDim.x) g[r] = (lk[r / K] - 1 == r % K) ? 1.0 : 0.0;
       __syncthreads();
       m_step(W, K, xt, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh, &lds);
-      e_step(W, K, xr, pi, lt, A, M, g, &lds);
+      e_step<MFMA>(W, K, xr, pi, lt, A, M, g, &lds);
       for (int it = 0; it < cfg.n_step; ++it) {
         m_step(W, K, xt, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh, &lds);
-        e_step(W, K, xr, pi, lt, A, M, g, &lds);
+        e_step<MFMA>(W, K, xr, pi, lt, A, M, g, &lds);
         for (int i = tid; i < N; i += blockDim.x) {
           double s = 0.0;
           for (int k = 0; k < K; ++k) s += (A[i * K + k] + log(clip_eps(pi[k], cfg.eps))) * g[i * K + k];
@@ -421,8 +477,16 @@ hipError_t launch_em_cluster(const EmWindow* wins, int n, const uint8_t* X, cons
                              const double* rng, uint64_t rng_len, const EmConfig& cfg, double* ws, double* outd,
                              int32_t* outi, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(em_cluster_kernel, dim3(n), dim3(256), 0, stream, wins, X, labels, rng, rng_len, cfg, ws,
-                     outd, outi);
+  // SVS_EM_MFMA=1: the E-step contraction on v_mfma_f64_16x16x4_f64 (measured
+  // alternative, see e_accumulate_mfma); default: the one-hot gather
+  const char* me = std::getenv("SVS_EM_MFMA");  // read per launch (a few per batch): tests switch it
+  const bool mfma = me && me[0] == '1';
+  if (mfma)
+    hipLaunchKernelGGL(em_cluster_kernel<true>, dim3(n), dim3(256), 0, stream, wins, X, labels, rng, rng_len, cfg,
+                       ws, outd, outi);
+  else
+    hipLaunchKernelGGL(em_cluster_kernel<false>, dim3(n), dim3(256), 0, stream, wins, X, labels, rng, rng_len, cfg,
+                       ws, outd, outi);
   return hipGetLastError();
 }
 

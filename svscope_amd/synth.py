@@ -62,13 +62,19 @@ def _to_str(codes):
     return _ALPHA[codes].tobytes().decode("ascii")
 
 
-def make_window(w, n_reads, ref_len, offset=50, chrom="chrS", sample_t="T1", sample_n="N1"):
+def make_window(w, n_reads, ref_len, offset=50, chrom="chrS", sample_t="T1", sample_n="N1", error=0.08,
+                ins_range=(200, 801)):
+    """One window; ``error`` scales the 8 % ONT profile (3.5/2.5/2 % sub/del/
+    ins), ``ins_range`` the somatic insertion length (the defaults are §8(d)'s
+    profile; other values give the harsher probes of tools/prune_probe.py)."""
     seed = (20250509 + w) % (2 ** 32)
     rs = np.random.RandomState(seed)
     ref = rs.randint(0, 4, size=ref_len)
     mid = ref_len // 2
+    k = error / 0.08
+    mut = {} if error == 0.08 else dict(p_sub=0.035 * k, p_del=0.025 * k, p_ins=0.02 * k)
     if w % 2 == 0:
-        ins_len = int(rs.randint(200, 801))
+        ins_len = int(rs.randint(*ins_range))
         som = np.concatenate([ref[:mid], rs.randint(0, 4, size=ins_len), ref[mid:]])
     else:
         del_len = int(rs.randint(100, 601))
@@ -82,11 +88,11 @@ def make_window(w, n_reads, ref_len, offset=50, chrom="chrS", sample_t="T1", sam
     for i in range(n_tumor):
         hap = som if i < n_som else ref
         rrs = np.random.RandomState((seed * 1000 + i) % (2 ** 32))
-        reads.append(_to_str(_mutate(hap, rrs)))
+        reads.append(_to_str(_mutate(hap, rrs, **mut)))
         ids.append(f"{sample_t}_tumor|w{w}_r{i}")
     for i in range(n_tumor, n_reads):
         rrs = np.random.RandomState((seed * 1000 + i) % (2 ** 32))
-        reads.append(_to_str(_mutate(ref, rrs)))
+        reads.append(_to_str(_mutate(ref, rrs, **mut)))
         ids.append(f"{sample_n}_normal|w{w}_r{i}")
     ref_s = _to_str(ref)
     start = 1_000_000 + w * 10_000 + offset

@@ -88,3 +88,18 @@ def test_em_matches_oracle_many_reads_and_wide_windows():
         np.testing.assert_array_equal(r["Rclust"], o["Rclust"])
         np.testing.assert_allclose(r["BICList"], o["BICList"], rtol=1e-9, atol=1e-5)
         np.testing.assert_allclose(r["lik"], o["lik"], rtol=0, atol=1e-5)
+
+
+@pytest.fixture
+def em_mfma(monkeypatch):
+    monkeypatch.setenv("SVS_EM_MFMA", "1")
+
+
+def test_em_mfma_variant_matches_reference_goldens(em_mfma):
+    """The v_mfma_f64_16x16x4_f64 E-step contraction (SVS_EM_MFMA=1) keeps the
+    reference's K and labels exactly, BIC / log-likelihood within 1e-5."""
+    test_em_matches_reference_goldens()
+
+
+def test_em_mfma_variant_matches_oracle(em_mfma):
+    test_em_matches_oracle_random_and_reinit_heavy()
