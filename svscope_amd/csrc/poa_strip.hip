@@ -83,6 +83,8 @@ struct StripConst {
   int32_t jc, je, ve, vc;
 };
 
+typedef int32_t svs_i32x4 __attribute__((ext_vector_type(4)));
+
 struct GapOut {
   int32_t Q, E, H, prevH, prevEe, prevQc;  // prevEe = E[j-1] + e, prevQc = Q[j-1] + c
 };
@@ -112,6 +114,12 @@ __device__ __forceinline__ void strip_gaps_nf(const PoaScore& P, int32_t j0, int
   o.prevEe = shr1_add(cr.cE + P.e, o.E, K.ve);
   o.prevQc = shr1_add(cr.cQ + P.c, o.Q, K.vc);
   o.prevH = wave_shr1(o.H, cr.cH, 0);
+#ifdef SVS_OPT_CARRY
+  // the next strip's carries are lane 63's Q - jc, E - je, Hpre and H
+  // (run1' = max(P1, run1) = Q - jc, run2' = max(P2, run2, T1, T2) = E - je):
+  // stored from lane 63 by the caller, no scalar work here
+  return;
+#endif
   const int32_t jl = j0 + 63;
   const int32_t p1l = readlane63(p1), p2l = readlane63(p2), hl = readlane63(Hpre);
   const int32_t T2l = cr.run1 + (jl - 1) * P.c + P.g - jl * P.e;
@@ -232,12 +240,20 @@ template <bool LDSP, int WPJ, bool PRUNE>
 #endif
 #define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? SVS_PRUNE_OCC : 1)))
 __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
-    const PoaJob* __restrict__ jobs, int n_jobs, PoaScore P, const uint32_t* __restrict__ rec_all,
+    const PoaJob* __restrict__ jobs, int n_jobs, PoaScore Parg, const uint32_t* __restrict__ rec_all,
     const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
     const uint32_t* __restrict__ pred_slot, const int32_t* __restrict__ col0, const uint8_t* __restrict__ seqs,
     uint16_t* __restrict__ tb, int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
     int32_t* __restrict__ gpool, int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
   extern __shared__ int32_t lds[];
+#ifdef SVS_FIXED_SCORES
+  // development: spoa's default scores as compile-time constants (the only
+  // ones the reference uses); the host checks the configuration
+  constexpr PoaScore P{5, -4, -8, -6, -10, -4};
+  (void)Parg;
+#else
+  const PoaScore P = Parg;
+#endif
   __shared__ int32_t prog[WPJ];  // per wave: strip * (V + 1) + rows done, carries published
   __shared__ int32_t s_err;
   __shared__ int32_t s_brow[WPJ], s_best[WPJ];
@@ -312,6 +328,13 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const uint8_t rc = seq[j - 1];  // seqs[seq_off - 1] is a zero pad byte (column 0)
     const int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
     int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
+#ifdef SVS_OPT_CARRY
+    // this strip's carry block as a raw buffer: lanes other than 63 store out
+    // of range (offset >= 2^31 > the block size), which the hardware drops
+    const __amdgpu_buffer_rsrc_t bout_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(bout, 0, static_cast<int32_t>(VP * 16), 0x00020000);
+    const uint32_t lane63_off = lane == 63 ? 0u : 0x80000000u;
+#endif
     const int32_t pw = (wave + WPJ - 1) % WPJ;          // producer of strip s-1
     const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
     int32_t avail = -1;                                  // producer progress seen so far
@@ -490,7 +513,9 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       };
       int32_t H, F, O, Q, E, prevH, prevEe, prevQc;  // prevEe = E[j-1] + e, prevQc = Q[j-1] + c
       uint32_t code;
+      int32_t Hpre_keep = 0;  // this row's Hpre (SVS_OPT_CARRY: lane 63's is a carry)
       auto gaps = [&](int32_t Hpre, bool inner_) {
+        Hpre_keep = Hpre;
         if (FIRST) {
           int32_t prevQ, prevE;
           strip_gaps(P, lane, j, j0, inner_, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
@@ -653,6 +678,17 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       pF = F;
       pO = O;
       pHm = prevH;
+#ifdef SVS_OPT_CARRY
+      if (!FIRST) {
+        if (write_bnd) {
+          // every lane issues the store; only lane 63's offset is in range
+          // (raw buffer, bounds-checked): no exec-mask branch per row
+          svs_i32x4 v = {Q - K.jc, E - K.je, Hpre_keep, H};
+          if (!any_alive) v = svs_i32x4{SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG};
+          __builtin_amdgcn_raw_buffer_store_b128(v, bout_rsrc, lane63_off + 16u * r, 0, 0);
+        }
+      } else
+#endif
       if (write_bnd && lane == 0) {
         *reinterpret_cast<int4*>(bout + 4ull * r) =
             any_alive ? make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH) : make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
