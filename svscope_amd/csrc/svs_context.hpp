@@ -5,6 +5,7 @@
 
 #include "threadpool.hpp"
 
+#include <algorithm>
 #include <memory>
 
 #include <cstdint>
@@ -27,16 +28,26 @@ struct SvsError : std::runtime_error {
   } while (0)
 
 // Growable device buffer (never shrinks; contents not preserved on growth).
+// Growth is geometric (at least doubling), and `hint` (e.g. the launch budget)
+// is tried first: a regrow frees the old buffer, and hipFree waits for the whole
+// device, so a buffer that regrows during a run stalls the pipeline (a 4-s stall
+// in a traced bench run, profiles/r02_v11).
 struct DeviceBuf {
   void* ptr = nullptr;
   size_t cap = 0;
-  void ensure(size_t bytes) {
+  void ensure(size_t bytes, size_t hint = 0) {
     if (bytes <= cap) return;
     if (ptr) SVS_HIP(hipFree(ptr));
     ptr = nullptr;
+    const size_t grown = std::max(bytes + bytes / 4 + 4096, 2 * cap);
     cap = 0;
-    size_t want = bytes + bytes / 4 + 4096;
-    if (hipMalloc(&ptr, want) != hipSuccess) {
+    size_t want = std::max(grown, hint);
+    if (want != grown && hipMalloc(&ptr, want) != hipSuccess) {
+      (void)hipGetLastError();
+      ptr = nullptr;
+      want = grown;
+    }
+    if (!ptr && hipMalloc(&ptr, want) != hipSuccess) {
       (void)hipGetLastError();
       want = bytes;
       if (hipMalloc(&ptr, want) != hipSuccess) {
@@ -63,8 +74,8 @@ struct PinnedBuf {
     if (bytes <= cap) return;
     if (ptr) SVS_HIP(hipHostFree(ptr));
     ptr = nullptr;
+    const size_t want = std::max(bytes + bytes / 4 + 4096, 2 * cap);  // geometric: few regrows
     cap = 0;
-    const size_t want = bytes + bytes / 4 + 4096;
     SVS_HIP(hipHostMalloc(&ptr, want, hipHostMallocDefault));
     cap = want;
   }

@@ -294,7 +294,9 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   host_ms += ms_since(th0);
 
   A.d_in.ensure(off);
-  A.d_tb.ensure(n_tb * 2 + 4096);
+  // the traceback codes dominate a launch's footprint: sized to the group's
+  // budget at the first launch, so it never regrows (and syncs) mid-run
+  A.d_tb.ensure(n_tb * 2 + 4096, ctx->device_budget / 2);
   A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096);
   A.d_aln.ensure(n_aln * 8);
   A.d_alen.ensure(nj * 12);
