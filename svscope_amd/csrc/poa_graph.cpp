@@ -210,6 +210,8 @@ void PoaGraph::export_rows(RowTables* t) const {
     t->max_preds = std::max<uint32_t>(t->max_preds, static_cast<uint32_t>(in_[node].size()));
   }
   t->pstart[V] = np;
+  t->n_rows = V;
+  t->n_edges = np;
   t->pred_slot.resize(np);
   // Row-pool slot assignment: a row lives from its computation until its last
   // successor has been computed; slot 0 holds the virtual row 0 for the whole job.
@@ -247,20 +249,30 @@ void PoaGraph::export_strip_rows(RowTables* t, const int32_t* gaps) const {
   t->pred_row.resize(E);
   t->pred_slot.resize(E);
   t->rec.resize(static_cast<size_t>(V) * kRecWords);
+  if (gaps) t->col0.resize(3 * static_cast<size_t>(V));
+  const StripDst dst{t->rec.data(), t->pstart.data(), t->pred_row.data(), t->pred_slot.data(),
+                     gaps ? t->col0.data() : nullptr};
+  export_strip_rows(t, gaps, &dst);
+}
+
+void PoaGraph::export_strip_rows(RowTables* t, const int32_t* gaps, const StripDst* dst) const {
+  const uint32_t V = num_nodes();
+  const uint32_t E = static_cast<uint32_t>(e_tail_.size());
+  t->n_rows = V;
+  t->n_edges = E;
   static thread_local std::vector<uint32_t> lds_last, slot, free_slots, dmin, dmax;
   lds_last.assign(V, 0);
   slot.resize(V);
   free_slots.clear();
-  uint32_t* __restrict__ pred_row = t->pred_row.data();
-  uint32_t* __restrict__ pstart = t->pstart.data();
+  uint32_t* __restrict__ pred_row = dst->pred_row;
+  uint32_t* __restrict__ pstart = dst->pstart;
   uint32_t* __restrict__ last = lds_last.data();
   const uint32_t* __restrict__ n2r = node_to_rank_.data();
   const uint32_t* __restrict__ etail = e_tail_.data();
   // pass 1 (ranks forward): in-edge rows (CSR), per row the last row that
   // reads it through the pool (an in-edge from the row just above does not),
   // and with gaps = {g, e, q, c} the column-0 values (fill_col0, fused)
-  if (gaps) t->col0.resize(3 * static_cast<size_t>(V));
-  int32_t* __restrict__ c0 = gaps ? t->col0.data() : nullptr;
+  int32_t* __restrict__ c0 = gaps ? dst->col0 : nullptr;
   uint32_t k = 0, max_preds = 0;
   for (uint32_t r = 0; r < V; ++r) {
     const NodeList& in = in_[rank_to_node_[r]];
@@ -293,8 +305,8 @@ void PoaGraph::export_strip_rows(RowTables* t, const int32_t* gaps) const {
   t->max_preds = max_preds;
   // pass 2 (forward): pool slots (a slot is free again after its row's last
   // reader) and row records w0, w1, w3
-  uint32_t* __restrict__ pslot = t->pred_slot.data();
-  uint32_t* __restrict__ rec = t->rec.data();
+  uint32_t* __restrict__ pslot = dst->pred_slot;
+  uint32_t* __restrict__ rec = dst->rec;
   // slot 0: virtual row 0.  Test hook: SVS_POA_TEST_WIDE_SLOTS=<n> numbers the
   // slots of graphs with >= n rows from 40 up, so that jobs with slot indices
   // past the pruning kernel's 31 liveness bits share launches with pruned ones.

@@ -26,6 +26,7 @@ struct RowTables {
   std::vector<int32_t> col0;        // per rank row: H, F, O of DP column 0 (fill_col0)
   uint32_t n_slots = 1;
   uint32_t max_preds = 0;
+  uint32_t n_rows = 0, n_edges = 0;  // set by export_strip_rows (also when it writes to a StripDst)
   // Strip-kernel tables (export_strip_rows): kRecWords words per row
   //   w0: base | sink << 8 | store << 9 | np << 10 | own pool slot << 16
   //       (kNoSlot: not stored)
@@ -121,6 +122,42 @@ constexpr uint32_t kRecWords = 4;
 constexpr uint32_t kInlinePreds = 2;
 constexpr uint32_t kNoSlot = 0xFFFF;
 
+// One strip job's tables as one contiguous block of the launch's staging
+// buffer (byte offsets from the block start; the block starts at a multiple of
+// 48 so that the 12-B column-0 triples and the 16-B records both index it):
+// col0 (12 V), records (16 V), pstart (4 (V+1)), pred_row (4 E), pred_slot
+// (4 E), then the read: one zero pad byte, the read, zeros up to ls + 64.
+struct StripBlock {
+  size_t col0, rec, pstart, pred_row, pred_slot, seq, bytes;
+};
+inline StripBlock strip_block_layout(uint32_t V, uint32_t E, uint32_t ls) {
+  StripBlock b;
+  size_t o = 0;
+  b.col0 = o;
+  o = (o + 12ull * V + 15) / 16 * 16;
+  b.rec = o;
+  o += 16ull * V;
+  b.pstart = o;
+  o += 4ull * (V + 1);
+  b.pred_row = o;
+  o += 4ull * E;
+  b.pred_slot = o;
+  o += 4ull * E;
+  b.seq = o + 1;
+  o += ls + 64;
+  b.bytes = (o + 47) / 48 * 48;
+  return b;
+}
+
+// Raw destinations for export_strip_rows (a StripBlock in pinned staging).
+struct StripDst {
+  uint32_t* rec;
+  uint32_t* pstart;
+  uint32_t* pred_row;
+  uint32_t* pred_slot;
+  int32_t* col0;
+};
+
 // Column 0 of the NW matrix depends only on the graph (gap runs down the
 // in-edges, spoa Initialize): F0 = max_p F0[p] + e (g for sources), O0 likewise
 // with q/c, H0 = max(F0, O0).  Computed once per job on the host.
@@ -129,6 +166,7 @@ void fill_col0(RowTables* t, int32_t g, int32_t e, int32_t q, int32_t c);
 class PoaGraph {
  public:
   uint32_t num_nodes() const { return static_cast<uint32_t>(base_.size()); }
+  uint32_t num_edges() const { return static_cast<uint32_t>(e_tail_.size()); }
   uint32_t num_sequences() const { return static_cast<uint32_t>(paths_.size()); }
   bool empty() const { return base_.empty(); }
 
@@ -147,6 +185,9 @@ class PoaGraph {
   void export_strip_rows(RowTables* t) const;
   // the same, also filling col0 as fill_col0(t, gaps[0..3] = g, e, q, c) does
   void export_strip_rows(RowTables* t, const int32_t* gaps) const;
+  // the same, writing the tables to dst instead of t's vectors (which are left
+  // untouched); t gets n_rows, n_edges, n_slots and max_preds
+  void export_strip_rows(RowTables* t, const int32_t* gaps, const StripDst* dst) const;
   std::vector<std::string> msa() const;
   std::string consensus(int32_t min_coverage);
 

@@ -6,6 +6,8 @@
 #include "threadpool.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <cstring>
 #include <memory>
 
 #include <cstdint>
@@ -79,6 +81,18 @@ struct PinnedBuf {
     SVS_HIP(hipHostMalloc(&ptr, want, hipHostMallocDefault));
     cap = want;
   }
+  // grows to at least `bytes`, keeping the first `keep` bytes
+  void grow_keep(size_t bytes, size_t keep) {
+    if (bytes <= cap) return;
+    void* old = ptr;
+    const size_t want = std::max(bytes + bytes / 4 + 4096, 2 * cap);
+    void* p = nullptr;
+    SVS_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
+    if (old && keep) std::memcpy(p, old, std::min(keep, cap));
+    if (old) SVS_HIP(hipHostFree(old));
+    ptr = p;
+    cap = want;
+  }
   template <class T> T* as() const { return static_cast<T*>(ptr); }
   void release() {
     if (ptr) (void)hipHostFree(ptr);
@@ -98,6 +112,13 @@ struct PoaArena {
   hipStream_t copy_stream = nullptr;  // this group's copies
   bool own = false;                   // stream is this group's, copies ride on it too
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr, h2d = nullptr;
+  // Staging of the next launch's strip tables in h_in: the fold exports each
+  // job's tables straight into a block claimed with an atomic bump (st_cur), so
+  // packing the launch copies nothing.  A new generation (st_gen) starts when
+  // the group's previous launch is done; st_peak = largest staging used so far.
+  std::atomic<size_t> st_cur{0};
+  uint32_t st_gen = 1;
+  size_t st_peak = 0;
   // s == nullptr: the group gets one stream of its own for copies and kernels,
   // so its kernel can start while the other group's launch is still draining
   // (its last, longest jobs leave most CUs idle); otherwise kernels of both

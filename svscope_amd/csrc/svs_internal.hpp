@@ -46,6 +46,12 @@ struct PoaTask {
   bool have_rate = false;
   bool retry = false;     // the current sequence's pruned run missed its bound: run it unpruned
   uint8_t prepped = 0;    // next step already readied after the fold: 1 export done, 2 complete
+  // where the strip tables of the next step are: 1 in rows' vectors, 2 in a
+  // block of the group's staging buffer (blk_off, valid while the buffer's
+  // generation is still blk_gen)
+  uint8_t rows_at = 0;
+  uint32_t blk_gen = 0;
+  uint64_t blk_off = 0;
   uint8_t n_retries = 0;
 
   std::string consensus;

@@ -103,13 +103,17 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_PRUNE_SLACK": "0", "SVS_POA_WPJ": "8"},
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_WPJ": "4"},
     {"SVS_POA_PRUNE_SLACK": "0", "SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "2"},
+    {"SVS_POA_STAGING": "vec"},
+    {"SVS_POA_STAGING": "vec", "SVS_POA_PRUNE_SLACK": "-0.3"},
 ])
 def test_kernel_variants_match_oracle(env):
     """Every POA kernel variant gives the oracle's result: row-major with 1/2/4
     waves per job, strip-major with 1/2/3/4/7/8/16 pipelined waves per job, the
     strip-major kernel with its pool in global memory, and the strip kernel's
     exact pruning off, at its tightest slack, and with a bound above the
-    optimum (every pruned job retried unpruned)."""
+    optimum (every pruned job retried unpruned; with the tables exported straight
+    into the staging buffer a retried job's block is exported again), and with
+    the tables packed from per-task vectors (SVS_POA_STAGING=vec)."""
     import os
     from svscope_amd import synth
     from svscope_amd.poa import poa_batch
