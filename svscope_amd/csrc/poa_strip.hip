@@ -45,6 +45,12 @@ namespace {
 // then 64 uint16 D = dF | dO << 8 with dF = min(H - F, tF), dO = min(H - O, tO)
 // (see pack_fo).
 constexpr int kSlotInts = 65 + 32;
+// Wide strips (see sweep_w): Hx[0..129], then 64 words of F/O pairs.
+constexpr int kSlotIntsW = 130 + 64;
+static_assert(kSlotIntsW * 4 == kStripSlotBytesWide, "wide pool slot size");
+static_assert(kSlotInts * 4 == kStripSlotBytes, "pool slot size");
+
+typedef int32_t svs_i32x2 __attribute__((ext_vector_type(2)));
 
 // F and O enter the recurrence only through F + e (against H + g) and O + c
 // (against H + q), and F, O <= H.  So F matters only while H - F <= e - g and
@@ -231,14 +237,17 @@ __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, 
 // ...; strip s reads the carries wave (w-1) mod WPJ left for strip s-1, which
 // it publishes every 8 rows through an LDS progress counter (workgroup-scope
 // release / acquire), so the waves form a row-skewed pipeline over strips.
-template <bool LDSP, int WPJ, bool PRUNE>
+template <bool LDSP, int WPJ, bool PRUNE, bool WIDE>
 // The pruning variant is held to 80 VGPRs (6 waves per SIMD; a few spills to
 // scratch in cold paths): measured faster than its natural 86 (5 waves),
 // profiles/r01_v36.  SVS_PRUNE_OCC overrides it in development builds.
 #ifndef SVS_PRUNE_OCC
 #define SVS_PRUNE_OCC 6
 #endif
-#define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? SVS_PRUNE_OCC : 1)))
+#ifndef SVS_WIDE_OCC
+#define SVS_WIDE_OCC 4
+#endif
+#define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? (WIDE ? SVS_WIDE_OCC : SVS_PRUNE_OCC) : 1)))
 __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore Parg, const uint32_t* __restrict__ rec_all,
     const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
@@ -268,16 +277,23 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   const uint32_t LS = J.ls;
   const uint32_t V = J.n_rows;
   const uint32_t VP = (V + 7) & ~7u;  // carry rows per strip, padded to whole 128-B lines
-  const int32_t nstrips = static_cast<int32_t>(LS >> 6);
+  static_assert(!WIDE || LDSP, "wide strips keep their pool in LDS");
+  // strip geometry: 64-column strips, or (WIDE) a 64-column strip 0 and then
+  // 128-column strips (sweep_w)
+  const int32_t nstrips = WIDE ? (LS <= 64 ? 1 : 1 + static_cast<int32_t>((LS - 64) >> 7))
+                               : static_cast<int32_t>(LS >> 6);
+  auto strip_of = [](int32_t j) -> int32_t { return WIDE ? (j < 64 ? 0 : 1 + ((j - 64) >> 7)) : (j >> 6); };
+  auto lane_of = [](int32_t j) -> int32_t { return WIDE && j >= 64 ? ((j - 64) & 127) >> 1 : (j & 63); };
+  constexpr int kStride = WIDE ? kSlotIntsW : kSlotInts;
   const uint32_t nslot = LDSP ? lds_slots : J.n_slots;
   int32_t* __restrict__ pool;  // this wave's pool: nslot x {H, F, O} x 64, then nslot boundary H
-  if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * kSlotInts;
+  if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * kStride;
   else pool = gpool + J.pool_off + static_cast<uint64_t>(wave) * ((nslot * kSlotInts + 63) / 64 * 64);
   uint16_t* __restrict__ tbj = tb + J.tb_off;
   const uint32_t* __restrict__ rec = rec_all + static_cast<uint64_t>(J.rec_off) * kRecWords;
   const uint32_t* __restrict__ rps = row_pstart + J.pstart_off;
   const uint32_t* __restrict__ prow = pred_row + J.pred_off;
-  const uint32_t* __restrict__ pslot = pred_slot + J.pred_off;
+  const uint32_t* __restrict__ pslot = pred_slot + J.pslot_off;
   const int32_t* __restrict__ rc0 = col0 + 3ull * J.row_off;
   const uint8_t* __restrict__ seq = seqs + J.seq_off;
   int32_t* __restrict__ bnd = bnd_all + J.bnd_off;
@@ -339,7 +355,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
     int32_t avail = -1;                                  // producer progress seen so far
     const bool write_bnd = s + 1 < nstrips;
-    const bool owns_L = (L >> 6) == s;
+    const bool owns_L = strip_of(L) == s;
     // pruning state of this strip: slot liveness bits (slots < 64, host-checked;
     // slot 0 = the virtual row 0, alive when row0_h + m (L - j) reaches lb at
     // some column j0-1 .. j0+63, i.e. at j0-1: it decreases along j), and the
@@ -454,7 +470,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         if (!live) {
           // no alive input: the row's cells are all dead, never computed
           if (store) {
-            int32_t* q = pool + own * kSlotInts;
+            int32_t* q = pool + own * kStride;
             q[lane + 1] = SVS_VNEG;
             q[lane] = SVS_VNEG;
             reinterpret_cast<uint16_t*>(q + 65)[lane] = 0;  // F = O = H = VNEG
@@ -503,7 +519,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         if (ps == kNoSlot) {
           hp = pH; fp = pF; op = pO; hpm = pHm;
         } else {
-          const int32_t* q = pool + ps * kSlotInts;
+          const int32_t* q = pool + ps * kStride;
           hpm = __builtin_nontemporal_load(q + lane);
           hp = __builtin_nontemporal_load(q + lane + 1);
           const uint32_t dd = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(q + 65) + lane);
@@ -669,7 +685,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       if (store) {
         // Hx[l+1] = H[l], then Hx[l] = prevH[l] (= H[l-1], lane 0: H[j0-1]);
         // the two full-wave writes agree wherever they overlap
-        int32_t* q = pool + own * kSlotInts;
+        int32_t* q = pool + own * kStride;
         q[lane + 1] = H;
         q[lane] = prevH;
         reinterpret_cast<uint16_t*>(q + 65)[lane] = static_cast<uint16_t>(pack_fo(H, F, O, tF, tO));
@@ -745,7 +761,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       }
       // rows passed over left stale pool slots: every slot but the virtual row's to VNEG
       for (uint32_t p = 1; p < nslot; ++p) {
-        int32_t* q = pool + p * kSlotInts;
+        int32_t* q = pool + p * kStride;
         q[lane + 1] = SVS_VNEG;
         if (lane == 0) q[0] = SVS_VNEG;
         reinterpret_cast<uint16_t*>(q + 65)[lane] = 0;
@@ -796,6 +812,408 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     __builtin_amdgcn_wave_barrier();
   };
 
+  // Wide strips (WIDE; every strip after the first): strip s >= 1 spans the
+  // 128 columns j0 .. j0+127, j0 = 64 + 128 (s-1), and lane l owns the column
+  // pair ja = j0 + 2l (element a) and jb = ja + 1 (element b).  A row then
+  // costs one record decode, one branch and one set of scalar bookkeeping per
+  // 128 cells instead of per 64; the horizontal-gap scans run over the 64
+  // per-lane pair maxima and are completed per element (gaps_w).  The values
+  // and traceback codes are those of sweep's: the same recurrence, the same
+  // tests.  Pool slot (kSlotIntsW words): Hx[i] = H at column j0 - 2 + i for
+  // i = 1 .. 129 (a lane's pair at the even index 2l + 2: one 8-B LDS access),
+  // then 64 words of F/O pairs (pack_fo of a | pack_fo of b << 16).
+  auto sweep_w = [&](int32_t s) {
+    const int32_t j0 = 64 + ((s - 1) << 7);
+    const int32_t ja = j0 + 2 * lane, jb = ja + 1;
+    const uint8_t rca = seq[ja - 1], rcb = seq[ja];
+    const int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s - 1) * VP * 4;
+    int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
+    const int32_t pw = (wave + WPJ - 1) % WPJ;
+    const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
+    int32_t avail = -1;
+    const bool write_bnd = s + 1 < nstrips;
+    const bool owns_L = strip_of(L) == s;
+    const bool L_b = ((L - j0) & 1) != 0;
+    constexpr uint32_t kRegBit = 1u << 31;
+    uint32_t alive = (!prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb) ? 1u : 0u;
+    const int32_t rra = L - ja, rrb = L - jb;
+    const int32_t mra = P.m * rra, mrb = P.m * rrb;
+    auto ub_of = [&](uint32_t w2, int32_t rr, int32_t mr) -> int32_t {
+      const int32_t dmin = static_cast<int32_t>(w2 & 0xFFFFu), dmax = static_cast<int32_t>(w2 >> 16);
+      const int32_t d = min(imax(rr, dmin), dmax) - rr;
+      return mr + d * (d >= 0 ? cg : P.m - cg);
+    };
+    // lane constants of both elements (strip_gaps_nf's, per column)
+    const int32_t qjc_a = P.q - ja * P.c, qjc_b = qjc_a - P.c;
+    const int32_t k1_a = (P.g - ja * P.e) - qjc_a, k1_b = (P.g - jb * P.e) - qjc_b;
+    const int32_t k2_a = (ja - 1) * P.c + P.g - ja * P.e, k2_b = ja * P.c + P.g - jb * P.e;
+    const int32_t jc_a = ja * P.c, jc_b = jb * P.c, je_a = ja * P.e, je_b = jb * P.e;
+    const int32_t ve = P.e, vc = P.c;
+    // virtual row 0 in slot 0
+    {
+      const int32_t ha = row0_h(P, ja), hb = row0_h(P, jb);
+      *reinterpret_cast<svs_i32x2*>(pool + 2 * lane + 2) = svs_i32x2{ha, hb};
+      pool[2 * lane + 1] = row0_h(P, ja - 1);
+      reinterpret_cast<uint32_t*>(pool + 130)[lane] =
+          pack_fo(ha, SVS_NEG_INF, SVS_NEG_INF, tF, tO) | (pack_fo(hb, SVS_NEG_INF, SVS_NEG_INF, tF, tO) << 16);
+    }
+    __builtin_amdgcn_wave_barrier();
+
+    auto fetch = [&](RowIn& d, uint32_t r) {
+      const uint32_t rr = r < V ? r : V - 1;
+      const uint32_t* w = rec + static_cast<uint64_t>(rr) * kRecWords;
+      d.w0 = w[0];
+      d.w1 = w[1];
+      if constexpr (PRUNE) {
+        d.w2 = w[2];
+        d.w3 = w[3];
+      }
+      if (WPJ > 1) {
+        const int32_t need = need0 + static_cast<int32_t>(rr) + 1;
+        if (avail < need) avail = strip_wait_ge(&prog[pw], need, &s_err);
+      }
+      const int4 v = *reinterpret_cast<const int4*>(bin + 4ull * rr);
+      d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
+    };
+
+    // the row just above (registers): H, F, O of both elements and H[ja - 1]
+    int32_t pHa = 0, pHb = 0, pFa = 0, pFb = 0, pOa = 0, pOb = 0, pHma = 0;
+    struct ColW {
+      int32_t Q, E, H, prevH, prevEe, prevQc;  // prevEe = E[j-1] + e, prevQc = Q[j-1] + c
+    };
+    // strip_gaps_nf over 128 columns: the scans of P1 and of u (P2's first
+    // term) run over the lane maxima max(a, b); a lane's element a then adds the
+    // exclusive prefix of the lanes before it, element b is the inclusive one.
+    // P2's second term P1[j-1] + k2[j] reads the exclusive prefix for a and
+    // element a's own prefix for b.  The strip's first column (lane 0, a) has
+    // no P1[j0-1] in the strip (exclusive prefix VNEG), and its T2 term equals
+    // T1 (cQ = (j0-1) c + run1), so it needs no lane-0 special case.
+    auto gaps_w = [&](int32_t Hpa, int32_t Hpb, StripCarry& cr, ColW& A_, ColW& B_) {
+      const int32_t p1a = shr1_add(cr.cHpre + qjc_a, Hpb, qjc_a);  // Hpre[ja-1] + q - ja c
+      const int32_t p1b = Hpa + qjc_b;
+      const int32_t ua = p1a + k1_a, ub = p1b + k1_b;
+      int32_t w1 = imax(p1a, p1b), w2 = imax(ua, ub);
+      wave_prefix_max2(w1, w2);
+      const int32_t x1 = wave_shr1(w1, SVS_VNEG, lane), x2 = wave_shr1(w2, SVS_VNEG, lane);
+      const int32_t s1a = imax(x1, p1a);
+      const int32_t p2a = imax(imax(x2, ua), x1 + k2_a);
+      const int32_t p2b = imax(w2, s1a + k2_b);
+      const int32_t T1 = cr.cQ + P.g - j0 * P.e;
+      const int32_t r2 = imax(cr.run2, T1);
+      A_.Q = jc_a + imax(s1a, cr.run1);
+      B_.Q = jc_b + imax(w1, cr.run1);
+      A_.E = je_a + imax(imax(p2a, r2), cr.run1 + k2_a);
+      B_.E = je_b + imax(imax(p2b, r2), cr.run1 + k2_b);
+      A_.H = imax(Hpa, imax(A_.E, A_.Q));
+      B_.H = imax(Hpb, imax(B_.E, B_.Q));
+      A_.prevH = wave_shr1(B_.H, cr.cH, lane);
+      B_.prevH = A_.H;
+      A_.prevEe = shr1_add(cr.cE + P.e, B_.E, ve);
+      B_.prevEe = A_.E + P.e;
+      A_.prevQc = shr1_add(cr.cQ + P.c, B_.Q, vc);
+      B_.prevQc = A_.Q + P.c;
+      // carries into strip s+1, from lane 63's element b (column jl)
+      const int32_t jl = j0 + 127;
+      const int32_t p1l = readlane63(w1), p2l = readlane63(p2b), hl = readlane63(Hpb);
+      const int32_t T2l = cr.run1 + (jl - 1) * P.c + P.g - jl * P.e;
+      cr.run2 = imax(imax(cr.run2, p2l), imax(T1, T2l));
+      cr.run1 = imax(cr.run1, p1l);
+      cr.cQ = jl * P.c + cr.run1;
+      cr.cE = jl * P.e + cr.run2;
+      cr.cHpre = hl;
+      cr.cH = imax(hl, imax(cr.cE, cr.cQ));
+    };
+    // traceback code of a cell with at most one in-edge (sweep's np <= 1 tests)
+    auto code1 = [&](const ColW& c, int32_t D, int32_t F, int32_t O, int32_t hp, int32_t fp, int32_t op,
+                     uint32_t np) -> uint32_t {
+      const bool dg = c.H == D;
+      const bool up = c.H == imax(F, O);
+      const bool ua = c.H == fp + P.e, ub = c.H == hp + P.g, uc = c.H == op + P.c;
+      const bool lf = c.H == imax(c.E, c.Q);
+      const bool la = c.H == c.prevEe, lg = c.H == c.prevH + P.g, lc = c.H == c.prevQc;
+      const bool lbit = c.prevH + P.g == c.E || c.prevH + P.q == c.Q;
+      const bool va = F == hp + P.g, vb = F == fp + P.e, vq = O == hp + P.q;
+      const uint32_t upc = (ua || (!ub && uc)) ? 5u : 1u;
+      const uint32_t lfc = (la || (!lg && lc)) ? 6u : 2u;
+      uint32_t code = dg ? 0u : (up ? upc : (lf ? lfc : 3u));
+      code |= lbit ? 0x100u : 0u;
+      if (np != 0) code |= (va || (!vb && vq)) ? 0x200u : 0u;
+      else code |= 31u << 10;
+      return code;
+    };
+    // two in-edges (sweep's np == 2 tests)
+    auto code2 = [&](const ColW& c, int32_t F, int32_t O, int32_t F0k, int32_t O0k, int32_t F1k, int32_t O1k,
+                     int32_t D0, int32_t D1, int32_t hp0, int32_t fp0, int32_t op0, int32_t hp1, int32_t fp1,
+                     int32_t op1) -> uint32_t {
+      const bool up0 = c.H == imax(F0k, O0k), up1 = c.H == imax(F1k, O1k);
+      const int32_t hpu = up0 ? hp0 : hp1, fpu = up0 ? fp0 : fp1, opu = up0 ? op0 : op1;
+      const bool ua = c.H == fpu + P.e, ub = c.H == hpu + P.g, uc = c.H == opu + P.c;
+      const bool ch0 = F == F0k || O == O0k;
+      const int32_t hpc = ch0 ? hp0 : hp1, fpc = ch0 ? fp0 : fp1;
+      const bool va = F == hpc + P.g, vb = F == fpc + P.e, vq = O == hpc + P.q;
+      const bool lf = c.H == imax(c.E, c.Q);
+      const bool la = c.H == c.prevEe, lg = c.H == c.prevH + P.g, lc = c.H == c.prevQc;
+      const bool lbit = c.prevH + P.g == c.E || c.prevH + P.q == c.Q;
+      const uint32_t upc = ((ua || (!ub && uc)) ? 5u : 1u) | (up0 ? 0u : 8u);
+      const uint32_t lfc = (la || (!lg && lc)) ? 6u : 2u;
+      uint32_t code = c.H == D0 ? 0u : (c.H == D1 ? 8u : (up0 || up1 ? upc : (lf ? lfc : 3u)));
+      code |= lbit ? 0x100u : 0u;
+      code |= ((va || (!vb && vq)) ? 0x200u : 0u) | (ch0 ? 0u : (1u << 10));
+      return code;
+    };
+
+    auto step = [&](uint32_t r, const RowIn& d) {
+      const uint32_t w0 = __builtin_amdgcn_readfirstlane(d.w0);
+      const uint32_t nb = w0 & 0xFFu;
+      const bool sink = (w0 >> 8) & 1u;
+      const bool store = (w0 >> 9) & 1u;
+      const uint32_t np = (w0 >> 10) & 31u;
+      const uint32_t own = w0 >> 16;
+      auto slot_alive = [&](uint32_t ps) -> bool {
+        if (ps == kNoSlot) return (alive >> 31) != 0;
+        return ps >= 31u || ((alive >> ps) & 1u) != 0;
+      };
+      const uint32_t own_bit = (store && own < 31u) ? 1u << own : 0u;
+      auto publish = [&]() {
+        if (WPJ > 1 && write_bnd && ((r & 7u) == 7u || r + 1 == V) && lane == 0)
+          __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
+                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
+      const int32_t cH_in = __builtin_amdgcn_readfirstlane(d.b3);
+      if (prune) {
+        bool live = cH_in > SVS_VNEG / 2;
+        if (!live) {
+          const uint32_t wp = __builtin_amdgcn_readfirstlane(d.w1);
+          live = slot_alive(wp & 0xFFFFu) || (np >= 2 && slot_alive(wp >> 16));
+          if (!live && np > kInlinePreds) {
+            const uint32_t* __restrict__ spill = pslot + rps[r];
+            for (uint32_t k = kInlinePreds; k < np && !live; ++k)
+              live = slot_alive(__builtin_amdgcn_readfirstlane(spill[k]));
+          }
+        }
+        if (!live) {
+          if (store) {
+            int32_t* q = pool + own * kSlotIntsW;
+            *reinterpret_cast<svs_i32x2*>(q + 2 * lane + 2) = svs_i32x2{SVS_VNEG, SVS_VNEG};
+            q[2 * lane + 1] = SVS_VNEG;
+            reinterpret_cast<uint32_t*>(q + 130)[lane] = 0;  // F = O = H = VNEG
+          }
+          alive &= ~(__builtin_amdgcn_readfirstlane(d.w3) | own_bit | kRegBit);
+          pHa = pHb = pFa = pFb = pOa = pOb = pHma = SVS_VNEG;
+          if (write_bnd && lane == 0)
+            *reinterpret_cast<int4*>(bout + 4ull * r) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
+          publish();
+          return;
+        }
+      }
+      if constexpr (PRUNE) rows_done += 2;  // in 64-column strip rows
+      uint2 w2w3 = make_uint2(0, 0);
+      if constexpr (PRUNE)
+        w2w3 = make_uint2(__builtin_amdgcn_readfirstlane(d.w2), __builtin_amdgcn_readfirstlane(d.w3));
+      StripCarry cr;
+      {
+        const int32_t jl = j0 - 1;
+        cr.run1 = __builtin_amdgcn_readfirstlane(d.b0);
+        cr.run2 = __builtin_amdgcn_readfirstlane(d.b1);
+        cr.cHpre = __builtin_amdgcn_readfirstlane(d.b2);
+        cr.cH = cH_in;
+        cr.cQ = jl * P.c + cr.run1;
+        cr.cE = jl * P.e + cr.run2;
+      }
+      const int32_t mca = rca == nb ? P.m : P.n, mcb = rcb == nb ? P.m : P.n;
+      // in-edge k: H, F, O at ja, jb and H at ja - 1 (H at jb - 1 is H at ja)
+      auto pred_w = [&](uint32_t ps, int32_t& hpa, int32_t& hpb, int32_t& fpa, int32_t& fpb, int32_t& opa,
+                        int32_t& opb, int32_t& hma) {
+        if (ps == kNoSlot) {
+          hpa = pHa; hpb = pHb; fpa = pFa; fpb = pFb; opa = pOa; opb = pOb; hma = pHma;
+        } else {
+          const int32_t* q = pool + ps * kSlotIntsW;
+          const svs_i32x2 hh = __builtin_nontemporal_load(reinterpret_cast<const svs_i32x2*>(q + 2 * lane + 2));
+          hma = __builtin_nontemporal_load(q + 2 * lane + 1);
+          const uint32_t dd = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(q + 130) + lane);
+          hpa = hh.x;
+          hpb = hh.y;
+          fpa = hpa - static_cast<int32_t>(dd & 0xFFu);
+          opa = hpa - static_cast<int32_t>((dd >> 8) & 0xFFu);
+          fpb = hpb - static_cast<int32_t>((dd >> 16) & 0xFFu);
+          opb = hpb - static_cast<int32_t>(dd >> 24);
+        }
+      };
+      ColW A_, B_;
+      int32_t Fa, Fb, Oa, Ob;
+      uint32_t ca, cb;
+      if (np <= 1) {
+        const uint32_t ps = __builtin_amdgcn_readfirstlane(d.w1) & 0xFFFFu;  // np == 0: slot 0 (virtual row)
+        int32_t hpa, hpb, fpa, fpb, opa, opb, hma;
+        pred_w(ps, hpa, hpb, fpa, fpb, opa, opb, hma);
+        Fa = imax(hpa + P.g, fpa + P.e);
+        Oa = imax(hpa + P.q, opa + P.c);
+        Fb = imax(hpb + P.g, fpb + P.e);
+        Ob = imax(hpb + P.q, opb + P.c);
+        const int32_t Da = hma + mca, Db = hpa + mcb;
+        gaps_w(imax(Da, imax(Fa, Oa)), imax(Db, imax(Fb, Ob)), cr, A_, B_);
+        ca = code1(A_, Da, Fa, Oa, hpa, fpa, opa, np);
+        cb = code1(B_, Db, Fb, Ob, hpb, fpb, opb, np);
+      } else if (np == 2) {
+        const uint32_t wp = __builtin_amdgcn_readfirstlane(d.w1);
+        int32_t hp0a, hp0b, fp0a, fp0b, op0a, op0b, hm0a, hp1a, hp1b, fp1a, fp1b, op1a, op1b, hm1a;
+        pred_w(wp & 0xFFFFu, hp0a, hp0b, fp0a, fp0b, op0a, op0b, hm0a);
+        pred_w(wp >> 16, hp1a, hp1b, fp1a, fp1b, op1a, op1b, hm1a);
+        const int32_t F0a = imax(hp0a + P.g, fp0a + P.e), O0a = imax(hp0a + P.q, op0a + P.c);
+        const int32_t F1a = imax(hp1a + P.g, fp1a + P.e), O1a = imax(hp1a + P.q, op1a + P.c);
+        const int32_t F0b = imax(hp0b + P.g, fp0b + P.e), O0b = imax(hp0b + P.q, op0b + P.c);
+        const int32_t F1b = imax(hp1b + P.g, fp1b + P.e), O1b = imax(hp1b + P.q, op1b + P.c);
+        Fa = imax(F0a, F1a);
+        Oa = imax(O0a, O1a);
+        Fb = imax(F0b, F1b);
+        Ob = imax(O0b, O1b);
+        const int32_t D0a = hm0a + mca, D1a = hm1a + mca, D0b = hp0a + mcb, D1b = hp1a + mcb;
+        gaps_w(imax(imax(D0a, D1a), imax(Fa, Oa)), imax(imax(D0b, D1b), imax(Fb, Ob)), cr, A_, B_);
+        ca = code2(A_, Fa, Oa, F0a, O0a, F1a, O1a, D0a, D1a, hp0a, fp0a, op0a, hp1a, fp1a, op1a);
+        cb = code2(B_, Fb, Ob, F0b, O0b, F1b, O1b, D0b, D1b, hp0b, fp0b, op0b, hp1b, fp1b, op1b);
+      } else {
+        const uint32_t* __restrict__ spill = pslot + rps[r];
+        Fa = Fb = Oa = Ob = SVS_VNEG;
+        int32_t Hda = SVS_VNEG, Hdb = SVS_VNEG;
+        for (uint32_t k = 0; k < np; ++k) {
+          int32_t hpa, hpb, fpa, fpb, opa, opb, hma;
+          pred_w(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hpa, hpb, fpa, fpb, opa, opb, hma);
+          Fa = imax(Fa, imax(hpa + P.g, fpa + P.e));
+          Oa = imax(Oa, imax(hpa + P.q, opa + P.c));
+          Fb = imax(Fb, imax(hpb + P.g, fpb + P.e));
+          Ob = imax(Ob, imax(hpb + P.q, opb + P.c));
+          Hda = imax(Hda, hma + mca);
+          Hdb = imax(Hdb, hpa + mcb);
+        }
+        gaps_w(imax(Hda, imax(Fa, Oa)), imax(Hdb, imax(Fb, Ob)), cr, A_, B_);
+        uint32_t dka = 31, uka = 31, uea = 0, cka = 31, csa = 0;
+        uint32_t dkb = 31, ukb = 31, ueb = 0, ckb = 31, csb = 0;
+        for (uint32_t k = 0; k < np; ++k) {
+          int32_t hpa, hpb, fpa, fpb, opa, opb, hma;
+          pred_w(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hpa, hpb, fpa, fpb, opa, opb, hma);
+          auto tests = [&](const ColW& c, int32_t F, int32_t O, int32_t hp, int32_t fp, int32_t op, int32_t D,
+                           uint32_t& dk, uint32_t& uk, uint32_t& ue, uint32_t& ck, uint32_t& cs) {
+            if (dk == 31 && c.H == D) dk = k;
+            if (uk == 31) {
+              const bool a = c.H == fp + P.e, b = c.H == hp + P.g, cc = c.H == op + P.c, dd = c.H == hp + P.q;
+              if (a || b || cc || dd) { uk = k; ue = (a || (!b && cc)) ? 1u : 0u; }
+            }
+            if (ck == 31) {
+              const bool a = F == hp + P.g, b = F == fp + P.e, cc = O == hp + P.q, dd = O == op + P.c;
+              if (a || b || cc || dd) { ck = k; cs = (a || (!b && cc)) ? 1u : 0u; }
+            }
+          };
+          tests(A_, Fa, Oa, hpa, fpa, opa, hma + mca, dka, uka, uea, cka, csa);
+          tests(B_, Fb, Ob, hpb, fpb, opb, hpa + mcb, dkb, ukb, ueb, ckb, csb);
+        }
+        auto left = [&](const ColW& c, uint32_t dk, uint32_t uk, uint32_t ue, uint32_t ck, uint32_t cs) {
+          const bool la = c.H == c.prevEe, lg = c.H == c.prevH + P.g;
+          const bool lc = c.H == c.prevQc, ld = c.H == c.prevH + P.q;
+          const bool lbit = c.prevH + P.g == c.E || c.prevH + P.q == c.Q;
+          return assemble_code(dk, uk, ue, la || lg || lc || ld, la || (!lg && lc), lbit, ck, cs);
+        };
+        ca = left(A_, dka, uka, uea, cka, csa);
+        cb = left(B_, dkb, ukb, ueb, ckb, csb);
+      }
+      *reinterpret_cast<uint32_t*>(tbj + static_cast<uint64_t>(r) * LS + ja) = (ca & 0xFFFFu) | (cb << 16);
+      bool any_alive = true;
+      if (prune) {
+        const int32_t uba = ub_of(w2w3.x, rra, mra), ubb = ub_of(w2w3.x, rrb, mrb);
+        any_alive = __builtin_amdgcn_ballot_w64((rra >= 0 && A_.H + uba >= lb) || (rrb >= 0 && B_.H + ubb >= lb)) != 0;
+        const bool out_alive = any_alive || cH_in > SVS_VNEG / 2;
+        const uint32_t ob = own_bit | kRegBit;
+        alive = ((alive & ~ob) | (out_alive ? ob : 0u)) & ~w2w3.y;
+      }
+      if (store) {
+        int32_t* q = pool + own * kSlotIntsW;
+        *reinterpret_cast<svs_i32x2*>(q + 2 * lane + 2) = svs_i32x2{A_.H, B_.H};
+        q[2 * lane + 1] = A_.prevH;
+        reinterpret_cast<uint32_t*>(q + 130)[lane] = pack_fo(A_.H, Fa, Oa, tF, tO) | (pack_fo(B_.H, Fb, Ob, tF, tO) << 16);
+      }
+      pHa = A_.H;
+      pHb = B_.H;
+      pFa = Fa;
+      pFb = Fb;
+      pOa = Oa;
+      pOb = Ob;
+      pHma = A_.prevH;
+      if (write_bnd && lane == 0) {
+        *reinterpret_cast<int4*>(bout + 4ull * r) =
+            any_alive ? make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH) : make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
+      }
+      publish();
+      if (sink && owns_L) {
+        const int32_t HL = L_b ? B_.H : A_.H;
+        if ((ja == L || jb == L) && HL > best) { best = HL; best_row = static_cast<int32_t>(r) + 1; }
+      }
+    };
+
+    // sweep's fast_forward for a strip after the first
+    auto fast_forward = [&](uint32_t r) -> uint32_t {
+      while (r < V) {
+        uint32_t lim = min(64u, V - r);
+        if (WPJ > 1) {
+          const int32_t least = need0 + static_cast<int32_t>(min(V, r + 8));
+          if (avail < least) avail = strip_wait_ge(&prog[pw], least, &s_err);
+          lim = min(lim, static_cast<uint32_t>(min(static_cast<int32_t>(V), avail - need0)) - r);
+        }
+        const uint32_t rr = r + static_cast<uint32_t>(lane);
+        const bool in = static_cast<uint32_t>(lane) < lim;
+        bool cand = false;
+        if (in) cand = __builtin_nontemporal_load(bin + 4ull * rr + 3) > SVS_VNEG / 2;
+        if ((alive & 1u) && in) cand = cand || ((rec[static_cast<uint64_t>(rr) * kRecWords] >> 10) & 31u) == 0;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
+        const uint32_t n = m ? static_cast<uint32_t>(__builtin_ctzll(m)) : lim;
+        if (write_bnd && static_cast<uint32_t>(lane) < n)
+          *reinterpret_cast<int4*>(bout + 4ull * rr) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
+        r += n;
+        if (m) break;
+      }
+      for (uint32_t p = 1; p < nslot; ++p) {
+        int32_t* q = pool + p * kSlotIntsW;
+        *reinterpret_cast<svs_i32x2*>(q + 2 * lane + 2) = svs_i32x2{SVS_VNEG, SVS_VNEG};
+        q[2 * lane + 1] = SVS_VNEG;
+        reinterpret_cast<uint32_t*>(q + 130)[lane] = 0;
+      }
+      pHa = pHb = pFa = pFb = pOa = pOb = pHma = SVS_VNEG;
+      if (WPJ > 1 && write_bnd && lane == 0) {
+        const uint32_t done = r >= V ? V : (r & ~7u);
+        __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(done),
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      return r;
+    };
+    auto dead_strip = [&]() { return (alive & ~1u) == 0; };
+
+    RowIn A, B;
+    uint32_t r = 0;
+    if (prune) r = fast_forward(0);
+    fetch(A, r);
+    fetch(B, r + 1);
+    while (r < V) {
+      step(r, A);
+      if (prune && dead_strip()) {
+        r = fast_forward(r + 1);
+        fetch(A, r);
+        fetch(B, r + 1);
+        continue;
+      }
+      fetch(A, r + 2);
+      if (r + 1 >= V) break;
+      step(r + 1, B);
+      if (prune && dead_strip()) {
+        r = fast_forward(r + 2);
+        fetch(A, r);
+        fetch(B, r + 1);
+        continue;
+      }
+      fetch(B, r + 3);
+      r += 2;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  };
+
   if (WPJ > 1) {
     if (lane == 0) {
       prog[wave] = -1;
@@ -808,6 +1226,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     using FalseT = std::integral_constant<bool, false>;
     for (int32_t s = wave; s < nstrips; s += WPJ) {
       if (s == 0) sweep(TrueT{}, 0);
+      else if constexpr (WIDE) sweep_w(s);
       else sweep(FalseT{}, s);
     }
   }
@@ -824,12 +1243,12 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
 
   // the owner of column L's strip holds the sink maximum; every wave's
   // traceback-code stores must be visible to wave 0's lane 0
-  best_row = __shfl(best_row, L & 63, 64);
-  best = __shfl(best, L & 63, 64);
+  best_row = __shfl(best_row, lane_of(L), 64);
+  best = __shfl(best, lane_of(L), 64);
   if (WPJ > 1) {
     if (lane == 0) {
       s_rows[wave] = rows_done;
-      if (((L >> 6) % WPJ) == wave) {
+      if ((strip_of(L) % WPJ) == wave) {
         s_brow[wave] = best_row;
         s_best[wave] = best;
       }
@@ -838,8 +1257,8 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     if (wave != 0) return;
-    best_row = s_brow[(L >> 6) % WPJ];
-    best = s_best[(L >> 6) % WPJ];
+    best_row = s_brow[strip_of(L) % WPJ];
+    best = s_best[strip_of(L) % WPJ];
     rows_done = 0;
     for (int w = 0; w < WPJ; ++w) rows_done += s_rows[w];
     if (s_err) {
@@ -858,7 +1277,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   // one or two per step.
   best_row = __builtin_amdgcn_readfirstlane(best_row);
   best = __builtin_amdgcn_readfirstlane(best);
-  if constexpr (!PRUNE) rows_done = V * static_cast<uint32_t>(nstrips);
+  if constexpr (!PRUNE) rows_done = V * (LS >> 6);  // in 64-column strip rows
   if (lane == 0) {
     aln_len[n_jobs + job_id] = best;
     aln_len[2 * n_jobs + job_id] = static_cast<int32_t>(rows_done);
@@ -925,15 +1344,15 @@ namespace {
 template <bool LP>
 const void* strip_kernel_ptr(int w) {
   switch (w) {
-    case 16: return LP ? reinterpret_cast<const void*>(&poa_strip_kernel<true, 16, false>) : nullptr;
-    case 8: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 8, false>);
-    case 7: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 7, false>);
-    case 6: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 6, false>);
-    case 5: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 5, false>);
-    case 4: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 4, false>);
-    case 3: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 3, false>);
-    case 2: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 2, false>);
-    default: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 1, false>);
+    case 16: return LP ? reinterpret_cast<const void*>(&poa_strip_kernel<true, 16, false, false>) : nullptr;
+    case 8: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 8, false, false>);
+    case 7: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 7, false, false>);
+    case 6: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 6, false, false>);
+    case 5: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 5, false, false>);
+    case 4: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 4, false, false>);
+    case 3: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 3, false, false>);
+    case 2: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 2, false, false>);
+    default: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 1, false, false>);
   }
 }
 
@@ -989,20 +1408,37 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   if (a.n_jobs <= 0) return hipSuccess;
   const int w = a.waves_per_job;
   const bool lds_pool = a.lds_slots > 0;
-  const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * kStripSlotBytes : 0;
-#define SVS_STRIP2(LP, W, PR)                                                                                     \
-  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, a.n_jobs, \
-                     a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.bnd,     \
-                     a.pool, a.aln, a.aln_len, a.lds_slots)
-#define SVS_STRIP(LP, W)          \
-  do {                            \
-    if (a.prune) {                \
-      SVS_STRIP2(LP, W, true);    \
-    } else {                      \
-      SVS_STRIP2(LP, W, false);   \
-    }                             \
+  if (a.wide && !lds_pool) return hipErrorInvalidValue;  // wide strips keep their pool in LDS
+  const size_t slot_bytes = a.wide ? kStripSlotBytesWide : kStripSlotBytes;
+  const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * slot_bytes : 0;
+#define SVS_STRIP3(LP, W, PR, WD)                                                                                  \
+  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR, WD>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs,         \
+                     a.n_jobs, a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, \
+                     a.bnd, a.pool, a.aln, a.aln_len, a.lds_slots)
+#define SVS_STRIP(LP, W)                 \
+  do {                                   \
+    if (a.prune) {                       \
+      SVS_STRIP3(LP, W, true, false);    \
+    } else {                             \
+      SVS_STRIP3(LP, W, false, false);   \
+    }                                    \
   } while (0)
-  if (lds_pool) {
+#define SVS_STRIPW(W)                    \
+  do {                                   \
+    if (a.prune) {                       \
+      SVS_STRIP3(true, W, true, true);   \
+    } else {                             \
+      SVS_STRIP3(true, W, false, true);  \
+    }                                    \
+  } while (0)
+  if (a.wide) {
+    // wide strips: 1, 2, 4, 8 or 16 waves per job (the host's choices)
+    if (w >= 16) SVS_STRIPW(16);
+    else if (w >= 8) SVS_STRIPW(8);
+    else if (w >= 4) SVS_STRIPW(4);
+    else if (w >= 2) SVS_STRIPW(2);
+    else SVS_STRIPW(1);
+  } else if (lds_pool) {
     switch (w) {
       case 16: SVS_STRIP(true, 16); break;
       case 8: SVS_STRIP(true, 8); break;
@@ -1020,8 +1456,9 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
     else if (w >= 2) SVS_STRIP(false, 2);
     else SVS_STRIP(false, 1);
   }
+#undef SVS_STRIPW
 #undef SVS_STRIP
-#undef SVS_STRIP2
+#undef SVS_STRIP3
   return hipGetLastError();
 }
 

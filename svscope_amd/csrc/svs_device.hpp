@@ -26,6 +26,7 @@ struct PoaJob {
   uint64_t bnd_off;   // strip kernel: int32 strip-boundary carries, 2 x n_rows x 4
   uint32_t rec_off;   // strip kernel: row records (kRecWords uint32 per row), in rows
   int32_t lb;         // strip kernel: pruning bound (kNoPrune = off), see poa_strip.hip
+  uint32_t pslot_off;  // strip kernel: base of this job's pred_slot entries
 };
 
 // PoaJob::lb value that turns the strip kernel's exact pruning off.
@@ -59,11 +60,19 @@ struct PoaLaunch {
   int32_t* bnd;          // strip-boundary carries
   uint32_t lds_slots;    // pool slots per wave held in LDS (max n_slots of the launch)
   bool prune;            // some job has a pruning bound: the pruning kernel variant
+  bool wide;             // 128-column strips after strip 0 (PoaJob::ls from strip_ls_wide)
 };
+
+// Row stride of a strip job with wide strips: 64 + a multiple of 128, >= len + 1.
+inline uint32_t strip_ls_wide(uint32_t len) {
+  return len + 1 <= 64 ? 64u : 64u + (len + 1 - 64 + 127) / 128 * 128;
+}
 
 // Strip-major kernel: LDS bytes per pool slot (65 int32 H incl. the boundary
 // column + 64 packed uint16 F/O distances), and the largest pool kept in LDS.
 constexpr uint32_t kStripSlotBytes = 65 * 4 + 64 * 2;
+// the same for wide strips (128 columns, two per lane)
+constexpr uint32_t kStripSlotBytesWide = 130 * 4 + 128 * 2;
 constexpr uint32_t kStripMaxLdsSlots = 80;
 // LDS a strip workgroup's pools may take (160 KiB per CU on gfx950, less the
 // kernel's own few static words)

@@ -175,8 +175,51 @@ struct KernelEnv {
   bool global_pool = strip_pool_forced_global();
 };
 
+// Strip tables go straight into the group's pinned staging buffer
+// (PoaArena::st_*) unless SVS_POA_STAGING=vec keeps them in each task's
+// vectors, copied into the buffer when the launch is packed.
+// Strips after the first 128 columns wide, two per lane (poa_strip.hip,
+// sweep_w) with SVS_POA_WIDE=1.
+bool wide_strips() {
+  const char* e = std::getenv("SVS_POA_WIDE");
+  return e && std::string(e) == "1";
+}
+
+bool direct_staging() {
+  const char* e = std::getenv("SVS_POA_STAGING");
+  return !(e && std::string(e) == "vec");
+}
+
+// a read in its block: zero pad byte, the read, zeros up to ls + 64 bytes
+void write_read(char* p, const std::string& s, uint32_t ls) {
+  p[-1] = 0;
+  std::memcpy(p, s.data(), s.size());
+  std::memset(p + s.size(), 0, ls + 63 - s.size());
+}
+
+// Exports the strip tables of t's next step into a fresh block of A's staging
+// buffer; false (nothing written) when the buffer is full.
+bool export_direct(PoaTask& t, const int32_t* gaps, PoaArena& A) {
+  const std::string& s = t.seqs[t.next];
+  // the read's region is sized for either strip width (strip_ls_wide >= the 64-column stride)
+  const uint32_t ls = strip_ls_wide(static_cast<uint32_t>(s.size()));
+  const StripBlock b = strip_block_layout(t.graph.num_nodes(), t.graph.num_edges(), ls);
+  const size_t off = A.st_cur.fetch_add(b.bytes, std::memory_order_relaxed);
+  if (off + b.bytes > A.h_in.cap) return false;
+  char* base = A.h_in.as<char>() + off;
+  const StripDst dst{reinterpret_cast<uint32_t*>(base + b.rec), reinterpret_cast<uint32_t*>(base + b.pstart),
+                     reinterpret_cast<uint32_t*>(base + b.pred_row), reinterpret_cast<uint32_t*>(base + b.pred_slot),
+                     reinterpret_cast<int32_t*>(base + b.col0)};
+  t.graph.export_strip_rows(&t.rows, gaps, &dst);
+  write_read(base + b.seq, s, ls);
+  t.rows_at = 2;
+  t.blk_off = off;
+  t.blk_gen = A.st_gen;
+  return true;
+}
+
 uint64_t job_bytes(const RowTables& tt, uint64_t L, const KernelEnv& ke) {
-  const uint64_t ls = round_up(L + 1, 64), V = tt.pstart.size() - 1;
+  const uint64_t ls = strip_ls_wide(static_cast<uint32_t>(L)), V = tt.n_rows;
   if (ke.strip) {
     // traceback codes + two strip-boundary carry buffers (+ a global pool when
     // the graph needs more slots than the LDS pool holds)
@@ -192,17 +235,34 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   auto th0 = Clock::now();
   const size_t nj = la.ids.size();
   la.jobs.assign(nj, PoaJob{});
-  uint64_t n_rows = 0, n_pstart = 0, n_pred = 0, n_seq = 0, n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
+  uint64_t n_rows = 0, n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
   uint32_t max_preds = 0, max_slots = 1;
   bool any_prune = false;
+  PoaArena& A = *la.arena;
+  const int32_t gaps[4] = {score.g, score.e, score.q, score.c};
+  // tables in an earlier generation of the staging buffer (a retried job, or
+  // the over-budget sub-launch path) are exported again
+  ctx->pool->parallel_for(nj, [&](size_t k) {
+    PoaTask& t = tasks[la.ids[k]];
+    if (t.rows_at != 2 || t.blk_gen == A.st_gen) return;
+    if (!export_direct(t, gaps, A)) {
+      t.graph.export_strip_rows(&t.rows, gaps);
+      t.rows_at = 1;
+    }
+  });
   for (size_t k = 0; k < nj; ++k) max_slots = std::max(max_slots, tasks[la.ids[k]].rows.n_slots);
   const bool lds_pool = max_slots <= kStripMaxLdsSlots && !strip_pool_forced_global();
+  const bool wide = lds_pool && wide_strips();
+  const uint64_t slot_bytes = wide ? kStripSlotBytesWide : kStripSlotBytes;
+  auto job_ls = [&](size_t len) -> uint32_t {
+    return wide ? strip_ls_wide(static_cast<uint32_t>(len)) : static_cast<uint32_t>(round_up(len + 1, 64));
+  };
   // waves per job: enough strip-pipeline waves to fill the CUs, only for reads
   // wide enough to give every wave several strips; SVS_POA_WPJ overrides
   uint32_t min_strips = 0xFFFFFFFFu;
   for (size_t k = 0; k < nj; ++k) {
-    const uint32_t ls = static_cast<uint32_t>(round_up(tasks[la.ids[k]].seqs[tasks[la.ids[k]].next].size() + 1, 64));
-    min_strips = std::min(min_strips, ls / 64);
+    const uint32_t ls = job_ls(tasks[la.ids[k]].seqs[tasks[la.ids[k]].next].size());
+    min_strips = std::min(min_strips, wide ? 1 + (ls - 64) / 128 : ls / 64);
   }
   int wpj = 1;
   const char* we = std::getenv("SVS_POA_WPJ");
@@ -218,25 +278,23 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     while (wpj < 8 && static_cast<size_t>(wpj) * nj < 6144 && min_strips >= static_cast<uint32_t>(6 * wpj)) wpj *= 2;
     // the small launches at the end of a batch: 16 waves per job (>= 2 strips
     // each), or the few remaining jobs leave most SIMDs idle
-    if (lds_pool && wpj == 8 && nj < 512 && min_strips >= 32) wpj = 16;
+    if (lds_pool && wpj == 8 && nj < 512 && min_strips >= (wide ? 16u : 32u)) wpj = 16;
   }
+  if (wide)
+    while (wpj & (wpj - 1)) wpj &= wpj - 1;  // the wide kernel comes in 1, 2, 4, 8, 16 waves per job
   // the per-wave LDS pools of one workgroup must fit the CU's LDS
-  while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * kStripSlotBytes > kStripLdsBytes) wpj /= 2;
-  if (std::getenv("SVS_POA_DEBUG")) std::fprintf(stderr, "[svs] strip launch: %zu jobs, wpj %d, slots %u\n", nj, wpj, max_slots);
+  while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * slot_bytes > kStripLdsBytes) wpj /= 2;
+  if (std::getenv("SVS_POA_DEBUG"))
+    std::fprintf(stderr, "[svs] strip launch: %zu jobs, wpj %d, slots %u, wide %d\n", nj, wpj, max_slots, wide ? 1 : 0);
   const PruneEnv penv;
   for (size_t k = 0; k < nj; ++k) {
     const auto& tt = tasks[la.ids[k]].rows;
     const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];
     PoaJob& J = la.jobs[k];
-    J.n_rows = static_cast<uint32_t>(tt.pstart.size() - 1);
+    J.n_rows = tt.n_rows;
     J.len = static_cast<uint32_t>(s.size());
-    J.ls = static_cast<uint32_t>(round_up(J.len + 1, 64));
+    J.ls = job_ls(J.len);
     J.n_slots = tt.n_slots;
-    J.row_off = static_cast<uint32_t>(n_rows);
-    J.rec_off = static_cast<uint32_t>(n_rows);
-    J.pstart_off = static_cast<uint32_t>(n_pstart);
-    J.pred_off = static_cast<uint32_t>(n_pred);
-    J.seq_off = static_cast<uint32_t>(n_seq + 1);  // one zero pad byte precedes each read
     J.tb_off = n_tb;
     J.bnd_off = n_bnd;
     J.pool_off = n_pool;
@@ -245,9 +303,6 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     if (J.n_slots > 31) J.lb = kNoPrune;  // the kernel tracks slot liveness in 31 bits
     any_prune = any_prune || J.lb != kNoPrune;
     n_rows += J.n_rows;
-    n_pstart += J.n_rows + 1;
-    n_pred += tt.pred_row.size();
-    n_seq += J.ls + 64;
     n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
     n_bnd += round_up(round_up(J.n_rows, 8) * (J.ls / 64) * 4, 64);
     if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 97, 64);
@@ -261,35 +316,55 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   if (any_prune)
     for (PoaJob& J : la.jobs)
       if (J.lb == kNoPrune) J.lb = kPruneAll;
-  if (n_rows * kRecWords > 0xFFFFFFFFull || n_pred > 0xFFFFFFFFull || n_seq > 0xFFFFFFFFull)
-    throw SvsError(SVS_E_UNSUPPORTED, "batch too large for 32-bit table offsets");
   la.n_aln = n_aln;
-  size_t off = 0;
-  auto sec = [&](size_t bytes) {
-    const size_t o = off;
-    off = round_up(off + bytes, 256);
-    return o;
-  };
-  const size_t s_jobs = sec(nj * sizeof(PoaJob));
-  const size_t s_rec = sec(n_rows * kRecWords * 4), s_ps = sec(n_pstart * 4), s_col0 = sec(n_rows * 12);
-  const size_t s_prow = sec(n_pred * 4), s_pslot = sec(n_pred * 4), s_seq = sec(n_seq + 256);
-  PoaArena& A = *la.arena;
-  A.h_in.ensure(off);
+  // every job's tables as one StripBlock in the staging buffer: blocks the
+  // fold exported in place, then blocks for tables held in vectors (copied),
+  // then the job descriptors
+  size_t start = std::min(A.st_cur.load(std::memory_order_relaxed), A.h_in.cap);
+  start = round_up(start, 48);
+  std::vector<StripBlock> lay(nj);
+  std::vector<size_t> boff(nj);
+  size_t end = start;
+  for (size_t k = 0; k < nj; ++k) {
+    const PoaTask& t = tasks[la.ids[k]];
+    lay[k] = strip_block_layout(t.rows.n_rows, t.rows.n_edges, strip_ls_wide(la.jobs[k].len));
+    if (t.rows_at == 2) {
+      boff[k] = t.blk_off;
+    } else {
+      boff[k] = end;
+      end += lay[k].bytes;
+    }
+  }
+  const size_t s_jobs = round_up(end, 256), off = s_jobs + nj * sizeof(PoaJob);
+  if (off > A.h_in.cap) A.h_in.grow_keep(off, start);
+  A.st_peak = std::max(A.st_peak, off);
+  if (off > 0xFFFFFFFFull) throw SvsError(SVS_E_UNSUPPORTED, "batch too large for 32-bit table offsets");
   char* hs = A.h_in.as<char>();
+  for (size_t k = 0; k < nj; ++k) {
+    PoaJob& J = la.jobs[k];
+    const size_t b = boff[k];
+    J.row_off = static_cast<uint32_t>((b + lay[k].col0) / 12);
+    J.rec_off = static_cast<uint32_t>((b + lay[k].rec) / 16);
+    J.pstart_off = static_cast<uint32_t>((b + lay[k].pstart) / 4);
+    J.pred_off = static_cast<uint32_t>((b + lay[k].pred_row) / 4);
+    J.pslot_off = static_cast<uint32_t>((b + lay[k].pred_slot) / 4);
+    J.seq_off = static_cast<uint32_t>(b + lay[k].seq);
+  }
   std::memcpy(hs + s_jobs, la.jobs.data(), nj * sizeof(PoaJob));
   ctx->pool->parallel_for(nj, [&](size_t k) {
-    const auto& tt = tasks[la.ids[k]].rows;
+    const PoaTask& t = tasks[la.ids[k]];
+    if (t.rows_at == 2) return;
+    const auto& tt = t.rows;
     const PoaJob& J = la.jobs[k];
-    std::memcpy(hs + s_rec + 4ull * kRecWords * J.rec_off, tt.rec.data(), 4ull * kRecWords * J.n_rows);
-    std::memcpy(hs + s_ps + 4ull * J.pstart_off, tt.pstart.data(), 4ull * (J.n_rows + 1));
-    std::memcpy(hs + s_col0 + 12ull * J.row_off, tt.col0.data(), 12ull * J.n_rows);
+    char* base = hs + boff[k];
+    std::memcpy(base + lay[k].rec, tt.rec.data(), 4ull * kRecWords * J.n_rows);
+    std::memcpy(base + lay[k].pstart, tt.pstart.data(), 4ull * (J.n_rows + 1));
+    std::memcpy(base + lay[k].col0, tt.col0.data(), 12ull * J.n_rows);
     if (!tt.pred_row.empty()) {
-      std::memcpy(hs + s_prow + 4ull * J.pred_off, tt.pred_row.data(), 4 * tt.pred_row.size());
-      std::memcpy(hs + s_pslot + 4ull * J.pred_off, tt.pred_slot.data(), 4 * tt.pred_slot.size());
+      std::memcpy(base + lay[k].pred_row, tt.pred_row.data(), 4 * tt.pred_row.size());
+      std::memcpy(base + lay[k].pred_slot, tt.pred_slot.data(), 4 * tt.pred_slot.size());
     }
-    const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];
-    std::memset(hs + s_seq + J.seq_off - 1, 0, J.ls + 64);
-    std::memcpy(hs + s_seq + J.seq_off, s.data(), s.size());
+    write_read(base + lay[k].seq, t.seqs[t.next], strip_ls_wide(J.len));
   });
   host_ms += ms_since(th0);
 
@@ -310,12 +385,13 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
   pl.n_jobs = static_cast<int>(nj);
   pl.score = score;
-  pl.rec = reinterpret_cast<const uint32_t*>(dg + s_rec);
-  pl.row_pstart = reinterpret_cast<const uint32_t*>(dg + s_ps);
-  pl.pred_row = reinterpret_cast<const uint32_t*>(dg + s_prow);
-  pl.pred_slot = reinterpret_cast<const uint32_t*>(dg + s_pslot);
-  pl.col0 = reinterpret_cast<const int32_t*>(dg + s_col0);
-  pl.seqs = reinterpret_cast<const uint8_t*>(dg + s_seq);
+  // every table indexes the staging copy from its start (PoaJob offsets)
+  pl.rec = reinterpret_cast<const uint32_t*>(dg);
+  pl.row_pstart = reinterpret_cast<const uint32_t*>(dg);
+  pl.pred_row = reinterpret_cast<const uint32_t*>(dg);
+  pl.pred_slot = reinterpret_cast<const uint32_t*>(dg);
+  pl.col0 = reinterpret_cast<const int32_t*>(dg);
+  pl.seqs = reinterpret_cast<const uint8_t*>(dg);
   pl.tb = A.d_tb.as<uint16_t>();
   pl.bnd = A.d_pool.as<int32_t>();
   pl.pool = A.d_pool.as<int32_t>() + n_bnd;
@@ -323,6 +399,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.aln_len = A.d_alen.as<int32_t>();
   pl.lds_slots = lds_pool ? max_slots : 0;
   pl.prune = any_prune;
+  pl.wide = wide;
   pl.waves_per_job = wpj;
   la.wpj = wpj;
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
@@ -364,6 +441,7 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, c
     J.row_off = static_cast<uint32_t>(n_rows);
     J.pstart_off = static_cast<uint32_t>(n_pstart);
     J.pred_off = static_cast<uint32_t>(n_pred);
+    J.pslot_off = J.pred_off;
     J.seq_off = static_cast<uint32_t>(n_seq + 1);  // one zero pad byte precedes each read
     J.tb_off = n_tb;
     J.pool_off = n_pool;
@@ -461,7 +539,7 @@ void pack_and_launch(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, c
 // fresh chain (no DP), empty ones are skipped; then either the row tables of
 // the next alignment are exported (returns 1) or, with every sequence in, the
 // consensus and MSA are computed (returns 2).
-uint8_t prep_task(PoaTask& t, const svs_poa_config& cfg) {
+uint8_t prep_task(PoaTask& t, const svs_poa_config& cfg, PoaArena* stage) {
   while (t.next < t.seqs.size()) {
     const std::string& s = t.seqs[t.next];
     if (s.empty()) { ++t.next; continue; }
@@ -471,10 +549,14 @@ uint8_t prep_task(PoaTask& t, const svs_poa_config& cfg) {
   if (t.next < t.seqs.size()) {
     if (use_strip_kernel()) {
       const int32_t gaps[4] = {cfg.g, cfg.e, cfg.q, cfg.c};
-      t.graph.export_strip_rows(&t.rows, gaps);
+      if (!stage || !export_direct(t, gaps, *stage)) {
+        t.graph.export_strip_rows(&t.rows, gaps);
+        t.rows_at = 1;
+      }
     } else {
       t.graph.export_rows(&t.rows);
       fill_col0(&t.rows, cfg.g, cfg.e, cfg.q, cfg.c);
+      t.rows_at = 1;
     }
     return 1;
   }
@@ -502,6 +584,14 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   }
   SVS_HIP(hipEventSynchronize(A.done));  // the other group's launch may still be queued behind it
   st.gpu_wait_ms += ms_since(tw0);
+  // the launch's staging copy is consumed: a new generation for the next one
+  PoaArena* stage = nullptr;
+  if (use_strip_kernel() && direct_staging()) {
+    A.st_gen += 1;
+    A.st_cur.store(0, std::memory_order_relaxed);
+    A.h_in.ensure(A.st_peak + A.st_peak / 4);
+    stage = &A;
+  }
   float ms = 0.f;
   SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
   st.kernel_ms += ms;
@@ -550,7 +640,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
     }
     t.graph.add_alignment_ranks(fwd, t.seqs[t.next]);
     ++t.next;
-    t.prepped = prep_task(t, cfg);
+    t.prepped = prep_task(t, cfg, stage);
   });
   host_ms += ms_since(th0);
   g_trace.host("fold", la.gid, th0, la.ids.size());
@@ -637,10 +727,11 @@ struct PoaScheduler::Impl {
       if (g.active.empty()) return;
       auto th0 = Clock::now();
       needs.assign(g.active.size(), 0);
+      PoaArena* stage = use_strip_kernel() && direct_staging() ? g.arena : nullptr;
       // sequences landing on an empty graph become a fresh chain (no DP)
       ctx->pool->parallel_for(g.active.size(), [&](size_t i) {
         PoaTask& t = tasks[g.active[i]];
-        const uint8_t state = t.prepped ? t.prepped : prep_task(t, cfg);
+        const uint8_t state = t.prepped ? t.prepped : prep_task(t, cfg, stage);
         t.prepped = 0;
         needs[i] = state == 1 ? 1 : 0;
       });
