@@ -44,7 +44,7 @@ struct PoaTask {
   // exact pruning of the strip kernel (svs_poa_engine.cpp: prune_bound)
   double rate = 0.0;      // best score / read length of the last alignment that needed no retry
   bool have_rate = false;
-  bool retry = false;     // the current sequence's pruned run missed its bound: run it unpruned
+  bool retry = false;     // the current sequence's pruned run missed its bound: run it again (prune_bound)
   uint8_t prepped = 0;    // next step already readied after the fold: 1 export done, 2 complete
   // where the strip tables of the next step are: 1 in rows' vectors, 2 in a
   // block of the group's staging buffer (blk_off, valid while the buffer's
@@ -52,7 +52,8 @@ struct PoaTask {
   uint8_t rows_at = 0;
   uint32_t blk_gen = 0;
   uint64_t blk_off = 0;
-  uint8_t n_retries = 0;
+  uint8_t n_retries = 0;     // retried alignments of this task
+  uint8_t read_retries = 0;  // retries of the current sequence
 
   std::string consensus;
   std::vector<std::string> msa;

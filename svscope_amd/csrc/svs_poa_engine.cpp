@@ -141,27 +141,48 @@ bool strip_pool_forced_global() {
 
 // Exact pruning bound of a strip job (poa_strip.hip): lb = the score per read
 // base of the task's last alignment that needed no retry x this read's length,
-// less a slack of SVS_POA_PRUNE_SLACK (default 0.05) x m x length.  Any value is exact: a
-// bound above the optimum only costs a retry with no bound.  Off for the first
-// alignment of a task, for a retry, after two retries of one task, for graphs
+// less a slack of SVS_POA_PRUNE_SLACK (default 0.025) x m x length.  Any value is exact: a
+// bound above the optimum only costs a retry.  The first retry of a read runs
+// with the looser slack SVS_POA_PRUNE_RETRY_SLACK (default 0.1; "none": no
+// bound), a second one with no bound; each retry of a task multiplies its
+// slack by SVS_POA_PRUNE_ADAPT (default 1.5, up to the retry slack).  Values
+// from the sweep in profiles/r02_v16, r02_v17.  Off for the first alignment of a task,
+// after SVS_POA_PRUNE_MAX_RETRIES (default 16) retries of one task, for graphs
 // too long for the 16-bit path lengths of the row records, and for score
 // parameters the kernel's upper bound does not cover (SVS_POA_PRUNE=0: off).
 struct PruneEnv {
   bool on = true;
-  double slack = 0.05;
+  double slack = 0.025;
+  bool retry_pruned = true;
+  double retry_slack = 0.1;
+  int max_retries = 16;
+  double adapt = 1.5;  // a task's slack grows by this factor after each retry (SVS_POA_PRUNE_ADAPT)
   PruneEnv() {  // read once per launch, not once per job
     const char* pe = std::getenv("SVS_POA_PRUNE");
     on = !(pe && std::string(pe) == "0");
     const char* se = std::getenv("SVS_POA_PRUNE_SLACK");
     if (se) slack = std::atof(se);
+    const char* re = std::getenv("SVS_POA_PRUNE_RETRY_SLACK");
+    if (re && std::string(re) == "none") retry_pruned = false;
+    else if (re) retry_slack = std::atof(re);
+    const char* me = std::getenv("SVS_POA_PRUNE_MAX_RETRIES");
+    if (me) max_retries = std::atoi(me);
+    const char* ae = std::getenv("SVS_POA_PRUNE_ADAPT");
+    if (ae) adapt = std::atof(ae);
   }
 };
 
 int32_t prune_bound(const PoaTask& t, const PoaScore& P, uint32_t n_rows, uint32_t len, const PruneEnv& pv) {
   const bool on = pv.on;
-  const double slack = pv.slack;
   const int32_t cg = std::max(std::max(P.g, P.e), std::max(P.q, P.c));
-  if (!on || !t.have_rate || t.retry || t.n_retries >= 2 || n_rows > 0xFFFFu || len > (1u << 20)) return kNoPrune;
+  if (!on || !t.have_rate || t.n_retries >= pv.max_retries || n_rows > 0xFFFFu || len > (1u << 20)) return kNoPrune;
+  if (t.read_retries >= (pv.retry_pruned ? 2 : 1)) return kNoPrune;
+  double slack = pv.retry_slack;
+  if (t.read_retries == 0) {
+    slack = pv.slack;
+    for (int k = 0; k < t.n_retries && slack < pv.retry_slack; ++k) slack *= pv.adapt;
+    slack = std::min(slack, std::max(pv.slack, pv.retry_slack));
+  }
   if (cg > 0 || P.m < P.n || P.m < 0) return kNoPrune;
   const double lb = std::floor(t.rate * len - slack * P.m * len);
   if (lb < -1e9 || lb > 1e9) return kNoPrune;
@@ -620,6 +641,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
       // (its row tables are still those of this step)
       t.retry = true;
       t.n_retries += 1;
+      t.read_retries += 1;
       t.prepped = 1;
       return;
     }
@@ -631,6 +653,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
         t.have_rate = true;
       }
       t.retry = false;
+      t.read_retries = 0;
     }
     const int32_t* p = aout + 2 * la.jobs[k].aln_off;
     std::vector<int32_t> fwd(2 * static_cast<size_t>(n));

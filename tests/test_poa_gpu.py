@@ -103,6 +103,15 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_PRUNE_SLACK": "0", "SVS_POA_WPJ": "8"},
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_WPJ": "4"},
     {"SVS_POA_PRUNE_SLACK": "0", "SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "2"},
+    {"SVS_POA_WIDE": "1", "SVS_POA_WPJ": "1"},
+    {"SVS_POA_WIDE": "1", "SVS_POA_WPJ": "2"},
+    {"SVS_POA_WIDE": "1", "SVS_POA_WPJ": "4"},
+    {"SVS_POA_WIDE": "1", "SVS_POA_WPJ": "16"},
+    {"SVS_POA_WIDE": "1", "SVS_POA_PRUNE": "0"},
+    {"SVS_POA_WIDE": "1", "SVS_POA_PRUNE_SLACK": "0", "SVS_POA_WPJ": "8"},
+    {"SVS_POA_WIDE": "1", "SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_WPJ": "4"},
+    {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "none"},
+    {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "-0.3", "SVS_POA_PRUNE_MAX_RETRIES": "100"},
     {"SVS_POA_STAGING": "vec"},
     {"SVS_POA_STAGING": "vec", "SVS_POA_PRUNE_SLACK": "-0.3"},
 ])
@@ -111,9 +120,11 @@ def test_kernel_variants_match_oracle(env):
     waves per job, strip-major with 1/2/3/4/7/8/16 pipelined waves per job, the
     strip-major kernel with its pool in global memory, and the strip kernel's
     exact pruning off, at its tightest slack, and with a bound above the
-    optimum (every pruned job retried unpruned; with the tables exported straight
+    optimum (every pruned job retried: with the looser retry slack, unpruned, or
+    twice, the second time unpruned; with the tables exported straight
     into the staging buffer a retried job's block is exported again), and with
-    the tables packed from per-task vectors (SVS_POA_STAGING=vec)."""
+    the tables packed from per-task vectors (SVS_POA_STAGING=vec); and all of
+    that again with 128-column strips after strip 0 (SVS_POA_WIDE=1)."""
     import os
     from svscope_amd import synth
     from svscope_amd.poa import poa_batch
