@@ -54,6 +54,7 @@ struct PoaTask {
   uint64_t blk_off = 0;
   uint8_t n_retries = 0;     // retried alignments of this task
   uint8_t read_retries = 0;  // retries of the current sequence
+  uint32_t last_rows = 0;    // strip rows (64 columns) the last alignment computed
 
   std::string consensus;
   std::vector<std::string> msa;

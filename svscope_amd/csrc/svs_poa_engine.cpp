@@ -630,6 +630,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   if (strip) {
     for (size_t k = 0; k < nj; ++k) {
       st.cells_computed += 64ull * static_cast<uint32_t>(alen[2 * nj + k]);
+      tasks[la.ids[k]].last_rows = static_cast<uint32_t>(alen[2 * nj + k]);
       if (alen[k] == kPruneRetry) st.prune_retries += 1;
     }
   }
@@ -776,6 +777,7 @@ struct PoaScheduler::Impl {
       const KernelEnv ke;
       for (uint32_t id : ids) total += job_bytes(tasks[id].rows, tasks[id].seqs[tasks[id].next].size(), ke);
       if (total <= budget) {
+        order_by_cost(ids);
         g.la.ids = std::move(ids);
         g.la.arena = g.arena;
         g.la.gid = gid(g);
@@ -808,6 +810,27 @@ struct PoaScheduler::Impl {
   }
 
   int gid(const Group& g) const { return static_cast<int>(&g - groups); }
+
+  // Longest expected job first (SVS_POA_JOB_ORDER=0: task order).  A launch
+  // holds more waves than the GPU keeps resident, and workgroups start in job
+  // order, so the jobs that start last should be short ones.  Expected cost:
+  // the strip rows the task's previous alignment computed; for a retry or a
+  // task with no history, the unpruned strip rows.
+  void order_by_cost(std::vector<uint32_t>& ids) {
+    static const bool on = [] {
+      const char* e = std::getenv("SVS_POA_JOB_ORDER");
+      return !(e && std::string(e) == "0");
+    }();
+    if (!on || !use_strip_kernel()) return;
+    std::vector<std::pair<uint64_t, uint32_t>> c(ids.size());
+    for (size_t i = 0; i < ids.size(); ++i) {
+      const PoaTask& t = tasks[ids[i]];
+      const uint64_t full = static_cast<uint64_t>(t.rows.n_rows) * ((t.seqs[t.next].size() + 64) / 64);
+      c[i] = {t.last_rows == 0 || t.retry ? full : t.last_rows, ids[i]};
+    }
+    std::stable_sort(c.begin(), c.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    for (size_t i = 0; i < ids.size(); ++i) ids[i] = c[i].second;
+  }
 
   // Releases the storage of up to one pool-width chunk of finished tasks;
   // false when none are left.
