@@ -300,6 +300,8 @@ def main():
             "cpu_baseline": cpu,
             "breakdown": {"poa_cells": cells, "poa_cells_computed": cells_done,
                           "prune_retries": poa["prune_retries"],
+                          "poa_prep_kernel_ms": round(poa.get("prep_ms", 0.0), 2),
+                          "poa_prep_jobs": poa.get("prep_jobs", 0),
                           "poa_kernel_ms": round(kms, 2), "poa_launches": launches,
                           "gcups": round(cells_done / (kms * 1e-3) / 1e9, 3) if kms else None,
                           "gcups_full_matrix_equivalent": round(cells / (kms * 1e-3) / 1e9, 3) if kms else None,

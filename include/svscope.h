@@ -59,7 +59,9 @@ typedef struct svs_poa_stats {
   double gpu_wait_ms;       /* host time blocked waiting for a launch's results */
   uint64_t cells_computed;  /* DP cells the kernel evaluated (64-column strip rows x 64;
                                below dp_cells when the exact pruning skips rows) */
-  uint64_t prune_retries;   /* pruned alignments re-run unpruned (bound above the optimum) */
+  uint64_t prune_retries;   /* pruned alignments re-run (bound above the optimum) */
+  double prep_ms;           /* device half of the row export (poa_strip_prep_kernel), HIP events */
+  uint64_t prep_jobs;       /* alignments whose row tables the device completed */
 } svs_poa_stats;
 
 /* One context per host thread; owns a HIP stream and device arenas. */

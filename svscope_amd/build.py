@@ -23,6 +23,7 @@ ARCH = os.environ.get("SVS_OFFLOAD_ARCH", "gfx950")
 SOURCES = [
     "poa_kernels.hip",
     "poa_strip.hip",
+    "poa_prep.hip",
     "em_kernels.hip",
     "misscore_kernels.hip",
     "poa_graph.cpp",

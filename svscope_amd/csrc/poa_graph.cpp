@@ -260,6 +260,7 @@ void PoaGraph::export_strip_rows(RowTables* t, const int32_t* gaps, const StripD
   const uint32_t E = static_cast<uint32_t>(e_tail_.size());
   t->n_rows = V;
   t->n_edges = E;
+  t->lite = false;
   static thread_local std::vector<uint32_t> lds_last, slot, free_slots, dmin, dmax;
   lds_last.assign(V, 0);
   slot.resize(V);
@@ -370,6 +371,58 @@ void PoaGraph::export_strip_rows(RowTables* t, const int32_t* gaps, const StripD
     }
     rec[static_cast<size_t>(r) * kRecWords + 2] = std::min(lo[r], 0xFFFFu) | (std::min(hi[r], 0xFFFFu) << 16);
   }
+}
+
+void PoaGraph::export_strip_lite(RowTables* t, const StripLiteDst* dst) const {
+  const uint32_t V = num_nodes();
+  t->n_rows = V;
+  t->n_edges = static_cast<uint32_t>(e_tail_.size());
+  t->lite = true;
+  static thread_local std::vector<uint32_t> lds_last;
+  lds_last.assign(V, 0);
+  uint32_t* __restrict__ pstart = dst->pstart;
+  uint32_t* __restrict__ pred_row = dst->pred_row;
+  uint32_t* __restrict__ info = dst->info;
+  uint32_t* __restrict__ last = lds_last.data();
+  const uint32_t* __restrict__ n2r = node_to_rank_.data();
+  const uint32_t* __restrict__ etail = e_tail_.data();
+  // pass 1 of export_strip_rows: in-edge rows, per row its last pool reader
+  uint32_t k = 0, max_preds = 0;
+  for (uint32_t r = 0; r < V; ++r) {
+    const uint32_t node = rank_to_node_[r];
+    const NodeList& in = in_[node];
+    pstart[r] = k;
+    max_preds = std::max(max_preds, in.size());
+    for (uint32_t e : in) {
+      const uint32_t pr = n2r[etail[e]];
+      pred_row[k++] = pr + 1;
+      if (pr + 1 != r && last[pr] < r + 1) last[pr] = r + 1;
+    }
+    info[r] = static_cast<uint8_t>(base_[node]) | (out_[node].empty() ? 0x100u : 0u) | (in.size() << 10);
+  }
+  pstart[V] = k;
+  t->max_preds = max_preds;
+  // the planner's free-list size, replayed: store bits, last-read flags and
+  // the slot count of export_strip_rows' pass 2
+  const char* wide_env = std::getenv("SVS_POA_TEST_WIDE_SLOTS");
+  const uint32_t wide_rows = wide_env ? static_cast<uint32_t>(std::strtoul(wide_env, nullptr, 10)) : 0u;
+  uint32_t next = (wide_rows != 0 && V >= wide_rows) ? 40 : 1, nfree = 0;
+  t->slot_base = next;
+  for (uint32_t r = 0; r < V; ++r) {
+    if (last[r] != 0) {
+      info[r] |= 0x200u;
+      if (nfree) --nfree;
+      else ++next;
+    }
+    for (uint32_t x = pstart[r]; x < pstart[r + 1]; ++x) {
+      const uint32_t pr = pred_row[x] - 1;
+      if (pr + 1 != r && last[pr] == r + 1) {
+        pred_row[x] |= 0x80000000u;
+        ++nfree;
+      }
+    }
+  }
+  t->n_slots = next;
 }
 
 void fill_col0(RowTables* t, int32_t g, int32_t e, int32_t q, int32_t c) {

@@ -27,6 +27,8 @@ struct RowTables {
   uint32_t n_slots = 1;
   uint32_t max_preds = 0;
   uint32_t n_rows = 0, n_edges = 0;  // set by export_strip_rows (also when it writes to a StripDst)
+  uint32_t slot_base = 1;             // first pool slot the planner hands out (export_strip_lite)
+  bool lite = false;                  // written by export_strip_lite (the device completes the tables)
   // Strip-kernel tables (export_strip_rows): kRecWords words per row
   //   w0: base | sink << 8 | store << 9 | np << 10 | own pool slot << 16
   //       (kNoSlot: not stored)
@@ -129,9 +131,10 @@ constexpr uint32_t kNoSlot = 0xFFFF;
 // (4 E), then the read: one zero pad byte, the read, zeros up to ls + 64.
 struct StripBlock {
   size_t col0, rec, pstart, pred_row, pred_slot, seq, bytes;
+  size_t info;  // strip_block_lite only
 };
 inline StripBlock strip_block_layout(uint32_t V, uint32_t E, uint32_t ls) {
-  StripBlock b;
+  StripBlock b{};
   size_t o = 0;
   b.col0 = o;
   o = (o + 12ull * V + 15) / 16 * 16;
@@ -148,6 +151,46 @@ inline StripBlock strip_block_layout(uint32_t V, uint32_t E, uint32_t ls) {
   b.bytes = (o + 47) / 48 * 48;
   return b;
 }
+
+// The same block for a job whose row records, in-edge slots and column 0 the
+// device derives (poa_prep.hip): pstart, pred_row (bit 31: this in-edge is its
+// tail row's last pool read), per row base | sink << 8 | store << 9 |
+// in-degree << 10, then the read.
+inline StripBlock strip_block_lite(uint32_t V, uint32_t E, uint32_t ls) {
+  StripBlock b{};
+  size_t o = 0;
+  b.pstart = o;
+  o += 4ull * (V + 1);
+  b.pred_row = o;
+  o += 4ull * E;
+  b.info = o;
+  o += 4ull * V;
+  b.seq = o + 1;
+  o += ls + 64;
+  b.bytes = (o + 47) / 48 * 48;
+  return b;
+}
+// Device-side output region of such a job: column 0 (12 V), records (16 V),
+// in-edge slots (4 E); starts at a multiple of 48.
+inline StripBlock strip_prep_out_layout(uint32_t V, uint32_t E) {
+  StripBlock b{};
+  size_t o = 0;
+  b.col0 = o;
+  o = (o + 12ull * V + 15) / 16 * 16;
+  b.rec = o;
+  o += 16ull * V;
+  b.pred_slot = o;
+  o += 4ull * E;
+  b.bytes = (o + 47) / 48 * 48;
+  return b;
+}
+
+// Destinations for export_strip_lite.
+struct StripLiteDst {
+  uint32_t* pstart;
+  uint32_t* pred_row;
+  uint32_t* info;
+};
 
 // Raw destinations for export_strip_rows (a StripBlock in pinned staging).
 struct StripDst {
@@ -188,6 +231,10 @@ class PoaGraph {
   // the same, writing the tables to dst instead of t's vectors (which are left
   // untouched); t gets n_rows, n_edges, n_slots and max_preds
   void export_strip_rows(RowTables* t, const int32_t* gaps, const StripDst* dst) const;
+  // Pass 1 of export_strip_rows only, for the device planner (poa_prep.hip):
+  // CSR in-edge rows with the last-read flag, per row words, and t's n_rows,
+  // n_edges, max_preds, slot_base and n_slots (the count the planner reaches).
+  void export_strip_lite(RowTables* t, const StripLiteDst* dst) const;
   std::vector<std::string> msa() const;
   std::string consensus(int32_t min_coverage);
 

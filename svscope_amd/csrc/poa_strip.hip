@@ -1312,7 +1312,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   auto pred_of = [&](int32_t row, uint32_t k) -> int32_t {
     if (k >= 2) {
       const uint32_t a = rps[row - 1], b = rps[row];
-      return (b == a) ? 0 : static_cast<int32_t>(prow[a + k]);
+      return (b == a) ? 0 : static_cast<int32_t>(prow[a + k] & 0x7FFFFFFFu);  // bit 31: export_strip_lite's flag
     }
     if (static_cast<uint32_t>(p_r - row) >= 64u) {
       p_r = row;
@@ -1320,8 +1320,8 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       uint32_t a = 0, b = 0;
       if (rr >= 1) { a = rps[rr - 1]; b = rps[rr]; }
       pn = static_cast<int32_t>(b - a);
-      p0 = pn > 0 ? static_cast<int32_t>(prow[a]) : 0;
-      p1 = pn > 1 ? static_cast<int32_t>(prow[a + 1]) : 0;
+      p0 = pn > 0 ? static_cast<int32_t>(prow[a] & 0x7FFFFFFFu) : 0;
+      p1 = pn > 1 ? static_cast<int32_t>(prow[a + 1] & 0x7FFFFFFFu) : 0;
     }
     const uint32_t l = static_cast<uint32_t>(p_r - row);
     const int32_t n = __builtin_amdgcn_readlane(pn, l);

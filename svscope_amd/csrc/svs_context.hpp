@@ -112,6 +112,7 @@ struct PoaArena {
   hipStream_t copy_stream = nullptr;  // this group's copies
   bool own = false;                   // stream is this group's, copies ride on it too
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr, h2d = nullptr;
+  hipEvent_t evp = nullptr;  // start of the launch's poa_strip_prep_kernel (ends at ev0)
   // Staging of the next launch's strip tables in h_in: the fold exports each
   // job's tables straight into a block claimed with an atomic bump (st_cur), so
   // packing the launch copies nothing.  A new generation (st_gen) starts when
@@ -134,6 +135,7 @@ struct PoaArena {
     }
     SVS_HIP(hipEventCreate(&ev0));
     SVS_HIP(hipEventCreate(&ev1));
+    SVS_HIP(hipEventCreate(&evp));
     SVS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
     SVS_HIP(hipEventCreateWithFlags(&h2d, hipEventDisableTiming));
   }
@@ -144,6 +146,7 @@ struct PoaArena {
     for (PinnedBuf* b : {&h_in, &h_aln, &h_alen}) b->release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    if (evp) (void)hipEventDestroy(evp);
     if (done) (void)hipEventDestroy(done);
     if (h2d) (void)hipEventDestroy(h2d);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);  // == stream when own

@@ -27,6 +27,9 @@ struct PoaJob {
   uint32_t rec_off;   // strip kernel: row records (kRecWords uint32 per row), in rows
   int32_t lb;         // strip kernel: pruning bound (kNoPrune = off), see poa_strip.hip
   uint32_t pslot_off;  // strip kernel: base of this job's pred_slot entries
+  uint32_t info_off;   // strip kernel, prep jobs: per-row words (export_strip_lite)
+  uint32_t prep;       // bit 0: row records, in-edge slots and column 0 come from
+                       // poa_strip_prep_kernel; bits 1..: the first pool slot
 };
 
 // PoaJob::lb value that turns the strip kernel's exact pruning off.
@@ -82,6 +85,13 @@ constexpr uint32_t kPoaMaxSlotsMultiWave = 64;
 
 hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream);
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream);
+// Device half of the strip row export (poa_prep.hip) for the jobs with
+// PoaJob::prep bit 0; every offset of those jobs indexes `base`.
+constexpr uint32_t kStripPrepMaxRows = 16384;  // rows of a prep job (LDS: 4 B per row)
+constexpr uint32_t kStripPrepMaxSlots = 64;    // pool slots of a prep job (free list in one VGPR)
+size_t strip_prep_lds_bytes(uint32_t max_rows);
+hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore& score, uint8_t* base,
+                                 uint32_t max_rows, hipStream_t stream);
 int choose_strip_wpj(int device, size_t n_jobs, uint32_t lds_slots, uint32_t min_strips);
 hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
                                 hipStream_t stream);

@@ -86,6 +86,8 @@ struct Launch {
   PoaArena* arena = nullptr;
   int wpj = 0;
   int gid = 0;
+  size_t prep_jobs = 0;  // jobs whose tables the device completed (poa_prep.hip)
+  int32_t gaps[4] = {0, 0, 0, 0};  // g, e, q, c of the launch (SVS_POA_VERIFY_PREP)
 };
 
 // Optional timeline (SVS_POA_TRACE=<file>): one line per host phase and per
@@ -211,6 +213,18 @@ bool direct_staging() {
   return !(e && std::string(e) == "vec");
 }
 
+// The device completes the strip tables (poa_prep.hip) of graphs it can hold
+// unless SVS_POA_DEVICE_PREP=0; SVS_POA_VERIFY_PREP=1 checks them against the
+// host's export after every launch (tests).
+bool device_prep() {
+  const char* e = std::getenv("SVS_POA_DEVICE_PREP");
+  return !(e && std::string(e) == "0");
+}
+bool verify_prep() {
+  const char* e = std::getenv("SVS_POA_VERIFY_PREP");
+  return e && std::string(e) == "1";
+}
+
 // a read in its block: zero pad byte, the read, zeros up to ls + 64 bytes
 void write_read(char* p, const std::string& s, uint32_t ls) {
   p[-1] = 0;
@@ -224,7 +238,27 @@ bool export_direct(PoaTask& t, const int32_t* gaps, PoaArena& A) {
   const std::string& s = t.seqs[t.next];
   // the read's region is sized for either strip width (strip_ls_wide >= the 64-column stride)
   const uint32_t ls = strip_ls_wide(static_cast<uint32_t>(s.size()));
-  const StripBlock b = strip_block_layout(t.graph.num_nodes(), t.graph.num_edges(), ls);
+  const uint32_t V = t.graph.num_nodes(), E = t.graph.num_edges();
+  if (device_prep() && V <= kStripPrepMaxRows && gaps[1] <= 0 && gaps[3] <= 0) {
+    // host pass 1 only; the device derives the rest (poa_prep.hip)
+    const StripBlock b = strip_block_lite(V, E, ls);
+    const size_t off = A.st_cur.fetch_add(b.bytes, std::memory_order_relaxed);
+    if (off + b.bytes > A.h_in.cap) return false;
+    char* base = A.h_in.as<char>() + off;
+    const StripLiteDst dst{reinterpret_cast<uint32_t*>(base + b.pstart), reinterpret_cast<uint32_t*>(base + b.pred_row),
+                           reinterpret_cast<uint32_t*>(base + b.info)};
+    t.graph.export_strip_lite(&t.rows, &dst);
+    if (t.rows.n_slots <= kStripPrepMaxSlots && t.rows.max_preds <= 31) {
+      write_read(base + b.seq, s, ls);
+      t.rows_at = 2;
+      t.blk_off = off;
+      t.blk_gen = A.st_gen;
+      return true;
+    }
+    // more pool slots or in-edges than the device planner takes: the full
+    // tables, in a block of their own
+  }
+  const StripBlock b = strip_block_layout(V, E, ls);
   const size_t off = A.st_cur.fetch_add(b.bytes, std::memory_order_relaxed);
   if (off + b.bytes > A.h_in.cap) return false;
   char* base = A.h_in.as<char>() + off;
@@ -348,7 +382,9 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   size_t end = start;
   for (size_t k = 0; k < nj; ++k) {
     const PoaTask& t = tasks[la.ids[k]];
-    lay[k] = strip_block_layout(t.rows.n_rows, t.rows.n_edges, strip_ls_wide(la.jobs[k].len));
+    const uint32_t lsw = strip_ls_wide(la.jobs[k].len);
+    lay[k] = (t.rows_at == 2 && t.rows.lite) ? strip_block_lite(t.rows.n_rows, t.rows.n_edges, lsw)
+                                              : strip_block_layout(t.rows.n_rows, t.rows.n_edges, lsw);
     if (t.rows_at == 2) {
       boff[k] = t.blk_off;
     } else {
@@ -361,16 +397,38 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   A.st_peak = std::max(A.st_peak, off);
   if (off > 0xFFFFFFFFull) throw SvsError(SVS_E_UNSUPPORTED, "batch too large for 32-bit table offsets");
   char* hs = A.h_in.as<char>();
+  // the device-derived tables of lite jobs: a region after the staging copy
+  // in the same device buffer, never copied from the host
+  size_t dev_end = round_up(off, 48);
+  uint32_t prep_rows = 0;
+  size_t n_prep = 0;
   for (size_t k = 0; k < nj; ++k) {
     PoaJob& J = la.jobs[k];
+    const PoaTask& t = tasks[la.ids[k]];
     const size_t b = boff[k];
-    J.row_off = static_cast<uint32_t>((b + lay[k].col0) / 12);
-    J.rec_off = static_cast<uint32_t>((b + lay[k].rec) / 16);
     J.pstart_off = static_cast<uint32_t>((b + lay[k].pstart) / 4);
     J.pred_off = static_cast<uint32_t>((b + lay[k].pred_row) / 4);
-    J.pslot_off = static_cast<uint32_t>((b + lay[k].pred_slot) / 4);
     J.seq_off = static_cast<uint32_t>(b + lay[k].seq);
+    if (t.rows_at == 2 && t.rows.lite) {
+      const StripBlock o = strip_prep_out_layout(t.rows.n_rows, t.rows.n_edges);
+      J.info_off = static_cast<uint32_t>((b + lay[k].info) / 4);
+      J.row_off = static_cast<uint32_t>((dev_end + o.col0) / 12);
+      J.rec_off = static_cast<uint32_t>((dev_end + o.rec) / 16);
+      J.pslot_off = static_cast<uint32_t>((dev_end + o.pred_slot) / 4);
+      J.prep = 1u | (t.rows.slot_base << 1);
+      dev_end += o.bytes;
+      prep_rows = std::max(prep_rows, t.rows.n_rows);
+      ++n_prep;
+    } else {
+      J.row_off = static_cast<uint32_t>((b + lay[k].col0) / 12);
+      J.rec_off = static_cast<uint32_t>((b + lay[k].rec) / 16);
+      J.pslot_off = static_cast<uint32_t>((b + lay[k].pred_slot) / 4);
+      J.prep = 0;
+    }
   }
+  if (dev_end / 16 > 0xFFFFFFFFull) throw SvsError(SVS_E_UNSUPPORTED, "batch too large for 32-bit table offsets");
+  la.prep_jobs = n_prep;
+  for (int x = 0; x < 4; ++x) la.gaps[x] = gaps[x];
   std::memcpy(hs + s_jobs, la.jobs.data(), nj * sizeof(PoaJob));
   ctx->pool->parallel_for(nj, [&](size_t k) {
     const PoaTask& t = tasks[la.ids[k]];
@@ -389,7 +447,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   });
   host_ms += ms_since(th0);
 
-  A.d_in.ensure(off);
+  A.d_in.ensure(dev_end);
   // the traceback codes dominate a launch's footprint: sized to the group's
   // budget at the first launch, so it never regrows (and syncs) mid-run
   A.d_tb.ensure(n_tb * 2 + 4096, ctx->device_budget / 2);
@@ -402,6 +460,10 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   SVS_HIP(hipMemcpyAsync(dg, hs, off, hipMemcpyHostToDevice, A.copy_stream));
   SVS_HIP(hipEventRecord(A.h2d, A.copy_stream));
   SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
+  SVS_HIP(hipEventRecord(A.evp, A.stream));
+  if (n_prep > 0)
+    SVS_HIP(launch_poa_strip_prep(reinterpret_cast<const PoaJob*>(dg + s_jobs), static_cast<int>(nj), score,
+                                  reinterpret_cast<uint8_t*>(dg), prep_rows, A.stream));
   PoaLaunch pl{};
   pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
   pl.n_jobs = static_cast<int>(nj);
@@ -586,6 +648,28 @@ uint8_t prep_task(PoaTask& t, const svs_poa_config& cfg, PoaArena* stage) {
   return 2;
 }
 
+// SVS_POA_VERIFY_PREP=1: the device-completed tables of a finished launch
+// against the host's full export of the same graphs (still unfolded).
+void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks) {
+  const PoaArena& A = *la.arena;
+  for (size_t k = 0; k < la.ids.size(); ++k) {
+    const PoaJob& J = la.jobs[k];
+    if (!(J.prep & 1u)) continue;
+    PoaTask& t = tasks[la.ids[k]];
+    RowTables h;
+    t.graph.export_strip_rows(&h, la.gaps);
+    const uint32_t V = J.n_rows, E = static_cast<uint32_t>(h.pred_row.size());
+    std::vector<uint32_t> rec(4ull * V), ps(E);
+    std::vector<int32_t> c0(3ull * V);
+    const char* d = A.d_in.as<char>();
+    SVS_HIP(hipMemcpy(rec.data(), d + 16ull * J.rec_off, rec.size() * 4, hipMemcpyDeviceToHost));
+    if (E) SVS_HIP(hipMemcpy(ps.data(), d + 4ull * J.pslot_off, ps.size() * 4, hipMemcpyDeviceToHost));
+    SVS_HIP(hipMemcpy(c0.data(), d + 12ull * J.row_off, c0.size() * 4, hipMemcpyDeviceToHost));
+    if (rec != h.rec || ps != h.pred_slot || c0 != h.col0 || h.n_slots != t.rows.n_slots)
+      throw SvsError(SVS_E_INTERNAL, "device strip tables differ from the host export (job " + std::to_string(k) + ")");
+  }
+}
+
 // Waits for the launch and folds its alignments back into the graphs, each
 // task's next step readied right after its fold while its graph is in cache
 // (prep_task; PoaTask::prepped).  While
@@ -616,6 +700,13 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   float ms = 0.f;
   SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
   st.kernel_ms += ms;
+  if (la.prep_jobs > 0) {
+    float pms = 0.f;
+    SVS_HIP(hipEventElapsedTime(&pms, A.evp, A.ev0));
+    st.prep_ms += pms;
+    st.prep_jobs += la.prep_jobs;
+    if (verify_prep()) verify_prep_tables(la, tasks);
+  }
   if (g_trace.f) {
     uint64_t cells = 0;
     for (const PoaJob& J : la.jobs) cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);

@@ -112,6 +112,11 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_WIDE": "1", "SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_WPJ": "4"},
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "none"},
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "-0.3", "SVS_POA_PRUNE_MAX_RETRIES": "100"},
+    {"SVS_POA_VERIFY_PREP": "1"},
+    {"SVS_POA_VERIFY_PREP": "1", "SVS_POA_WPJ": "1"},
+    {"SVS_POA_VERIFY_PREP": "1", "SVS_POA_PRUNE_SLACK": "-0.3"},
+    {"SVS_POA_VERIFY_PREP": "1", "SVS_POA_WIDE": "1"},
+    {"SVS_POA_DEVICE_PREP": "0"},
     {"SVS_POA_STAGING": "vec"},
     {"SVS_POA_STAGING": "vec", "SVS_POA_PRUNE_SLACK": "-0.3"},
 ])
@@ -124,7 +129,10 @@ def test_kernel_variants_match_oracle(env):
     twice, the second time unpruned; with the tables exported straight
     into the staging buffer a retried job's block is exported again), and with
     the tables packed from per-task vectors (SVS_POA_STAGING=vec); and all of
-    that again with 128-column strips after strip 0 (SVS_POA_WIDE=1)."""
+    that again with 128-column strips after strip 0 (SVS_POA_WIDE=1); with the
+    row tables completed on the device checked table for table against the
+    host's export (SVS_POA_VERIFY_PREP=1), and with the host export only
+    (SVS_POA_DEVICE_PREP=0)."""
     import os
     from svscope_amd import synth
     from svscope_amd.poa import poa_batch
@@ -168,6 +176,7 @@ def test_pruning_stats_and_exactness(slack, retries):
         assert st["prune_retries"] > 0
     else:
         assert st["cells_computed"] < 0.6 * st["dp_cells"], st
+    assert st["prep_jobs"] > 0, st  # the device completed the row tables
 
 
 def test_wide_slot_jobs_share_pruned_launches():
@@ -183,15 +192,17 @@ def test_wide_slot_jobs_share_pruned_launches():
     small = [synth.make_window(w, 8, 900)[0] for w in range(10, 14)]
     small += helpers.random_cases(77, 20, max_seqs=10, max_len=260, edits=20)
     cases = [c for pair in zip(small[:2], wide) for c in pair] + small[2:]
-    old = os.environ.get("SVS_POA_TEST_WIDE_SLOTS")
-    os.environ["SVS_POA_TEST_WIDE_SLOTS"] = "1500"
+    env = {"SVS_POA_TEST_WIDE_SLOTS": "1500", "SVS_POA_VERIFY_PREP": "1"}  # device planner from slot 40 too
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         got, st = poa_batch(cases, return_stats=True)
     finally:
-        if old is None:
-            os.environ.pop("SVS_POA_TEST_WIDE_SLOTS", None)
-        else:
-            os.environ["SVS_POA_TEST_WIDE_SLOTS"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     for seqs, g in zip(cases, got):
         assert g == oracle_poa(seqs, 1)
     assert st["cells_computed"] < st["dp_cells"], st  # the bounded jobs were pruned
