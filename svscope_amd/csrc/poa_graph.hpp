@@ -171,7 +171,8 @@ inline StripBlock strip_block_lite(uint32_t V, uint32_t E, uint32_t ls) {
   return b;
 }
 // Device-side output region of such a job: column 0 (12 V), records (16 V),
-// in-edge slots (4 E); starts at a multiple of 48.
+// in-edge slots (4 E, rounded to 16 B), then the device planner's scratch
+// (3 words per row, rows rounded to 4); starts at a multiple of 48.
 inline StripBlock strip_prep_out_layout(uint32_t V, uint32_t E) {
   StripBlock b{};
   size_t o = 0;
@@ -180,7 +181,8 @@ inline StripBlock strip_prep_out_layout(uint32_t V, uint32_t E) {
   b.rec = o;
   o += 16ull * V;
   b.pred_slot = o;
-  o += 4ull * E;
+  o += 4ull * ((E + 3u) & ~3u);
+  o += 12ull * ((V + 3u) & ~3u);
   b.bytes = (o + 47) / 48 * 48;
   return b;
 }

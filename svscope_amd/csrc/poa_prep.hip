@@ -6,16 +6,19 @@
 // path lengths of w2.  The tables come out identical to the host's; the
 // engine can check that (SVS_POA_VERIFY_PREP=1, svs_poa_engine.cpp).
 //
-// One wave per job.  The row loops are sequential, as on the host (a slot is
-// handed out from a LIFO free list in rank order; path lengths are a backward
-// DP over the rows), so the wave runs them in lockstep with uniform values:
-//  * inputs come through LDS, 64 rows (and their in-edges) per chunk, loaded
-//    by all lanes with coalesced loads;
-//  * per row, one LDS word holds slot | fewest nodes from a source << 16 in
-//    the forward pass, then fewest | most nodes to a sink << 16 backwards;
+// Three waves per job, one per sequential pass (a slot is handed out from a
+// LIFO free list in rank order; the path lengths are forward and backward DPs
+// over the rows), each running its row loop in lockstep with uniform values:
+//  * inputs come in chunks of 64 rows, loaded by all lanes with coalesced
+//    loads one chunk ahead, held in VGPRs (lane i = row r0 + i; the chunk's
+//    first 128 in-edges likewise) and read with v_readlane;
+//  * the chunk in use keeps its per-row words in a VGPR; finished chunks go to
+//    a per-job scratch area for the rarer references further back;
 //  * the free list lives in one VGPR (lane i = entry i, <= 64 entries,
 //    host-checked), the row outputs of a chunk in VGPR lanes, stored once per
 //    chunk.
+// No LDS, so the kernel can share CUs with the other group's DP kernel
+// (SVS_POA_PREP_STREAM=1).
 // Column 0 follows from the fewest-nodes distance sd alone: with e, c <= 0
 // (host-checked) F0 = g + sd e and O0 = q + sd c.
 #include <hip/hip_runtime.h>
@@ -29,18 +32,36 @@ namespace svs {
 namespace {
 
 constexpr uint32_t kChunk = 64;
-constexpr uint32_t kChunkEdges = kChunk * 31;  // in-degree <= 31 (host-checked)
+constexpr uint32_t kRegEdges = 128;  // in-edges of a chunk held in two VGPRs; more spill to LDS
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t l) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(v), static_cast<int32_t>(l)));
+}
 // lane l of `old` replaced by v (l uniform): one compare and one select
-__device__ __forceinline__ int32_t set_lane(int32_t v, uint32_t l, int32_t old) {
-  return threadIdx.x == l ? v : old;
+__device__ __forceinline__ uint32_t set_lane(uint32_t v, uint32_t l, uint32_t old) {
+  return (threadIdx.x & 63u) == l ? v : old;
 }
 
-__global__ __launch_bounds__(64) void poa_strip_prep_kernel(const PoaJob* __restrict__ jobs, PoaScore P,
-                                                           uint8_t* __restrict__ base) {
-  extern __shared__ uint32_t lds[];
-  const uint32_t lane = threadIdx.x;
+// One chunk of rows r0 .. r0 + n - 1 in registers: lane i holds row r0 + i's
+// in-edge start and per-row word, and in-edges e0 + i, e0 + 64 + i (further
+// in-edges of a chunk are read from memory).  Loaded one chunk ahead.
+struct Chunk {
+  uint32_t r0, n, e0, e1;
+  uint32_t ps, info, ea, eb;
+};
+
+// Three waves per job, one per independent sequential pass:
+//  wave 0: pool slots (LIFO free list), record words w0, w1, w3, in-edge slots;
+//  wave 1: fewest nodes from a source (sd) -> column 0;
+//  wave 2: fewest / most nodes to a sink (backwards) -> record word w2.
+// Each keeps the words of its current chunk in a VGPR and writes finished
+// chunks to a per-job scratch area (`scr`, 3 words per row) that the rare
+// references further back read.
+__global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __restrict__ jobs, PoaScore P,
+                                                            uint8_t* __restrict__ base) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = uni(threadIdx.x >> 6);
   const PoaJob J = jobs[blockIdx.x];
   if (!(J.prep & 1u)) return;
   const uint32_t V = J.n_rows;
@@ -50,140 +71,172 @@ __global__ __launch_bounds__(64) void poa_strip_prep_kernel(const PoaJob* __rest
   uint32_t* __restrict__ rec = reinterpret_cast<uint32_t*>(base) + 4ull * J.rec_off;
   uint32_t* __restrict__ pslot = reinterpret_cast<uint32_t*>(base) + J.pslot_off;
   int32_t* __restrict__ c0 = reinterpret_cast<int32_t*>(base) + 3ull * J.row_off;
-  uint32_t* state = lds;                         // V words
-  uint32_t* cps = lds + ((V + 3u) & ~3u);        // kChunk + 1 words
-  uint32_t* cinfo = cps + kChunk + 4;            // kChunk words
-  uint32_t* cedge = cinfo + kChunk;              // <= kChunkEdges words
+  // this wave's scratch words, one per row (after the job's in-edge slots)
+  uint32_t* scr = reinterpret_cast<uint32_t*>(base) + J.pslot_off + ((uni(gps[V]) + 3u) & ~3u) +
+                  static_cast<uint64_t>(wave) * ((V + 3u) & ~3u);
+  const uint32_t E = uni(gps[V]);
 
-  // rows r0 .. r0 + n - 1 with their in-edges into LDS; returns n
-  auto load_chunk = [&](uint32_t r0) -> uint32_t {
-    const uint32_t n = min(kChunk, V - r0);
-    __syncthreads();  // the previous chunk's reads are done
-    if (lane < n) {
-      cps[lane] = gps[r0 + lane];
-      cinfo[lane] = ginfo[r0 + lane];
-    }
-    if (lane == 0) cps[n] = gps[r0 + n];
-    __syncthreads();
-    const uint32_t e0 = uni(cps[0]), e1 = uni(cps[n]);
-    for (uint32_t x = e0 + lane; x < e1; x += 64) cedge[x - e0] = gpr[x];
-    __syncthreads();
-    return n;
+  auto load = [&](uint32_t r0) -> Chunk {
+    Chunk c;
+    c.r0 = r0;
+    c.n = min(kChunk, V - r0);
+    c.e0 = uni(gps[r0]);
+    c.e1 = uni(gps[r0 + c.n]);
+    c.ps = lane < c.n ? gps[r0 + lane] : 0u;
+    c.info = lane < c.n ? ginfo[r0 + lane] : 0u;
+    c.ea = c.e0 + lane < c.e1 ? gpr[c.e0 + lane] : 0u;
+    c.eb = c.e0 + 64 + lane < c.e1 ? gpr[c.e0 + 64 + lane] : 0u;
+    return c;
+  };
+  auto edge = [&](const Chunk& c, uint32_t x) -> uint32_t {
+    const uint32_t i = x - c.e0;
+    if (i < 64) return lane_of(c.ea, i);
+    if (i < kRegEdges) return lane_of(c.eb, i - 64);
+    return uni(gpr[x]);
+  };
+  auto pstart_of = [&](const Chunk& c, uint32_t i) -> uint32_t { return i < c.n ? lane_of(c.ps, i) : c.e1; };
+  // scratch is read back by the wave that wrote it, past the vector L1 (which
+  // may hold a line from before the store)
+  auto ld = [](const uint32_t* p) -> uint32_t {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto flush_fence = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
-  // forward: pool slots, records w0/w1/w3, in-edge slots, column 0
-  uint32_t next = J.prep >> 1, fsp = 0;
-  int32_t fstack = 0;               // free list: lane i = entry i
-  uint32_t sd_prev = 0;             // sd of the row just above
-  int32_t ebuf = 0;                 // in-edge slots of edges ebase + lane
-  uint32_t ebase = 0;
-  for (uint32_t r0 = 0; r0 < V; r0 += kChunk) {
-    const uint32_t n = load_chunk(r0);
-    const uint32_t e0 = uni(cps[0]);
-    int32_t ow0 = 0, ow1 = 0, ow3 = 0, osd = 0;  // rows r0 + lane
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t r = r0 + i;
-      const uint32_t a = uni(cps[i]), b = uni(cps[i + 1]);
-      const uint32_t inf = uni(cinfo[i]);
-      uint32_t own = kNoSlot;
-      if ((inf >> 9) & 1u) {
-        if (fsp != 0) {
-          --fsp;
-          own = uni(static_cast<uint32_t>(__builtin_amdgcn_readlane(fstack, static_cast<int>(fsp))));
-        } else {
-          own = next++;
+  if (wave == 0) {
+    // pool slots, record words w0 w1 w3, in-edge slots
+    uint32_t next = J.prep >> 1, fsp = 0;
+    uint32_t fstack = 0;  // free list: lane i = entry i
+    uint32_t ebuf = 0, ebase = 0;  // in-edge slots of edges ebase + lane
+    Chunk cur = load(0);
+    for (;;) {
+      const Chunk nxt = cur.r0 + kChunk < V ? load(cur.r0 + kChunk) : cur;
+      uint32_t win = 0;  // lane i: pool slot of row r0 + i
+      uint32_t ow0 = 0, ow1 = 0, ow3 = 0;
+      for (uint32_t i = 0; i < cur.n; ++i) {
+        const uint32_t r = cur.r0 + i;
+        const uint32_t a = pstart_of(cur, i), b = pstart_of(cur, i + 1);
+        const uint32_t inf = lane_of(cur.info, i);
+        uint32_t own = kNoSlot;
+        if ((inf >> 9) & 1u) {
+          if (fsp != 0) own = lane_of(fstack, --fsp);
+          else own = next++;
         }
+        uint32_t w1 = 0, w3 = 0;
+        for (uint32_t x = a; x < b; ++x) {
+          const uint32_t pe = edge(cur, x);
+          const uint32_t pr = (pe & 0x7FFFFFFFu) - 1;
+          uint32_t ps = kNoSlot;
+          if (pr + 1 != r) ps = pr >= cur.r0 ? lane_of(win, pr - cur.r0) : uni(ld(scr + pr));
+          if (x - ebase == 64) {
+            pslot[ebase + lane] = ebuf;
+            ebase += 64;
+          }
+          ebuf = set_lane(ps, x - ebase, ebuf);
+          if (x - a < kInlinePreds) w1 |= ps << (16 * (x - a));
+          if (pe >> 31) {  // this row is the tail row's last pool reader: its slot is free again
+            fstack = set_lane(ps, fsp++, fstack);
+            if (ps < 31u) w3 |= 1u << ps;
+          }
+        }
+        win = set_lane(own, i, win);
+        ow0 = set_lane(inf | (own << 16), i, ow0);
+        ow1 = set_lane(w1, i, ow1);
+        ow3 = set_lane(w3, i, ow3);
       }
-      uint32_t w1 = 0, w3 = 0, sd = 0xFFFFu;
-      for (uint32_t x = a; x < b; ++x) {
-        const uint32_t pe = uni(cedge[x - e0]);
-        const uint32_t pr = (pe & 0x7FFFFFFFu) - 1;
-        uint32_t ps, sdp;
-        if (pr + 1 == r) {
-          ps = kNoSlot;
-          sdp = sd_prev;
-        } else {
-          const uint32_t v = uni(state[pr]);
-          ps = v & 0xFFFFu;
-          sdp = v >> 16;
-        }
-        if (x - ebase == 64) {
-          pslot[ebase + lane] = static_cast<uint32_t>(ebuf);
-          ebase += 64;
-        }
-        ebuf = set_lane(static_cast<int32_t>(ps), x - ebase, ebuf);
-        if (x - a < kInlinePreds) w1 |= ps << (16 * (x - a));
-        if (pe >> 31) {  // this row is the tail row's last pool reader: its slot is free again
-          fstack = set_lane(static_cast<int32_t>(ps), fsp, fstack);
-          ++fsp;
-          if (ps < 31u) w3 |= 1u << ps;
-        }
-        sd = min(sd, sdp + 1);
+      if (lane < cur.n) {
+        const uint64_t r = cur.r0 + lane;
+        scr[r] = win;
+        *reinterpret_cast<uint2*>(rec + 4 * r) = make_uint2(ow0, ow1);
+        rec[4 * r + 3] = ow3;
       }
-      if (a == b) sd = 0;  // a source
-      if (lane == 0) state[r] = own | (sd << 16);
-      sd_prev = sd;
-      ow0 = set_lane(static_cast<int32_t>(inf | (own << 16)), i, ow0);
-      ow1 = set_lane(static_cast<int32_t>(w1), i, ow1);
-      ow3 = set_lane(static_cast<int32_t>(w3), i, ow3);
-      osd = set_lane(static_cast<int32_t>(sd), i, osd);
+      flush_fence();
+      if (cur.r0 + kChunk >= V) break;
+      cur = nxt;
     }
-    if (lane < n) {
-      const uint64_t r = r0 + lane;
-      *reinterpret_cast<uint4*>(rec + 4 * r) =
-          make_uint4(static_cast<uint32_t>(ow0), static_cast<uint32_t>(ow1), 0u, static_cast<uint32_t>(ow3));
-      const int32_t F0 = P.g + osd * P.e, O0 = P.q + osd * P.c;
-      c0[3 * r] = F0 > O0 ? F0 : O0;
-      c0[3 * r + 1] = F0;
-      c0[3 * r + 2] = O0;
-    }
-  }
-  {
-    const uint32_t E = uni(gps[V]);
-    if (ebase + lane < E) pslot[ebase + lane] = static_cast<uint32_t>(ebuf);
-  }
-
-  // backward: fewest / most nodes on a path to a sink (record word w2); every
-  // out-edge leads to a higher rank, so a row is final when the scan reaches it
-  __syncthreads();
-  for (uint32_t r = lane; r < V; r += 64) state[r] = 0xFFFFu;  // lo 0xFFFF (none seen), hi 0
-  for (uint32_t r0 = (V - 1) / kChunk * kChunk;; r0 -= kChunk) {
-    const uint32_t n = load_chunk(r0);
-    const uint32_t e0 = uni(cps[0]);
-    int32_t ow2 = 0;
-    for (uint32_t i = n; i-- > 0;) {
-      const uint32_t r = r0 + i;
-      const uint32_t v = uni(state[r]);
-      uint32_t lo = v & 0xFFFFu;
-      const uint32_t hi = v >> 16;
-      if ((uni(cinfo[i]) >> 8) & 1u) lo = 0;  // a sink
-      const uint32_t l1 = min(lo + 1, 0xFFFFu), h1 = min(hi + 1, 0xFFFFu);
-      const uint32_t a = uni(cps[i]), b = uni(cps[i + 1]);
-      for (uint32_t x = a; x < b; ++x) {
-        const uint32_t p = (uni(cedge[x - e0]) & 0x7FFFFFFFu) - 1;
-        const uint32_t pv = uni(state[p]);
-        const uint32_t plo = min(pv & 0xFFFFu, l1), phi = max(pv >> 16, h1);
-        if (lane == 0) state[p] = plo | (phi << 16);
+    if (ebase + lane < E) pslot[ebase + lane] = ebuf;
+  } else if (wave == 1) {
+    // fewest nodes from a source -> column 0: F0 = g + sd e, O0 = q + sd c
+    uint32_t sd_prev = 0;
+    Chunk cur = load(0);
+    for (;;) {
+      const Chunk nxt = cur.r0 + kChunk < V ? load(cur.r0 + kChunk) : cur;
+      uint32_t win = 0;  // lane i: sd of row r0 + i
+      for (uint32_t i = 0; i < cur.n; ++i) {
+        const uint32_t r = cur.r0 + i;
+        const uint32_t a = pstart_of(cur, i), b = pstart_of(cur, i + 1);
+        uint32_t sd = a == b ? 0u : 0xFFFFu;  // a source: 0
+        for (uint32_t x = a; x < b; ++x) {
+          const uint32_t pr = (edge(cur, x) & 0x7FFFFFFFu) - 1;
+          const uint32_t sdp = pr + 1 == r ? sd_prev : (pr >= cur.r0 ? lane_of(win, pr - cur.r0) : uni(ld(scr + pr)));
+          sd = min(sd, sdp + 1);
+        }
+        sd_prev = sd;
+        win = set_lane(sd, i, win);
       }
-      ow2 = set_lane(static_cast<int32_t>(lo | (hi << 16)), i, ow2);
+      if (lane < cur.n) {
+        const uint64_t r = cur.r0 + lane;
+        scr[r] = win;
+        const int32_t F0 = P.g + static_cast<int32_t>(win) * P.e, O0 = P.q + static_cast<int32_t>(win) * P.c;
+        c0[3 * r] = F0 > O0 ? F0 : O0;
+        c0[3 * r + 1] = F0;
+        c0[3 * r + 2] = O0;
+      }
+      flush_fence();
+      if (cur.r0 + kChunk >= V) break;
+      cur = nxt;
     }
-    if (lane < n) rec[4ull * (r0 + lane) + 2] = static_cast<uint32_t>(ow2);
-    if (r0 == 0) break;
+  } else {
+    // fewest / most nodes to a sink (record word w2); every out-edge leads to
+    // a higher rank, so a row is final when the scan reaches it.  Pushes into
+    // rows of the chunk in use go to its register window, pushes into earlier
+    // chunks to scratch (picked up when that chunk's turn comes).
+    for (uint32_t r = lane; r < V; r += 64) scr[r] = 0xFFFFu;  // lo 0xFFFF (none seen), hi 0
+    flush_fence();
+    Chunk cur = load((V - 1) / kChunk * kChunk);
+    for (;;) {
+      const Chunk nxt = cur.r0 > 0 ? load(cur.r0 - kChunk) : cur;
+      uint32_t win = lane < cur.n ? ld(scr + cur.r0 + lane) : 0xFFFFu;
+      uint32_t ow2 = 0;
+      for (uint32_t i = cur.n; i-- > 0;) {
+        const uint32_t v = lane_of(win, i);
+        uint32_t lo = v & 0xFFFFu;
+        const uint32_t hi = v >> 16;
+        if ((lane_of(cur.info, i) >> 8) & 1u) lo = 0;  // a sink
+        const uint32_t l1 = min(lo + 1, 0xFFFFu), h1 = min(hi + 1, 0xFFFFu);
+        const uint32_t a = pstart_of(cur, i), b = pstart_of(cur, i + 1);
+        for (uint32_t x = a; x < b; ++x) {
+          const uint32_t p = (edge(cur, x) & 0x7FFFFFFFu) - 1;
+          if (p >= cur.r0) {
+            const uint32_t pv = lane_of(win, p - cur.r0);
+            win = set_lane(min(pv & 0xFFFFu, l1) | (max(pv >> 16, h1) << 16), p - cur.r0, win);
+          } else {
+            const uint32_t pv = uni(ld(scr + p));
+            if (lane == 0) scr[p] = min(pv & 0xFFFFu, l1) | (max(pv >> 16, h1) << 16);
+            flush_fence();
+          }
+        }
+        ow2 = set_lane(lo | (hi << 16), i, ow2);
+      }
+      if (lane < cur.n) rec[4ull * (cur.r0 + lane) + 2] = ow2;
+      if (cur.r0 == 0) break;
+      cur = nxt;
+    }
   }
 }
 
 }  // namespace
 
-size_t strip_prep_lds_bytes(uint32_t max_rows) {
-  return 4ull * (((max_rows + 3u) & ~3u) + kChunk + 4 + kChunk + kChunkEdges);
-}
+size_t strip_prep_scratch_words(uint32_t V) { return 3ull * ((V + 3u) & ~3u); }
 
 hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore& score, uint8_t* base,
                                  uint32_t max_rows, hipStream_t stream) {
   if (n_jobs <= 0) return hipSuccess;
   if (max_rows > kStripPrepMaxRows) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(poa_strip_prep_kernel, dim3(n_jobs), dim3(64), strip_prep_lds_bytes(max_rows), stream, jobs,
-                     score, base);
+  hipLaunchKernelGGL(poa_strip_prep_kernel, dim3(n_jobs), dim3(192), 0, stream, jobs, score, base);
   return hipGetLastError();
 }
 

@@ -112,7 +112,8 @@ struct PoaArena {
   hipStream_t copy_stream = nullptr;  // this group's copies
   bool own = false;                   // stream is this group's, copies ride on it too
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr, h2d = nullptr;
-  hipEvent_t evp = nullptr;  // start of the launch's poa_strip_prep_kernel (ends at ev0)
+  hipEvent_t evp = nullptr, evp1 = nullptr;  // around the launch's poa_strip_prep_kernel
+  hipStream_t prep_stream = nullptr;          // SVS_POA_PREP_STREAM=1: that kernel's own stream
   // Staging of the next launch's strip tables in h_in: the fold exports each
   // job's tables straight into a block claimed with an atomic bump (st_cur), so
   // packing the launch copies nothing.  A new generation (st_gen) starts when
@@ -136,6 +137,8 @@ struct PoaArena {
     SVS_HIP(hipEventCreate(&ev0));
     SVS_HIP(hipEventCreate(&ev1));
     SVS_HIP(hipEventCreate(&evp));
+    SVS_HIP(hipEventCreate(&evp1));
+    SVS_HIP(hipStreamCreateWithFlags(&prep_stream, hipStreamNonBlocking));
     SVS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
     SVS_HIP(hipEventCreateWithFlags(&h2d, hipEventDisableTiming));
   }
@@ -147,6 +150,11 @@ struct PoaArena {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (evp) (void)hipEventDestroy(evp);
+    if (evp1) (void)hipEventDestroy(evp1);
+    if (prep_stream) {
+      (void)hipStreamSynchronize(prep_stream);
+      (void)hipStreamDestroy(prep_stream);
+    }
     if (done) (void)hipEventDestroy(done);
     if (h2d) (void)hipEventDestroy(h2d);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);  // == stream when own

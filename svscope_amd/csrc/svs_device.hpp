@@ -87,9 +87,9 @@ hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream);
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream);
 // Device half of the strip row export (poa_prep.hip) for the jobs with
 // PoaJob::prep bit 0; every offset of those jobs indexes `base`.
-constexpr uint32_t kStripPrepMaxRows = 16384;  // rows of a prep job (LDS: 4 B per row)
+constexpr uint32_t kStripPrepMaxRows = 16384;  // rows of a prep job (16-bit path lengths and slots)
 constexpr uint32_t kStripPrepMaxSlots = 64;    // pool slots of a prep job (free list in one VGPR)
-size_t strip_prep_lds_bytes(uint32_t max_rows);
+size_t strip_prep_scratch_words(uint32_t n_rows);  // after the job's in-edge slots (rounded to 4)
 hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore& score, uint8_t* base,
                                  uint32_t max_rows, hipStream_t stream);
 int choose_strip_wpj(int device, size_t n_jobs, uint32_t lds_slots, uint32_t min_strips);

@@ -460,10 +460,21 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   SVS_HIP(hipMemcpyAsync(dg, hs, off, hipMemcpyHostToDevice, A.copy_stream));
   SVS_HIP(hipEventRecord(A.h2d, A.copy_stream));
   SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
-  SVS_HIP(hipEventRecord(A.evp, A.stream));
-  if (n_prep > 0)
+  if (n_prep > 0) {
+    // on the kernel stream, or (SVS_POA_PREP_STREAM=1) on a stream of its own
+    // so that it can run beside the other group's DP kernel
+    static const bool own = [] {
+      const char* e = std::getenv("SVS_POA_PREP_STREAM");
+      return e && std::string(e) == "1";
+    }();
+    hipStream_t ps = own ? A.prep_stream : A.stream;
+    if (own) SVS_HIP(hipStreamWaitEvent(ps, A.h2d, 0));
+    SVS_HIP(hipEventRecord(A.evp, ps));
     SVS_HIP(launch_poa_strip_prep(reinterpret_cast<const PoaJob*>(dg + s_jobs), static_cast<int>(nj), score,
-                                  reinterpret_cast<uint8_t*>(dg), prep_rows, A.stream));
+                                  reinterpret_cast<uint8_t*>(dg), prep_rows, ps));
+    SVS_HIP(hipEventRecord(A.evp1, ps));
+    if (own) SVS_HIP(hipStreamWaitEvent(A.stream, A.evp1, 0));
+  }
   PoaLaunch pl{};
   pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
   pl.n_jobs = static_cast<int>(nj);
@@ -702,7 +713,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   st.kernel_ms += ms;
   if (la.prep_jobs > 0) {
     float pms = 0.f;
-    SVS_HIP(hipEventElapsedTime(&pms, A.evp, A.ev0));
+    SVS_HIP(hipEventElapsedTime(&pms, A.evp, A.evp1));
     st.prep_ms += pms;
     st.prep_jobs += la.prep_jobs;
     if (verify_prep()) verify_prep_tables(la, tasks);
