@@ -296,7 +296,16 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(cells_done * BYTES_PER_CELL / max(1, launches)),
-                         "mean_launch_ms": round(kms / max(1, launches), 4)},
+                         "mean_launch_ms": round(kms / max(1, launches), 4),
+                         # SURVEY.md §8(d) prices Σcells over every DP cell of spoa's full
+                         # matrix (its "50 % needs ~2e11 cells/s, ~100 windows/s");
+                         # frac above counts only the cells the pruned kernel evaluates
+                         "all_dp_cells": {"achieved": round(cells * BYTES_PER_CELL / (kms * 1e-3) / 1e9, 2)
+                                          if kms else None,
+                                          "frac": round(cells * BYTES_PER_CELL / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                                          if kms else None,
+                                          "note": "every DP cell of the full matrix; above 1 because exact "
+                                                  "pruning skips most cells, so not an HBM-traffic figure"}},
             "cpu_baseline": cpu,
             "breakdown": {"poa_cells": cells, "poa_cells_computed": cells_done,
                           "prune_retries": poa["prune_retries"],

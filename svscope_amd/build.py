@@ -55,9 +55,9 @@ def _compile(src):
     cmd = [_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
            "-Wall", "-Wno-unused-result", "-c", path, "-o", obj]
     if not src.endswith(".hip"):
-        # host-only translation units: no device code, skip the offload step
+        # host-only translation units: no device code, no device pass at all
         cmd = [_hipcc(), "-O3", "-std=c++17", "-fPIC", "-Wall", "-D__HIP_PLATFORM_AMD__",
-               "-c", path, "-o", obj]
+               "--offload-host-only", "-c", path, "-o", obj]
     subprocess.check_call(cmd)
     return obj
 

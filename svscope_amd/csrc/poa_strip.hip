@@ -66,17 +66,17 @@ __device__ __forceinline__ uint32_t pack_fo(int32_t H, int32_t F, int32_t O, uin
 }
 
 // d = (lane > 0 ? a[lane-1] : d) + b, one DPP-combined VALU op (wave_shr:1
-// leaves lane 0 unwritten; the caller preloads d with lane 0's value).
+// leaves lane 0 unwritten; the caller preloads d with lane 0's value).  Kept
+// in asm: the builtin form needs a separate move of d into the destination
+// (update_dpp's "old" is not the identity of the add), one VALU more per call.
 __device__ __forceinline__ int32_t shr1_add(int32_t d, int32_t a, int32_t b) {
   asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(d) : "v"(a), "v"(b));
   return d;
 }
-// d = (lane > 0 ? a[lane-1] : 0) + b (bound_ctrl: lane 0 reads zero).
+// d = (lane > 0 ? a[lane-1] : 0) + b: wave_shr:1 with bound_ctrl (lane 0
+// reads zero), which the compiler folds into one v_add_u32_dpp.
 __device__ __forceinline__ int32_t shr1_add_bc(int32_t a, int32_t b) {
-  int32_t d;
-  asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
-               : "=v"(d) : "v"(a), "v"(b));
-  return d;
+  return __builtin_amdgcn_update_dpp(0, a, 0x138, 0xF, 0xF, true) + b;
 }
 
 // Lane constants of one strip (columns j = j0 + lane, j0 > 0) for the
@@ -396,7 +396,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
 
     auto fetch = [&](RowIn& d, uint32_t r) {
       const uint32_t rr = r < V ? r : V - 1;
-      const uint32_t* w = rec + static_cast<uint64_t>(rr) * kRecWords;
+      const uint32_t* w = rec + rr * kRecWords;  // 32-bit: a job has < 2^30 rows
       d.w0 = w[0];
       d.w1 = w[1];
       if constexpr (PRUNE) {
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
 #endif
           }
         }
-        const int4 v = *reinterpret_cast<const int4*>(bin + 4ull * rr);
+        const int4 v = *reinterpret_cast<const int4*>(bin + 4u * rr);
         d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
       }
     };
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
           pr_slow += 1;
 #endif
           if (write_bnd && lane == 0)
-            *reinterpret_cast<int4*>(bout + 4ull * r) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
+            *reinterpret_cast<int4*>(bout + 4u * r) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
           publish();
           return;
         }
@@ -706,7 +706,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       } else
 #endif
       if (write_bnd && lane == 0) {
-        *reinterpret_cast<int4*>(bout + 4ull * r) =
+        *reinterpret_cast<int4*>(bout + 4u * r) =
             any_alive ? make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH) : make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
       }
       publish();
@@ -861,7 +861,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
 
     auto fetch = [&](RowIn& d, uint32_t r) {
       const uint32_t rr = r < V ? r : V - 1;
-      const uint32_t* w = rec + static_cast<uint64_t>(rr) * kRecWords;
+      const uint32_t* w = rec + rr * kRecWords;  // 32-bit: a job has < 2^30 rows
       d.w0 = w[0];
       d.w1 = w[1];
       if constexpr (PRUNE) {
@@ -872,7 +872,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const int32_t need = need0 + static_cast<int32_t>(rr) + 1;
         if (avail < need) avail = strip_wait_ge(&prog[pw], need, &s_err);
       }
-      const int4 v = *reinterpret_cast<const int4*>(bin + 4ull * rr);
+      const int4 v = *reinterpret_cast<const int4*>(bin + 4u * rr);
       d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
     };
 
@@ -1001,7 +1001,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
           alive &= ~(__builtin_amdgcn_readfirstlane(d.w3) | own_bit | kRegBit);
           pHa = pHb = pFa = pFb = pOa = pOb = pHma = SVS_VNEG;
           if (write_bnd && lane == 0)
-            *reinterpret_cast<int4*>(bout + 4ull * r) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
+            *reinterpret_cast<int4*>(bout + 4u * r) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
           publish();
           return;
         }
@@ -1138,7 +1138,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       pOb = Ob;
       pHma = A_.prevH;
       if (write_bnd && lane == 0) {
-        *reinterpret_cast<int4*>(bout + 4ull * r) =
+        *reinterpret_cast<int4*>(bout + 4u * r) =
             any_alive ? make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH) : make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
       }
       publish();

@@ -15,54 +15,45 @@ namespace svs {
 
 __device__ __forceinline__ int32_t imax(int32_t a, int32_t b) { return a > b ? a : b; }
 
-// Inclusive prefix max over the 64 lanes of a wave (DPP: row_shr 1/2/4/8,
-// then row_bcast15 / row_bcast31).  Lanes with no source keep the identity.
+// One step of an inclusive prefix-max scan: x = max(x, x[src lane]) as a
+// DPP-combined v_max_i32_dpp.  Lanes with no source (row_shr at a row's start)
+// or in a masked row read the identity INT32_MIN, so they keep x.  Written
+// with the builtin so that the compiler sees the DPP read-after-write hazard
+// (2 wait states on gfx950) and fills it with independent work instead of a
+// fixed s_nop.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int32_t dpp_max_step(int32_t x) {
+  return imax(x, __builtin_amdgcn_update_dpp(static_cast<int32_t>(INT32_MIN), x, CTRL, ROW_MASK, 0xF, false));
+}
+
+// Inclusive prefix max over the 64 lanes of a wave: row_shr 1/2/4/8 within
+// each 16-lane row, then row_bcast15 (rows 1, 3) and row_bcast31 (rows 2, 3).
 __device__ __forceinline__ int32_t wave_prefix_max(int32_t x) {
-  // v_max_i32_dpp x, x[src lane], x: lanes whose DPP source is out of range
-  // (BOUND_CTRL=0) or whose row is masked off are not written and keep x.
-  // Each step reads the previous step's VALU result: 2 wait states (s_nop 1),
-  // which hipcc does not insert inside asm.
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
-      : "+v"(x));
+  x = dpp_max_step<0x111, 0xF>(x);
+  x = dpp_max_step<0x112, 0xF>(x);
+  x = dpp_max_step<0x114, 0xF>(x);
+  x = dpp_max_step<0x118, 0xF>(x);
+  x = dpp_max_step<0x142, 0xA>(x);
+  x = dpp_max_step<0x143, 0xC>(x);
   return x;
 }
 
-// Two independent inclusive prefix-max scans, interleaved: each DPP step of
-// one scan is the other's wait state, so the pair costs 6 s_nop 0 instead of
-// 12 s_nop 1 and the two dependency chains overlap.
+// Two independent inclusive prefix-max scans, written step by step so that
+// the compiler interleaves the two dependency chains (each step of one scan
+// covers a wait state of the other).
 __device__ __forceinline__ void wave_prefix_max2(int32_t& a, int32_t& b) {
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
-      "v_max_i32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 0\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
-      "v_max_i32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 0\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_max_i32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 0\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
-      "v_max_i32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 0\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-      "v_max_i32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-      "s_nop 0\n\t"
-      "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
-      "v_max_i32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf"
-      : "+v"(a), "+v"(b));
+  a = dpp_max_step<0x111, 0xF>(a);
+  b = dpp_max_step<0x111, 0xF>(b);
+  a = dpp_max_step<0x112, 0xF>(a);
+  b = dpp_max_step<0x112, 0xF>(b);
+  a = dpp_max_step<0x114, 0xF>(a);
+  b = dpp_max_step<0x114, 0xF>(b);
+  a = dpp_max_step<0x118, 0xF>(a);
+  b = dpp_max_step<0x118, 0xF>(b);
+  a = dpp_max_step<0x142, 0xA>(a);
+  b = dpp_max_step<0x142, 0xA>(b);
+  a = dpp_max_step<0x143, 0xC>(a);
+  b = dpp_max_step<0x143, 0xC>(b);
 }
 
 // lane l <- x[l-1]; lane 0 <- fill (wave-uniform).  DPP wave_shr:1.

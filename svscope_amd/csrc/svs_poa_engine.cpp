@@ -290,7 +290,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   auto th0 = Clock::now();
   const size_t nj = la.ids.size();
   la.jobs.assign(nj, PoaJob{});
-  uint64_t n_rows = 0, n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
+  uint64_t n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
   uint32_t max_preds = 0, max_slots = 1;
   bool any_prune = false;
   PoaArena& A = *la.arena;
@@ -357,7 +357,6 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     J.lb = prune_bound(tasks[la.ids[k]], score, J.n_rows, J.len, penv);
     if (J.n_slots > 31) J.lb = kNoPrune;  // the kernel tracks slot liveness in 31 bits
     any_prune = any_prune || J.lb != kNoPrune;
-    n_rows += J.n_rows;
     n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
     n_bnd += round_up(round_up(J.n_rows, 8) * (J.ls / 64) * 4, 64);
     if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 97, 64);
