@@ -12,8 +12,10 @@
 //  * inputs come in chunks of 64 rows, loaded by all lanes with coalesced
 //    loads one chunk ahead, held in VGPRs (lane i = row r0 + i; the chunk's
 //    first 128 in-edges likewise) and read with v_readlane;
-//  * the chunk in use keeps its per-row words in a VGPR; finished chunks go to
-//    a per-job scratch area for the rarer references further back;
+//  * the chunk in use keeps its per-row words in a VGPR, and so does the chunk
+//    before it (the backward pass: the pushes pending for the chunk after
+//    it); finished chunks go to a per-job scratch area for the rarer
+//    references more than one chunk back;
 //  * the free list lives in one VGPR (lane i = entry i, <= 64 entries,
 //    host-checked), the row outputs of a chunk in VGPR lanes, stored once per
 //    chunk.
@@ -105,12 +107,23 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
+  // a word more than one chunk back (waves 0, 1): the scratch stores of the
+  // finished chunks are drained once, at the first such read after them
+  bool dirty = false;
+  auto far = [&](uint32_t x) -> uint32_t {
+    if (dirty) {
+      flush_fence();
+      dirty = false;
+    }
+    return uni(ld(scr + x));
+  };
 
   if (wave == 0) {
     // pool slots, record words w0 w1 w3, in-edge slots
     uint32_t next = J.prep >> 1, fsp = 0;
     uint32_t fstack = 0;  // free list: lane i = entry i
     uint32_t ebuf = 0, ebase = 0;  // in-edge slots of edges ebase + lane
+    uint32_t pwin = 0;             // lane i: pool slot of row r0 - 64 + i (the chunk before)
     Chunk cur = load(0);
     for (;;) {
       const Chunk nxt = cur.r0 + kChunk < V ? load(cur.r0 + kChunk) : cur;
@@ -130,7 +143,9 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
           const uint32_t pe = edge(cur, x);
           const uint32_t pr = (pe & 0x7FFFFFFFu) - 1;
           uint32_t ps = kNoSlot;
-          if (pr + 1 != r) ps = pr >= cur.r0 ? lane_of(win, pr - cur.r0) : uni(ld(scr + pr));
+          if (pr + 1 != r)
+            ps = pr >= cur.r0 ? lane_of(win, pr - cur.r0)
+                              : (pr + kChunk >= cur.r0 ? lane_of(pwin, pr + kChunk - cur.r0) : far(pr));
           if (x - ebase == 64) {
             pslot[ebase + lane] = ebuf;
             ebase += 64;
@@ -153,14 +168,16 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
         *reinterpret_cast<uint2*>(rec + 4 * r) = make_uint2(ow0, ow1);
         rec[4 * r + 3] = ow3;
       }
-      flush_fence();
+      dirty = true;
       if (cur.r0 + kChunk >= V) break;
+      pwin = win;
       cur = nxt;
     }
     if (ebase + lane < E) pslot[ebase + lane] = ebuf;
   } else if (wave == 1) {
     // fewest nodes from a source -> column 0: F0 = g + sd e, O0 = q + sd c
     uint32_t sd_prev = 0;
+    uint32_t pwin = 0;  // lane i: sd of row r0 - 64 + i (the chunk before)
     Chunk cur = load(0);
     for (;;) {
       const Chunk nxt = cur.r0 + kChunk < V ? load(cur.r0 + kChunk) : cur;
@@ -171,7 +188,11 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
         uint32_t sd = a == b ? 0u : 0xFFFFu;  // a source: 0
         for (uint32_t x = a; x < b; ++x) {
           const uint32_t pr = (edge(cur, x) & 0x7FFFFFFFu) - 1;
-          const uint32_t sdp = pr + 1 == r ? sd_prev : (pr >= cur.r0 ? lane_of(win, pr - cur.r0) : uni(ld(scr + pr)));
+          const uint32_t sdp =
+              pr + 1 == r ? sd_prev
+                          : (pr >= cur.r0 ? lane_of(win, pr - cur.r0)
+                                          : (pr + kChunk >= cur.r0 ? lane_of(pwin, pr + kChunk - cur.r0)
+                                                                   : far(pr)));
           sd = min(sd, sdp + 1);
         }
         sd_prev = sd;
@@ -185,21 +206,28 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
         c0[3 * r + 1] = F0;
         c0[3 * r + 2] = O0;
       }
-      flush_fence();
+      dirty = true;
       if (cur.r0 + kChunk >= V) break;
+      pwin = win;
       cur = nxt;
     }
   } else {
     // fewest / most nodes to a sink (record word w2); every out-edge leads to
     // a higher rank, so a row is final when the scan reaches it.  Pushes into
-    // rows of the chunk in use go to its register window, pushes into earlier
-    // chunks to scratch (picked up when that chunk's turn comes).
+    // rows of the chunk in use go to its register window, pushes into the
+    // chunk before it to a second register window (nwin), pushes further back
+    // to scratch (picked up when that chunk's turn comes).
     for (uint32_t r = lane; r < V; r += 64) scr[r] = 0xFFFFu;  // lo 0xFFFF (none seen), hi 0
     flush_fence();
+    auto merge = [](uint32_t a, uint32_t b) -> uint32_t {
+      return min(a & 0xFFFFu, b & 0xFFFFu) | (max(a >> 16, b >> 16) << 16);
+    };
     Chunk cur = load((V - 1) / kChunk * kChunk);
+    uint32_t nwin = 0xFFFFu;  // pushes into the chunk processed next (every chunk before the last is full)
     for (;;) {
       const Chunk nxt = cur.r0 > 0 ? load(cur.r0 - kChunk) : cur;
-      uint32_t win = lane < cur.n ? ld(scr + cur.r0 + lane) : 0xFFFFu;
+      uint32_t win = lane < cur.n ? merge(ld(scr + cur.r0 + lane), nwin) : 0xFFFFu;
+      nwin = 0xFFFFu;
       uint32_t ow2 = 0;
       for (uint32_t i = cur.n; i-- > 0;) {
         const uint32_t v = lane_of(win, i);
@@ -213,6 +241,10 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
           if (p >= cur.r0) {
             const uint32_t pv = lane_of(win, p - cur.r0);
             win = set_lane(min(pv & 0xFFFFu, l1) | (max(pv >> 16, h1) << 16), p - cur.r0, win);
+          } else if (p + kChunk >= cur.r0) {
+            const uint32_t q = p + kChunk - cur.r0;
+            const uint32_t pv = lane_of(nwin, q);
+            nwin = set_lane(min(pv & 0xFFFFu, l1) | (max(pv >> 16, h1) << 16), q, nwin);
           } else {
             const uint32_t pv = uni(ld(scr + p));
             if (lane == 0) scr[p] = min(pv & 0xFFFFu, l1) | (max(pv >> 16, h1) << 16);
