@@ -356,6 +356,10 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     int32_t avail = -1;                                  // producer progress seen so far
     const bool write_bnd = s + 1 < nstrips;
     const bool owns_L = strip_of(L) == s;
+    // rows left until the next whole 8-row carry line, where progress is
+    // published (the strip's last row after the row loop): a countdown
+    // instead of a test of r per row
+    uint32_t pub_left = 8;
     // pruning state of this strip: slot liveness bits (slots < 64, host-checked;
     // slot 0 = the virtual row 0, alive when row0_h + m (L - j) reaches lb at
     // some column j0-1 .. j0+63, i.e. at j0-1: it decreases along j), and the
@@ -444,9 +448,12 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       };
       const uint32_t own_bit = (store && own < 31u) ? 1u << own : 0u;
       auto publish = [&]() {
-        if (WPJ > 1 && write_bnd && ((r & 7u) == 7u || r + 1 == V) && lane == 0)
-          __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
-                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (WPJ > 1 && write_bnd && --pub_left == 0) {
+          pub_left = 8;
+          if (lane == 0)
+            __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       };
       const int32_t cH_in = FIRST ? SVS_VNEG : __builtin_amdgcn_readfirstlane(d.b3);
       if (prune) {
@@ -785,12 +792,14 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     RowIn A, B;
     uint32_t r = 0;
     if (prune) r = fast_forward(0);
+    pub_left = 8u - (r & 7u);
     fetch(A, r);
     fetch(B, r + 1);
     while (r < V) {
       step(r, A);
       if (prune && dead_strip()) {
         r = fast_forward(r + 1);
+        pub_left = 8u - (r & 7u);
         fetch(A, r);
         fetch(B, r + 1);
         continue;
@@ -800,6 +809,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       step(r + 1, B);
       if (prune && dead_strip()) {
         r = fast_forward(r + 2);
+        pub_left = 8u - (r & 7u);
         fetch(A, r);
         fetch(B, r + 1);
         continue;
@@ -807,6 +817,10 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       fetch(B, r + 3);
       r += 2;
     }
+    // the strip's last rows (V not a multiple of 8): every carry is stored
+    if (WPJ > 1 && write_bnd && lane == 0)
+      __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(V), __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
     // this strip's boundary stores must land before the next strip reads them
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
