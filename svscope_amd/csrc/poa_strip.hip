@@ -342,6 +342,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const int32_t j0 = s << 6;
     const int32_t j = j0 + lane;
     const uint8_t rc = seq[j - 1];  // seqs[seq_off - 1] is a zero pad byte (column 0)
+    uint16_t* __restrict__ tbl = tbj + j;  // this lane's column of the traceback codes
     const int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
     int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
 #ifdef SVS_OPT_CARRY
@@ -369,7 +370,18 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     constexpr uint32_t kRegBit = 1u << 31;
     uint32_t alive = (FIRST || !prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb) ? 1u : 0u;
     const int32_t rrem = L - j;              // read bases after column j
+#ifdef SVS_ROWTAIL_OLD
     const int32_t mrr = P.m * rrem;
+#else
+    // lanes past column L are never alive: their m rr term is VNEG/2, so
+    // H + ub stays below every real bound (no overflow: H >= VNEG - gaps);
+    // the liveness ballot then needs no rrem >= 0 lane mask
+    const int32_t mrr = rrem >= 0 ? P.m * rrem : SVS_VNEG / 2;
+    // every lane tracks its own sink maximum; only the lane of column L in
+    // the last strip (which owns L, swept last by its wave) is read
+    best = SVS_NEG_INF;
+    best_row = 0;
+#endif
     // m rr + cg max(0, dmin - rr) - (m - cg) max(0, rr - dmax) as
     // m rr + d (d >= 0 ? cg : m - cg) with d = clamp(rr, dmin, dmax) - rr
     auto ub_of = [&](uint32_t w2, int32_t rr, int32_t mr) -> int32_t {
@@ -400,7 +412,8 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
 
     auto fetch = [&](RowIn& d, uint32_t r) {
       const uint32_t rr = r < V ? r : V - 1;
-      const uint32_t* w = rec + rr * kRecWords;  // 32-bit: a job has < 2^30 rows
+      // 32-bit byte offsets off the job's bases (a job has < 2^28 rows)
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(rec) + (rr << 4));
       d.w0 = w[0];
       d.w1 = w[1];
       if constexpr (PRUNE) {
@@ -427,7 +440,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
 #endif
           }
         }
-        const int4 v = *reinterpret_cast<const int4*>(bin + 4u * rr);
+        const int4 v = *reinterpret_cast<const int4*>(reinterpret_cast<const char*>(bin) + (rr << 4));
         d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
       }
     };
@@ -450,7 +463,11 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       auto publish = [&]() {
         if (WPJ > 1 && write_bnd && --pub_left == 0) {
           pub_left = 8;
+#ifdef SVS_ROWTAIL_OLD
           if (lane == 0)
+#endif
+          // (every lane stores the same value: no exec-mask branch, and the
+          // countdown stays a scalar)
             __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
                                __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -489,7 +506,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
           pr_slow += 1;
 #endif
           if (write_bnd && lane == 0)
-            *reinterpret_cast<int4*>(bout + 4u * r) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
+            *reinterpret_cast<int4*>(reinterpret_cast<char*>(bout) + (r << 4)) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
           publish();
           return;
         }
@@ -663,7 +680,13 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
         code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k, uc_stop);
       }
+#ifdef SVS_ROWTAIL_OLD
       tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
+#else
+      // 32-bit row offset off this lane's column: the host keeps n_rows x ls
+      // below 2^31 per job
+      tbl[r * LS] = static_cast<uint16_t>(code);
+#endif
 #ifdef SVS_PROBE_SALU
       // development probe: extra scalar work per computed row (issue-bound test)
       {
@@ -684,7 +707,11 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       bool any_alive = true;
       if (prune) {
         const int32_t ub = ub_of(w2w3.x, rrem, mrr);
+#ifdef SVS_ROWTAIL_OLD
         any_alive = __builtin_amdgcn_ballot_w64(rrem >= 0 && H + ub >= lb) != 0;
+#else
+        any_alive = __builtin_amdgcn_ballot_w64(H + ub >= lb) != 0;
+#endif
         const bool out_alive = any_alive || cH_in > SVS_VNEG / 2;
         const uint32_t ob = own_bit | kRegBit;
         alive = ((alive & ~ob) | (out_alive ? ob : 0u)) & ~w2w3.y;
@@ -713,11 +740,19 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       } else
 #endif
       if (write_bnd && lane == 0) {
-        *reinterpret_cast<int4*>(bout + 4u * r) =
+        *reinterpret_cast<int4*>(reinterpret_cast<char*>(bout) + (r << 4)) =
             any_alive ? make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH) : make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
       }
       publish();
+#ifdef SVS_ROWTAIL_OLD
       if (sink && owns_L && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
+#else
+      if (sink) {
+        const bool u = H > best;
+        best = u ? H : best;
+        best_row = u ? static_cast<int32_t>(r) + 1 : best_row;
+      }
+#endif
     };
 
     // Pruning: with no slot (but the virtual row's) and not the register row
@@ -852,6 +887,11 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     uint32_t alive = (!prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb) ? 1u : 0u;
     const int32_t rra = L - ja, rrb = L - jb;
     const int32_t mra = P.m * rra, mrb = P.m * rrb;
+#ifndef SVS_ROWTAIL_OLD
+    // strip 0 (sweep) lets every lane track a sink maximum: start clean
+    best = SVS_NEG_INF;
+    best_row = 0;
+#endif
     auto ub_of = [&](uint32_t w2, int32_t rr, int32_t mr) -> int32_t {
       const int32_t dmin = static_cast<int32_t>(w2 & 0xFFFFu), dmax = static_cast<int32_t>(w2 >> 16);
       const int32_t d = min(imax(rr, dmin), dmax) - rr;

@@ -350,6 +350,8 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     J.len = static_cast<uint32_t>(s.size());
     J.ls = job_ls(J.len);
     J.n_slots = tt.n_slots;
+    if (static_cast<uint64_t>(J.n_rows) * J.ls > 0x7FFFFFFFull)  // the strip kernel's 32-bit code offsets
+      throw SvsError(SVS_E_UNSUPPORTED, "a job's traceback matrix exceeds 2^31 cells");
     J.tb_off = n_tb;
     J.bnd_off = n_bnd;
     J.pool_off = n_pool;
