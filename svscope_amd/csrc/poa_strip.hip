@@ -356,7 +356,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
     int32_t avail = -1;                                  // producer progress seen so far
     const bool write_bnd = s + 1 < nstrips;
-    const bool owns_L = strip_of(L) == s;
     // rows left until the next whole 8-row carry line, where progress is
     // published (the strip's last row after the row loop): a countdown
     // instead of a test of r per row
@@ -370,9 +369,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     constexpr uint32_t kRegBit = 1u << 31;
     uint32_t alive = (FIRST || !prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb) ? 1u : 0u;
     const int32_t rrem = L - j;              // read bases after column j
-#ifdef SVS_ROWTAIL_OLD
-    const int32_t mrr = P.m * rrem;
-#else
     // lanes past column L are never alive: their m rr term is VNEG/2, so
     // H + ub stays below every real bound (no overflow: H >= VNEG - gaps);
     // the liveness ballot then needs no rrem >= 0 lane mask
@@ -381,7 +377,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     // the last strip (which owns L, swept last by its wave) is read
     best = SVS_NEG_INF;
     best_row = 0;
-#endif
     // m rr + cg max(0, dmin - rr) - (m - cg) max(0, rr - dmax) as
     // m rr + d (d >= 0 ? cg : m - cg) with d = clamp(rr, dmin, dmax) - rr
     auto ub_of = [&](uint32_t w2, int32_t rr, int32_t mr) -> int32_t {
@@ -463,13 +458,10 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       auto publish = [&]() {
         if (WPJ > 1 && write_bnd && --pub_left == 0) {
           pub_left = 8;
-#ifdef SVS_ROWTAIL_OLD
-          if (lane == 0)
-#endif
-          // (every lane stores the same value: no exec-mask branch, and the
-          // countdown stays a scalar)
-            __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
-                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          // every lane stores the same value: no exec-mask branch, and the
+          // countdown stays a scalar
+          __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
+                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       };
       const int32_t cH_in = FIRST ? SVS_VNEG : __builtin_amdgcn_readfirstlane(d.b3);
@@ -680,13 +672,9 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
         code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k, uc_stop);
       }
-#ifdef SVS_ROWTAIL_OLD
-      tbj[static_cast<uint64_t>(r) * LS + j] = static_cast<uint16_t>(code);
-#else
       // 32-bit row offset off this lane's column: the host keeps n_rows x ls
       // below 2^31 per job
       tbl[r * LS] = static_cast<uint16_t>(code);
-#endif
 #ifdef SVS_PROBE_SALU
       // development probe: extra scalar work per computed row (issue-bound test)
       {
@@ -707,11 +695,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       bool any_alive = true;
       if (prune) {
         const int32_t ub = ub_of(w2w3.x, rrem, mrr);
-#ifdef SVS_ROWTAIL_OLD
-        any_alive = __builtin_amdgcn_ballot_w64(rrem >= 0 && H + ub >= lb) != 0;
-#else
         any_alive = __builtin_amdgcn_ballot_w64(H + ub >= lb) != 0;
-#endif
         const bool out_alive = any_alive || cH_in > SVS_VNEG / 2;
         const uint32_t ob = own_bit | kRegBit;
         alive = ((alive & ~ob) | (out_alive ? ob : 0u)) & ~w2w3.y;
@@ -744,15 +728,11 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
             any_alive ? make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH) : make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
       }
       publish();
-#ifdef SVS_ROWTAIL_OLD
-      if (sink && owns_L && j == L && H > best) { best = H; best_row = static_cast<int32_t>(r) + 1; }
-#else
       if (sink) {
         const bool u = H > best;
         best = u ? H : best;
         best_row = u ? static_cast<int32_t>(r) + 1 : best_row;
       }
-#endif
     };
 
     // Pruning: with no slot (but the virtual row's) and not the register row
@@ -887,11 +867,9 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     uint32_t alive = (!prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb) ? 1u : 0u;
     const int32_t rra = L - ja, rrb = L - jb;
     const int32_t mra = P.m * rra, mrb = P.m * rrb;
-#ifndef SVS_ROWTAIL_OLD
     // strip 0 (sweep) lets every lane track a sink maximum: start clean
     best = SVS_NEG_INF;
     best_row = 0;
-#endif
     auto ub_of = [&](uint32_t w2, int32_t rr, int32_t mr) -> int32_t {
       const int32_t dmin = static_cast<int32_t>(w2 & 0xFFFFu), dmax = static_cast<int32_t>(w2 >> 16);
       const int32_t d = min(imax(rr, dmin), dmax) - rr;
