@@ -285,6 +285,8 @@ uint64_t job_bytes(const RowTables& tt, uint64_t L, const KernelEnv& ke) {
   return V * ls * 2 + static_cast<uint64_t>(tt.n_slots) * 3 * ls * 4 + (V + L + 1) * 8;
 }
 
+void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks);
+
 void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, const PoaScore& score,
                            svs_poa_stats& st, double& host_ms) {
   auto th0 = Clock::now();
@@ -475,6 +477,11 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
                                   reinterpret_cast<uint8_t*>(dg), prep_rows, ps));
     SVS_HIP(hipEventRecord(A.evp1, ps));
     if (own) SVS_HIP(hipStreamWaitEvent(A.stream, A.evp1, 0));
+    if (verify_prep()) {
+      // before the DP kernel reads them: a wrong table fails here, not there
+      SVS_HIP(hipStreamSynchronize(ps));
+      verify_prep_tables(la, tasks);
+    }
   }
   PoaLaunch pl{};
   pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
@@ -717,7 +724,6 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
     SVS_HIP(hipEventElapsedTime(&pms, A.evp, A.evp1));
     st.prep_ms += pms;
     st.prep_jobs += la.prep_jobs;
-    if (verify_prep()) verify_prep_tables(la, tasks);
   }
   if (g_trace.f) {
     uint64_t cells = 0;
