@@ -117,33 +117,19 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
     }
     return uni(ld(scr + x));
   };
-  // Chain rows of a chunk: one in-edge, from the row just above (and, for the
-  // slot pass, no pool slot of their own).  Most rows are; the sequential
-  // passes visit only the others and derive the chain rows' words lane-parallel.
-  auto chain_rows = [&](const Chunk& c, bool need_no_slot) -> uint64_t {
-    const uint32_t r = c.r0 + lane;
-    bool chain = false;
-    if (lane < c.n && ((c.info >> 10) & 63u) == 1u && !(need_no_slot && ((c.info >> 9) & 1u)))
-      chain = (gpr[c.ps] & 0x7FFFFFFFu) == r;  // stored as pred row + 1
-    return __builtin_amdgcn_ballot_w64(chain);
-  };
-  auto rows_mask = [](uint32_t n) -> uint64_t { return n >= 64 ? ~0ull : (1ull << n) - 1; };
 
   if (wave == 0) {
     // pool slots, record words w0 w1 w3, in-edge slots
     uint32_t next = J.prep >> 1, fsp = 0;
     uint32_t fstack = 0;  // free list: lane i = entry i
-    uint32_t ebuf = kNoSlot, ebase = 0;  // in-edge slots of edges ebase + lane
-    uint32_t pwin = 0;                   // lane i: pool slot of row r0 - 64 + i (the chunk before)
+    uint32_t ebuf = 0, ebase = 0;  // in-edge slots of edges ebase + lane
+    uint32_t pwin = 0;             // lane i: pool slot of row r0 - 64 + i (the chunk before)
     Chunk cur = load(0);
     for (;;) {
       const Chunk nxt = cur.r0 + kChunk < V ? load(cur.r0 + kChunk) : cur;
-      // chain rows: no slot, w0 = info | kNoSlot << 16, w1 = kNoSlot (their
-      // in-edge is the register row), w3 = 0, in-edge slot kNoSlot
-      uint32_t win = kNoSlot;  // lane i: pool slot of row r0 + i
-      uint32_t ow0 = cur.info | (kNoSlot << 16), ow1 = kNoSlot, ow3 = 0;
-      for (uint64_t m = rows_mask(cur.n) & ~chain_rows(cur, true); m; m &= m - 1) {
-        const uint32_t i = static_cast<uint32_t>(__builtin_ctzll(m));
+      uint32_t win = 0;  // lane i: pool slot of row r0 + i
+      uint32_t ow0 = 0, ow1 = 0, ow3 = 0;
+      for (uint32_t i = 0; i < cur.n; ++i) {
         const uint32_t r = cur.r0 + i;
         const uint32_t a = pstart_of(cur, i), b = pstart_of(cur, i + 1);
         const uint32_t inf = lane_of(cur.info, i);
@@ -160,10 +146,9 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
           if (pr + 1 != r)
             ps = pr >= cur.r0 ? lane_of(win, pr - cur.r0)
                               : (pr + kChunk >= cur.r0 ? lane_of(pwin, pr + kChunk - cur.r0) : far(pr));
-          while (x - ebase >= 64) {  // (chain rows' edges in between keep kNoSlot)
+          if (x - ebase == 64) {
             pslot[ebase + lane] = ebuf;
             ebase += 64;
-            ebuf = kNoSlot;
           }
           ebuf = set_lane(ps, x - ebase, ebuf);
           if (x - a < kInlinePreds) w1 |= ps << (16 * (x - a));
@@ -188,8 +173,7 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
       pwin = win;
       cur = nxt;
     }
-    for (; ebase < E; ebase += 64, ebuf = kNoSlot)
-      if (ebase + lane < E) pslot[ebase + lane] = ebuf;
+    if (ebase + lane < E) pslot[ebase + lane] = ebuf;
   } else if (wave == 1) {
     // fewest nodes from a source -> column 0: F0 = g + sd e, O0 = q + sd c
     uint32_t sd_prev = 0;
@@ -198,19 +182,8 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
     for (;;) {
       const Chunk nxt = cur.r0 + kChunk < V ? load(cur.r0 + kChunk) : cur;
       uint32_t win = 0;  // lane i: sd of row r0 + i
-      // a run of chain rows after row li (sd lsd) continues it one node at a
-      // time: filled lane-parallel before the next row that reads them
-      int32_t li = -1;
-      uint32_t lsd = sd_prev;
-      auto fill = [&](int32_t upto) {
-        const int32_t l = static_cast<int32_t>(lane);
-        win = (l > li && l < upto) ? lsd + static_cast<uint32_t>(l - li) : win;
-      };
-      for (uint64_t m = rows_mask(cur.n) & ~chain_rows(cur, false); m; m &= m - 1) {
-        const uint32_t i = static_cast<uint32_t>(__builtin_ctzll(m));
+      for (uint32_t i = 0; i < cur.n; ++i) {
         const uint32_t r = cur.r0 + i;
-        fill(static_cast<int32_t>(i));
-        sd_prev = lsd + static_cast<uint32_t>(static_cast<int32_t>(i) - 1 - li);  // sd of row r - 1
         const uint32_t a = pstart_of(cur, i), b = pstart_of(cur, i + 1);
         uint32_t sd = a == b ? 0u : 0xFFFFu;  // a source: 0
         for (uint32_t x = a; x < b; ++x) {
@@ -222,12 +195,9 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
                                                                    : far(pr)));
           sd = min(sd, sdp + 1);
         }
+        sd_prev = sd;
         win = set_lane(sd, i, win);
-        li = static_cast<int32_t>(i);
-        lsd = sd;
       }
-      fill(static_cast<int32_t>(cur.n));
-      sd_prev = lsd + static_cast<uint32_t>(static_cast<int32_t>(cur.n) - 1 - li);
       if (lane < cur.n) {
         const uint64_t r = cur.r0 + lane;
         scr[r] = win;
@@ -259,26 +229,12 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
       uint32_t win = lane < cur.n ? merge(ld(scr + cur.r0 + lane), nwin) : 0xFFFFu;
       nwin = 0xFFFFu;
       uint32_t ow2 = 0;
-      const uint64_t chain = chain_rows(cur, false);
       for (uint32_t i = cur.n; i-- > 0;) {
         const uint32_t v = lane_of(win, i);
         uint32_t lo = v & 0xFFFFu;
         const uint32_t hi = v >> 16;
         if ((lane_of(cur.info, i) >> 8) & 1u) lo = 0;  // a sink
         const uint32_t l1 = min(lo + 1, 0xFFFFu), h1 = min(hi + 1, 0xFFFFu);
-        ow2 = set_lane(lo | (hi << 16), i, ow2);
-        if ((chain >> i) & 1u) {
-          // a chain row's one in-edge is the row above: in this chunk, or the
-          // previous chunk's last row (processed next)
-          if (i > 0) {
-            const uint32_t pv = lane_of(win, i - 1);
-            win = set_lane(min(pv & 0xFFFFu, l1) | (max(pv >> 16, h1) << 16), i - 1, win);
-          } else {
-            const uint32_t pv = lane_of(nwin, kChunk - 1);
-            nwin = set_lane(min(pv & 0xFFFFu, l1) | (max(pv >> 16, h1) << 16), kChunk - 1, nwin);
-          }
-          continue;
-        }
         const uint32_t a = pstart_of(cur, i), b = pstart_of(cur, i + 1);
         for (uint32_t x = a; x < b; ++x) {
           const uint32_t p = (edge(cur, x) & 0x7FFFFFFFu) - 1;
@@ -295,6 +251,7 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
             flush_fence();
           }
         }
+        ow2 = set_lane(lo | (hi << 16), i, ow2);
       }
       if (lane < cur.n) rec[4ull * (cur.r0 + lane) + 2] = ow2;
       if (cur.r0 == 0) break;

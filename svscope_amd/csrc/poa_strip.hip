@@ -441,7 +441,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     };
 
     int32_t pH = 0, pF = 0, pO = 0, pHm = 0;  // the row just above (registers); pHm = its H[j-1]
-    auto step = [&](uint32_t r, RowIn& d) {
+    auto step = [&](uint32_t r, const RowIn& d) {
       const uint32_t w0 = __builtin_amdgcn_readfirstlane(d.w0);
       const uint32_t nb = w0 & 0xFFu;
       const bool sink = (w0 >> 8) & 1u;
@@ -499,9 +499,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
 #endif
           if (write_bnd && lane == 0)
             *reinterpret_cast<int4*>(reinterpret_cast<char*>(bout) + (r << 4)) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
-#ifdef SVS_LATE_FETCH
-          fetch(d, r + 2);  // this row's inputs are used up: refill the set
-#endif
           publish();
           return;
         }
@@ -551,14 +548,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       int32_t Hpre_keep = 0;  // this row's Hpre (SVS_OPT_CARRY: lane 63's is a carry)
       auto gaps = [&](int32_t Hpre, bool inner_) {
         Hpre_keep = Hpre;
-#ifdef SVS_LATE_FETCH
-        // Hpre consumed the pool reads: refill this set (row r + 2) now, so the
-        // scalar loads have the rest of the row to land before the next row's
-        // pool reads wait on lgkmcnt (which counts them too).  Rows with more
-        // than two in-edges (strip 0: more than one) read the pool and the
-        // record again below and refill after that.
-        if (np <= 1 || (!FIRST && np == 2)) fetch(d, r + 2);
-#endif
         if (FIRST) {
           int32_t prevQ, prevE;
           strip_gaps(P, lane, j, j0, inner_, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
@@ -682,9 +671,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const bool lc = inner && H == prevQc, ld = inner && H == prevH + P.q;
         const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
         code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k, uc_stop);
-#ifdef SVS_LATE_FETCH
-        fetch(d, r + 2);
-#endif
       }
       // 32-bit row offset off this lane's column: the host keeps n_rows x ls
       // below 2^31 per job
@@ -833,9 +819,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         fetch(B, r + 1);
         continue;
       }
-#ifndef SVS_LATE_FETCH
       fetch(A, r + 2);
-#endif
       if (r + 1 >= V) break;
       step(r + 1, B);
       if (prune && dead_strip()) {
@@ -845,9 +829,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         fetch(B, r + 1);
         continue;
       }
-#ifndef SVS_LATE_FETCH
       fetch(B, r + 3);
-#endif
       r += 2;
     }
     // the strip's last rows (V not a multiple of 8): every carry is stored
