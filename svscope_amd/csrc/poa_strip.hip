@@ -215,6 +215,11 @@ __device__ unsigned long long svs_strip_prof[8];
 #endif
 
 // Bounded LDS-flag wait (workgroup scope); sets *err after kStripSpinLimit polls.
+#ifndef SVS_POLL_N  // development: the nap schedule of the progress polls
+#define SVS_POLL_N 8
+#define SVS_POLL_S1 1
+#define SVS_POLL_S2 4
+#endif
 constexpr long kStripSpinLimit = 1l << 26;
 __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, int32_t* err) {
   long n = 0;
@@ -223,8 +228,8 @@ __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, 
               __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))) < target) {
     // short naps first, then longer ones: a wave far behind its producer
     // should not take issue slots from the waves that are computing
-    if (n < 8) __builtin_amdgcn_s_sleep(1);
-    else __builtin_amdgcn_s_sleep(4);
+    if (n < SVS_POLL_N) __builtin_amdgcn_s_sleep(SVS_POLL_S1);
+    else __builtin_amdgcn_s_sleep(SVS_POLL_S2);
     if (++n > kStripSpinLimit) {
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return target;
