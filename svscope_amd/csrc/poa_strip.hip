@@ -215,10 +215,15 @@ __device__ unsigned long long svs_strip_prof[8];
 #endif
 
 // Bounded LDS-flag wait (workgroup scope); sets *err after kStripSpinLimit polls.
-#ifndef SVS_POLL_N  // development: the nap schedule of the progress polls
-#define SVS_POLL_N 8
-#define SVS_POLL_S1 1
-#define SVS_POLL_S2 4
+// Nap schedule of the progress polls: the first SVS_POLL_N polls sleep
+// SVS_POLL_S1 x 64 cycles, later ones SVS_POLL_S2 x 64.  A consumer that
+// caught up with its producer waits for the next 8-row line, thousands of
+// cycles: polling often only takes issue slots from the computing waves
+// (profiles/r02_v42: 8/1/4 -> always 8 is 1.5 % less kernel time).
+#ifndef SVS_POLL_N
+#define SVS_POLL_N 0
+#define SVS_POLL_S1 8
+#define SVS_POLL_S2 8
 #endif
 constexpr long kStripSpinLimit = 1l << 26;
 __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, int32_t* err) {
@@ -226,8 +231,6 @@ __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, 
   int32_t v;
   while ((v = __builtin_amdgcn_readfirstlane(
               __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))) < target) {
-    // short naps first, then longer ones: a wave far behind its producer
-    // should not take issue slots from the waves that are computing
     if (n < SVS_POLL_N) __builtin_amdgcn_s_sleep(SVS_POLL_S1);
     else __builtin_amdgcn_s_sleep(SVS_POLL_S2);
     if (++n > kStripSpinLimit) {
