@@ -48,7 +48,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "candidate-windows/sec (64 reads × 3 kb) localGraph, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0
+FP64_MATRIX_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix peak (the EM's dtype)
 BYTES_PER_CELL = 20
+GOLDEN_DIGESTS = os.path.join(ROOT, "tests", "golden", "bench_config3_digests.json")
 N_READS, REF_LEN = 64, 3000
 WARMUP_ID_BASE = 1 << 30  # warmup windows never share a seed with timed ones
 
@@ -142,6 +144,26 @@ def pmc_traffic_per_cell():
         return None
 
 
+def record_digests(recs, first_id):
+    """SHA-256 of each timed record's Raw.bed line (local_graph.record_line,
+    SVscope.py:171-180) for the windows the committed CPU-oracle fixture covers
+    (tests/golden/bench_config3_digests.json: window ids 0..255 of rank 0), and
+    whether they all match it.  None when the fixture covers none of them."""
+    import hashlib
+    from svscope_amd.local_graph import record_line
+    if not os.path.exists(GOLDEN_DIGESTS):
+        return None
+    gold = json.load(open(GOLDEN_DIGESTS))
+    n = min(len(recs), len(gold["digests"]) - first_id)
+    if first_id != 0 or n <= 0:
+        return None
+    got = [hashlib.sha256(record_line(r).encode()).hexdigest() for r in recs[:n]]
+    bad = [k for k in range(n) if got[k] != gold["digests"][k]]
+    return {"windows": n, "digest": hashlib.sha256("\n".join(got).encode()).hexdigest(),
+            "oracle_digest": gold["all"] if n == len(gold["digests"]) else None,
+            "match": not bad, "mismatched_windows": bad[:16]}
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -227,6 +249,10 @@ def main():
 
     dist = None
     if world > 1:
+        # this rank's CPU slice and engine pool size (svscope_amd/hostcpu.py),
+        # before the library creates its context
+        from svscope_amd import hostcpu
+        hostcpu.apply(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -269,8 +295,12 @@ def main():
     achieved = cells_done * BYTES_PER_CELL / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     total_windows = B * K * world
 
+    em_flops = st.get("em_flops", 0.0)
+    em_s = st["em_kernel_ms"] / 1e3
+    em_tflops = em_flops / em_s / 1e12 if em_s > 0 else 0.0
     if rank == 0:
         value = total_windows / elapsed
+        digests = record_digests(recs, timed_ids[0])
         per_cell = pmc_traffic_per_cell()
         traffic = round(per_cell * cells_done / max(1, launches)) if per_cell is not None else None
         out = {
@@ -307,6 +337,7 @@ def main():
                                           "note": "every DP cell of the full matrix; above 1 because exact "
                                                   "pruning skips most cells, so not an HBM-traffic figure"}},
             "cpu_baseline": cpu,
+            "oracle_check": digests,
             "breakdown": {"poa_cells": cells, "poa_cells_computed": cells_done,
                           "prune_retries": poa["prune_retries"],
                           "poa_prep_kernel_ms": round(poa.get("prep_ms", 0.0), 2),
@@ -319,6 +350,11 @@ def main():
                           "h2d_bytes": poa["h2d_bytes"], "d2h_bytes": poa["d2h_bytes"],
                           "em_output_windows": n_em,
                           "em_kernel_s": round(st["em_kernel_ms"] / 1e3, 3),
+                          # EM roofline is the FP64 matrix peak;
+                          # dense-equivalent FLOPs = sum_K 41 x 2 N (5 nf) K per window
+                          "em_roofline": {"bound": "mfma", "dense_equiv_flops": em_flops,
+                                          "achieved": round(em_tflops, 3), "peak": FP64_MATRIX_PEAK_TFLOPS,
+                                          "unit": "TFLOP/s", "frac": round(em_tflops / FP64_MATRIX_PEAK_TFLOPS, 5)},
                           "em_wall_s": round(st["em_wall_ms"] / 1e3, 3),
                           "em_launches": st["em_launches"], "em_windows": st["em_windows"],
                           "consensus_tasks": st["consensus_tasks"],

@@ -176,6 +176,9 @@ typedef struct svs_decision_stats {
   svs_poa_stats poa;   /* MSA + consensus POA together */
   double wall_ms, features_ms, labelling_ms, em_wall_ms, em_kernel_ms;
   int64_t msa_tasks, consensus_tasks, em_windows, em_launches;
+  /* SURVEY.md §8(d) dense-equivalent EM FLOPs of the windows sent to EM:
+   * per window sum over K of 41 x 2 N (5 nf) K (21 E-steps + 20 M-steps) */
+  double em_flops;
 } svs_decision_stats;
 
 typedef struct svs_decision_result svs_decision_result;

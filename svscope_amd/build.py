@@ -21,7 +21,6 @@ LIB = os.path.join(LIB_DIR, "libsvscope_hip.so")
 ARCH = os.environ.get("SVS_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [
-    "poa_kernels.hip",
     "poa_strip.hip",
     "poa_prep.hip",
     "em_kernels.hip",

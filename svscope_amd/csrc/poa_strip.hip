@@ -45,12 +45,7 @@ namespace {
 // then 64 uint16 D = dF | dO << 8 with dF = min(H - F, tF), dO = min(H - O, tO)
 // (see pack_fo).
 constexpr int kSlotInts = 65 + 32;
-// Wide strips (see sweep_w): Hx[0..129], then 64 words of F/O pairs.
-constexpr int kSlotIntsW = 130 + 64;
-static_assert(kSlotIntsW * 4 == kStripSlotBytesWide, "wide pool slot size");
 static_assert(kSlotInts * 4 == kStripSlotBytes, "pool slot size");
-
-typedef int32_t svs_i32x2 __attribute__((ext_vector_type(2)));
 
 // F and O enter the recurrence only through F + e (against H + g) and O + c
 // (against H + q), and F, O <= H.  So F matters only while H - F <= e - g and
@@ -120,12 +115,6 @@ __device__ __forceinline__ void strip_gaps_nf(const PoaScore& P, int32_t j0, int
   o.prevEe = shr1_add(cr.cE + P.e, o.E, K.ve);
   o.prevQc = shr1_add(cr.cQ + P.c, o.Q, K.vc);
   o.prevH = wave_shr1(o.H, cr.cH, 0);
-#ifdef SVS_OPT_CARRY
-  // the next strip's carries are lane 63's Q - jc, E - je, Hpre and H
-  // (run1' = max(P1, run1) = Q - jc, run2' = max(P2, run2, T1, T2) = E - je):
-  // stored from lane 63 by the caller, no scalar work here
-  return;
-#endif
   const int32_t jl = j0 + 63;
   const int32_t p1l = readlane63(p1), p2l = readlane63(p2), hl = readlane63(Hpre);
   const int32_t T2l = cr.run1 + (jl - 1) * P.c + P.g - jl * P.e;
@@ -149,70 +138,8 @@ __device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, con
   return (d.w1 >> (16 * k)) & 0xFFFFu;
 }
 
-// Traceback code of a one-in-edge cell off column 0 (the np <= 1 tests of
-// poa_strip_kernel) as 14 compares and 16 selects/shifts, all VALU: the
-// compares write three rotating SGPR pairs, each read as a v_cndmask mask three
-// instructions later (gfx950 needs two wait states between a VALU SGPR write
-// and a VALU mask read).  Written as one asm block because LLVM otherwise
-// merges the select chains into scalar mask logic (s_and/s_or_b64), which
-// competes with the row loop's bookkeeping for the scalar issue slots.
-//   code = dg ? 0 : up ? upc : lf ? lfc : 3,  upc = ua || (!ub && uc) ? 5 : 1,
-//   lfc = la || (!lb && lc) ? 6 : 2,  | lbit << 8  | vbit << 9
-__device__ __forceinline__ uint32_t code_np1(int32_t H, int32_t D, int32_t mFO, int32_t mEQ, int32_t fpe,
-                                             int32_t hpg, int32_t opc, int32_t hpq, int32_t prevEe,
-                                             int32_t prevHg, int32_t prevQc, int32_t prevHq, int32_t E, int32_t Q,
-                                             int32_t F, int32_t O) {
-  uint32_t r1, r2, c, t, v;
-  uint64_t m0, m1, m2;
-  asm("v_cmp_eq_u32_e64 %[m0], %[H], %[opc]\n\t"
-      "v_cmp_eq_u32_e64 %[m1], %[H], %[hpg]\n\t"
-      "v_cmp_eq_u32_e64 %[m2], %[H], %[fpe]\n\t"
-      "v_cndmask_b32_e64 %[r1], 1, 5, %[m0]\n\t"
-      "v_cmp_eq_u32_e64 %[m0], %[H], %[prevQc]\n\t"
-      "v_cndmask_b32_e64 %[r1], %[r1], 1, %[m1]\n\t"
-      "v_cmp_eq_u32_e64 %[m1], %[H], %[prevHg]\n\t"
-      "v_cndmask_b32_e64 %[r1], %[r1], 5, %[m2]\n\t"
-      "v_cmp_eq_u32_e64 %[m2], %[H], %[prevEe]\n\t"
-      "v_cndmask_b32_e64 %[r2], 2, 6, %[m0]\n\t"
-      "v_cmp_eq_u32_e64 %[m0], %[H], %[mEQ]\n\t"
-      "v_cndmask_b32_e64 %[r2], %[r2], 2, %[m1]\n\t"
-      "v_cmp_eq_u32_e64 %[m1], %[H], %[mFO]\n\t"
-      "v_cndmask_b32_e64 %[r2], %[r2], 6, %[m2]\n\t"
-      "v_cmp_eq_u32_e64 %[m2], %[H], %[D]\n\t"
-      "v_cndmask_b32_e64 %[c], 3, %[r2], %[m0]\n\t"
-      "v_cmp_eq_u32_e64 %[m0], %[E], %[prevHg]\n\t"
-      "v_cndmask_b32_e64 %[c], %[c], %[r1], %[m1]\n\t"
-      "v_cmp_eq_u32_e64 %[m1], %[Q], %[prevHq]\n\t"
-      "v_cndmask_b32_e64 %[c], %[c], 0, %[m2]\n\t"
-      "v_cmp_eq_u32_e64 %[m2], %[O], %[hpq]\n\t"
-      "v_cndmask_b32_e64 %[t], 0, 1, %[m0]\n\t"
-      "v_cmp_eq_u32_e64 %[m0], %[F], %[fpe]\n\t"
-      "v_cndmask_b32_e64 %[t], %[t], 1, %[m1]\n\t"
-      "v_cmp_eq_u32_e64 %[m1], %[F], %[hpg]\n\t"
-      "v_cndmask_b32_e64 %[v], 0, 1, %[m2]\n\t"
-      "v_lshl_or_b32 %[c], %[t], 8, %[c]\n\t"
-      "v_cndmask_b32_e64 %[v], %[v], 0, %[m0]\n\t"
-      "v_cndmask_b32_e64 %[v], %[v], 1, %[m1]\n\t"
-      "v_lshl_or_b32 %[c], %[v], 9, %[c]"
-      : [r1] "=&v"(r1), [r2] "=&v"(r2), [c] "=&v"(c), [t] "=&v"(t), [v] "=&v"(v), [m0] "=&s"(m0), [m1] "=&s"(m1),
-        [m2] "=&s"(m2)
-      : [H] "v"(H), [D] "v"(D), [mFO] "v"(mFO), [mEQ] "v"(mEQ), [fpe] "v"(fpe), [hpg] "v"(hpg), [opc] "v"(opc),
-        [hpq] "v"(hpq), [prevEe] "v"(prevEe), [prevHg] "v"(prevHg), [prevQc] "v"(prevQc), [prevHq] "v"(prevHq),
-        [E] "v"(E), [Q] "v"(Q), [F] "v"(F), [O] "v"(O));
-  return c;
-}
-
 }  // namespace
 
-#ifdef SVS_STRIP_PROF
-// development build only: per-wave cycle attribution summed over the launch
-// [0] sweep cycles, [1] producer waits in fetch, [2] fast_forward cycles,
-// [3] producer waits inside fast_forward, [4] computed strip rows, [5] ff calls,
-// [6] rows skipped one by one, [7] waves
-__device__ unsigned long long svs_strip_prof[8];
-#define SVS_PROF_T() __builtin_amdgcn_s_memtime()
-#define SVS_PROF_ADD(i, v) do { if (lane == 0) atomicAdd(&svs_strip_prof[i], (unsigned long long)(v)); } while (0)
-#endif
 
 // Bounded LDS-flag wait (workgroup scope); sets *err after kStripSpinLimit polls.
 // Nap schedule of the progress polls: the first SVS_POLL_N polls sleep
@@ -245,17 +172,14 @@ __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, 
 // ...; strip s reads the carries wave (w-1) mod WPJ left for strip s-1, which
 // it publishes every 8 rows through an LDS progress counter (workgroup-scope
 // release / acquire), so the waves form a row-skewed pipeline over strips.
-template <bool LDSP, int WPJ, bool PRUNE, bool WIDE>
+template <bool LDSP, int WPJ, bool PRUNE>
 // The pruning variant is held to 80 VGPRs (6 waves per SIMD; a few spills to
 // scratch in cold paths): measured faster than its natural 86 (5 waves),
 // profiles/r01_v36.  SVS_PRUNE_OCC overrides it in development builds.
 #ifndef SVS_PRUNE_OCC
 #define SVS_PRUNE_OCC 6
 #endif
-#ifndef SVS_WIDE_OCC
-#define SVS_WIDE_OCC 4
-#endif
-#define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? (WIDE ? SVS_WIDE_OCC : SVS_PRUNE_OCC) : 1)))
+#define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? SVS_PRUNE_OCC : 1)))
 __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore Parg, const uint32_t* __restrict__ rec_all,
     const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
@@ -263,14 +187,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     uint16_t* __restrict__ tb, int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
     int32_t* __restrict__ gpool, int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
   extern __shared__ int32_t lds[];
-#ifdef SVS_FIXED_SCORES
-  // development: spoa's default scores as compile-time constants (the only
-  // ones the reference uses); the host checks the configuration
-  constexpr PoaScore P{5, -4, -8, -6, -10, -4};
-  (void)Parg;
-#else
   const PoaScore P = Parg;
-#endif
   __shared__ int32_t prog[WPJ];  // per wave: strip * (V + 1) + rows done, carries published
   __shared__ int32_t s_err;
   __shared__ int32_t s_brow[WPJ], s_best[WPJ];
@@ -285,14 +202,11 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   const uint32_t LS = J.ls;
   const uint32_t V = J.n_rows;
   const uint32_t VP = (V + 7) & ~7u;  // carry rows per strip, padded to whole 128-B lines
-  static_assert(!WIDE || LDSP, "wide strips keep their pool in LDS");
-  // strip geometry: 64-column strips, or (WIDE) a 64-column strip 0 and then
-  // 128-column strips (sweep_w)
-  const int32_t nstrips = WIDE ? (LS <= 64 ? 1 : 1 + static_cast<int32_t>((LS - 64) >> 7))
-                               : static_cast<int32_t>(LS >> 6);
-  auto strip_of = [](int32_t j) -> int32_t { return WIDE ? (j < 64 ? 0 : 1 + ((j - 64) >> 7)) : (j >> 6); };
-  auto lane_of = [](int32_t j) -> int32_t { return WIDE && j >= 64 ? ((j - 64) & 127) >> 1 : (j & 63); };
-  constexpr int kStride = WIDE ? kSlotIntsW : kSlotInts;
+  // 64-column strips
+  const int32_t nstrips = static_cast<int32_t>(LS >> 6);
+  auto strip_of = [](int32_t j) -> int32_t { return j >> 6; };
+  auto lane_of = [](int32_t j) -> int32_t { return j & 63; };
+  constexpr int kStride = kSlotInts;
   const uint32_t nslot = LDSP ? lds_slots : J.n_slots;
   int32_t* __restrict__ pool;  // this wave's pool: nslot x {H, F, O} x 64, then nslot boundary H
   if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * kStride;
@@ -341,10 +255,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   const int32_t cg = imax(imax(P.g, P.e), imax(P.q, P.c));  // best per-base gap score (<= 0, host-checked)
   uint32_t rows_done = 0;
 
-#ifdef SVS_STRIP_PROF
-  uint64_t pr_wait = 0, pr_ff = 0, pr_ffwait = 0, pr_ffn = 0, pr_slow = 0;
-  const uint64_t pr_t0 = SVS_PROF_T();
-#endif
   auto sweep = [&](auto first_tag, int32_t s) {
     constexpr bool FIRST = decltype(first_tag)::value;
     const int32_t j0 = s << 6;
@@ -353,13 +263,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     uint16_t* __restrict__ tbl = tbj + j;  // this lane's column of the traceback codes
     const int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
     int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
-#ifdef SVS_OPT_CARRY
-    // this strip's carry block as a raw buffer: lanes other than 63 store out
-    // of range (offset >= 2^31 > the block size), which the hardware drops
-    const __amdgpu_buffer_rsrc_t bout_rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(bout, 0, static_cast<int32_t>(VP * 16), 0x00020000);
-    const uint32_t lane63_off = lane == 63 ? 0u : 0x80000000u;
-#endif
     const int32_t pw = (wave + WPJ - 1) % WPJ;          // producer of strip s-1
     const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
     int32_t avail = -1;                                  // producer progress seen so far
@@ -377,9 +280,11 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     constexpr uint32_t kRegBit = 1u << 31;
     uint32_t alive = (FIRST || !prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb) ? 1u : 0u;
     const int32_t rrem = L - j;              // read bases after column j
-    // lanes past column L are never alive: their m rr term is VNEG/2, so
-    // H + ub stays below every real bound (no overflow: H >= VNEG - gaps);
-    // the liveness ballot then needs no rrem >= 0 lane mask
+    // lanes past column L are never alive for a real bound: their m rr term
+    // is VNEG/2, so H + ub stays below -5e8 while prune_bound keeps real
+    // bounds >= -1e8 (no overflow: H >= VNEG - gaps); a kPruneAll job may see
+    // them alive, which only keeps rows it computes anyway.  The liveness
+    // ballot then needs no rrem >= 0 lane mask
     const int32_t mrr = rrem >= 0 ? P.m * rrem : SVS_VNEG / 2;
     // every lane tracks its own sink maximum; only the lane of column L in
     // the last strip (which owns L, swept last by its wave) is read
@@ -434,13 +339,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         if (WPJ > 1) {
           const int32_t need = need0 + static_cast<int32_t>(rr) + 1;
           if (avail < need) {
-#ifdef SVS_STRIP_PROF
-            const uint64_t tw = SVS_PROF_T();
             avail = strip_wait_ge(&prog[pw], need, &s_err);
-            pr_wait += SVS_PROF_T() - tw;
-#else
-            avail = strip_wait_ge(&prog[pw], need, &s_err);
-#endif
           }
         }
         const int4 v = *reinterpret_cast<const int4*>(reinterpret_cast<const char*>(bin) + (rr << 4));
@@ -502,9 +401,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
           // own slot dead, slots whose last reader this row is (w3) released
           alive &= ~(__builtin_amdgcn_readfirstlane(d.w3) | own_bit | kRegBit);
           pH = pF = pO = pHm = SVS_VNEG;
-#ifdef SVS_STRIP_PROF
-          pr_slow += 1;
-#endif
           if (write_bnd && lane == 0)
             *reinterpret_cast<int4*>(reinterpret_cast<char*>(bout) + (r << 4)) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
           publish();
@@ -553,9 +449,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       };
       int32_t H, F, O, Q, E, prevH, prevEe, prevQc;  // prevEe = E[j-1] + e, prevQc = Q[j-1] + c
       uint32_t code;
-      int32_t Hpre_keep = 0;  // this row's Hpre (SVS_OPT_CARRY: lane 63's is a carry)
       auto gaps = [&](int32_t Hpre, bool inner_) {
-        Hpre_keep = Hpre;
         if (FIRST) {
           int32_t prevQ, prevE;
           strip_gaps(P, lane, j, j0, inner_, Hpre, H0, cr, Q, E, H, prevQ, prevE, prevH);
@@ -571,17 +465,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const uint32_t ps = __builtin_amdgcn_readfirstlane(d.w1) & 0xFFFFu;  // np == 0: slot 0 (virtual row)
         int32_t hp, fp, op, hpm;
         pred_vals(ps, hp, fp, op, hpm);
-#ifdef SVS_OPT_CODE
-        if constexpr (!FIRST) {
-          const int32_t hpg = hp + P.g, fpe = fp + P.e, hpq = hp + P.q, opc = op + P.c, D = hpm + mc;
-          F = imax(hpg, fpe);
-          O = imax(hpq, opc);
-          gaps(imax(D, imax(F, O)), true);
-          code = code_np1(H, D, imax(F, O), imax(E, Q), fpe, hpg, opc, hpq, prevEe, prevH + P.g, prevQc,
-                          prevH + P.q, E, Q, F, O);
-          if (np == 0) code = (code & 0x1FFu) | (31u << 10);
-        } else
-#endif
         {
         F = imax(hp + P.g, fp + P.e);
         O = imax(hp + P.q, op + P.c);
@@ -683,23 +566,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       // 32-bit row offset off this lane's column: the host keeps n_rows x ls
       // below 2^31 per job
       tbl[r * LS] = static_cast<uint16_t>(code);
-#ifdef SVS_PROBE_SALU
-      // development probe: extra scalar work per computed row (issue-bound test)
-      {
-        uint32_t z = w0;
-#pragma unroll
-        for (int q = 0; q < SVS_PROBE_SALU; ++q) asm volatile("s_add_u32 %0, %0, 1" : "+s"(z));
-        asm volatile("" ::"s"(z));
-      }
-#endif
-#ifdef SVS_PROBE_VALU
-      {
-        uint32_t z = code;
-#pragma unroll
-        for (int q = 0; q < SVS_PROBE_VALU; ++q) asm volatile("v_add_u32 %0, %0, %0" : "+v"(z));
-        asm volatile("" ::"v"(z));
-      }
-#endif
       bool any_alive = true;
       if (prune) {
         const int32_t ub = ub_of(w2w3.x, rrem, mrr);
@@ -720,17 +586,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       pF = F;
       pO = O;
       pHm = prevH;
-#ifdef SVS_OPT_CARRY
-      if (!FIRST) {
-        if (write_bnd) {
-          // every lane issues the store; only lane 63's offset is in range
-          // (raw buffer, bounds-checked): no exec-mask branch per row
-          svs_i32x4 v = {Q - K.jc, E - K.je, Hpre_keep, H};
-          if (!any_alive) v = svs_i32x4{SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG};
-          __builtin_amdgcn_raw_buffer_store_b128(v, bout_rsrc, lane63_off + 16u * r, 0, 0);
-        }
-      } else
-#endif
       if (write_bnd && lane == 0) {
         *reinterpret_cast<int4*>(reinterpret_cast<char*>(bout) + (r << 4)) =
             any_alive ? make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH) : make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
@@ -749,10 +604,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     // Scans 64 rows per step with one load per lane, hands VNEG carries on for
     // the rows it passes, and returns the first row with such an input (or V).
     auto fast_forward = [&](uint32_t r) -> uint32_t {
-#ifdef SVS_STRIP_PROF
-      const uint64_t tf = SVS_PROF_T();
-      pr_ffn += 1;
-#endif
       while (r < V) {
         uint32_t lim = min(64u, V - r);  // rows this step may look at
         if (!FIRST && WPJ > 1) {
@@ -760,13 +611,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
           // is not waited for, so the scan keeps pace with its producer
           const int32_t least = need0 + static_cast<int32_t>(min(V, r + 8));
           if (avail < least) {
-#ifdef SVS_STRIP_PROF
-            const uint64_t tw = SVS_PROF_T();
             avail = strip_wait_ge(&prog[pw], least, &s_err);
-            pr_ffwait += SVS_PROF_T() - tw;
-#else
-            avail = strip_wait_ge(&prog[pw], least, &s_err);
-#endif
           }
           lim = min(lim, static_cast<uint32_t>(min(static_cast<int32_t>(V), avail - need0)) - r);
         }
@@ -803,9 +648,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(done),
                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-#ifdef SVS_STRIP_PROF
-      pr_ff += SVS_PROF_T() - tf;
-#endif
       return r;
     };
     auto dead_strip = [&]() { return (alive & ~1u) == 0; };
@@ -849,411 +691,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     __builtin_amdgcn_wave_barrier();
   };
 
-  // Wide strips (WIDE; every strip after the first): strip s >= 1 spans the
-  // 128 columns j0 .. j0+127, j0 = 64 + 128 (s-1), and lane l owns the column
-  // pair ja = j0 + 2l (element a) and jb = ja + 1 (element b).  A row then
-  // costs one record decode, one branch and one set of scalar bookkeeping per
-  // 128 cells instead of per 64; the horizontal-gap scans run over the 64
-  // per-lane pair maxima and are completed per element (gaps_w).  The values
-  // and traceback codes are those of sweep's: the same recurrence, the same
-  // tests.  Pool slot (kSlotIntsW words): Hx[i] = H at column j0 - 2 + i for
-  // i = 1 .. 129 (a lane's pair at the even index 2l + 2: one 8-B LDS access),
-  // then 64 words of F/O pairs (pack_fo of a | pack_fo of b << 16).
-  auto sweep_w = [&](int32_t s) {
-    const int32_t j0 = 64 + ((s - 1) << 7);
-    const int32_t ja = j0 + 2 * lane, jb = ja + 1;
-    const uint8_t rca = seq[ja - 1], rcb = seq[ja];
-    const int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s - 1) * VP * 4;
-    int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
-    const int32_t pw = (wave + WPJ - 1) % WPJ;
-    const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
-    int32_t avail = -1;
-    const bool write_bnd = s + 1 < nstrips;
-    const bool owns_L = strip_of(L) == s;
-    const bool L_b = ((L - j0) & 1) != 0;
-    constexpr uint32_t kRegBit = 1u << 31;
-    uint32_t alive = (!prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb) ? 1u : 0u;
-    const int32_t rra = L - ja, rrb = L - jb;
-    const int32_t mra = P.m * rra, mrb = P.m * rrb;
-    // strip 0 (sweep) lets every lane track a sink maximum: start clean
-    best = SVS_NEG_INF;
-    best_row = 0;
-    auto ub_of = [&](uint32_t w2, int32_t rr, int32_t mr) -> int32_t {
-      const int32_t dmin = static_cast<int32_t>(w2 & 0xFFFFu), dmax = static_cast<int32_t>(w2 >> 16);
-      const int32_t d = min(imax(rr, dmin), dmax) - rr;
-      return mr + d * (d >= 0 ? cg : P.m - cg);
-    };
-    // lane constants of both elements (strip_gaps_nf's, per column)
-    const int32_t qjc_a = P.q - ja * P.c, qjc_b = qjc_a - P.c;
-    const int32_t k1_a = (P.g - ja * P.e) - qjc_a, k1_b = (P.g - jb * P.e) - qjc_b;
-    const int32_t k2_a = (ja - 1) * P.c + P.g - ja * P.e, k2_b = ja * P.c + P.g - jb * P.e;
-    const int32_t jc_a = ja * P.c, jc_b = jb * P.c, je_a = ja * P.e, je_b = jb * P.e;
-    const int32_t ve = P.e, vc = P.c;
-    // virtual row 0 in slot 0
-    {
-      const int32_t ha = row0_h(P, ja), hb = row0_h(P, jb);
-      *reinterpret_cast<svs_i32x2*>(pool + 2 * lane + 2) = svs_i32x2{ha, hb};
-      pool[2 * lane + 1] = row0_h(P, ja - 1);
-      reinterpret_cast<uint32_t*>(pool + 130)[lane] =
-          pack_fo(ha, SVS_NEG_INF, SVS_NEG_INF, tF, tO) | (pack_fo(hb, SVS_NEG_INF, SVS_NEG_INF, tF, tO) << 16);
-    }
-    __builtin_amdgcn_wave_barrier();
-
-    auto fetch = [&](RowIn& d, uint32_t r) {
-      const uint32_t rr = r < V ? r : V - 1;
-      const uint32_t* w = rec + rr * kRecWords;  // 32-bit: a job has < 2^30 rows
-      d.w0 = w[0];
-      d.w1 = w[1];
-      if constexpr (PRUNE) {
-        d.w2 = w[2];
-        d.w3 = w[3];
-      }
-      if (WPJ > 1) {
-        const int32_t need = need0 + static_cast<int32_t>(rr) + 1;
-        if (avail < need) avail = strip_wait_ge(&prog[pw], need, &s_err);
-      }
-      const int4 v = *reinterpret_cast<const int4*>(bin + 4u * rr);
-      d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
-    };
-
-    // the row just above (registers): H, F, O of both elements and H[ja - 1]
-    int32_t pHa = 0, pHb = 0, pFa = 0, pFb = 0, pOa = 0, pOb = 0, pHma = 0;
-    struct ColW {
-      int32_t Q, E, H, prevH, prevEe, prevQc;  // prevEe = E[j-1] + e, prevQc = Q[j-1] + c
-    };
-    // strip_gaps_nf over 128 columns: the scans of P1 and of u (P2's first
-    // term) run over the lane maxima max(a, b); a lane's element a then adds the
-    // exclusive prefix of the lanes before it, element b is the inclusive one.
-    // P2's second term P1[j-1] + k2[j] reads the exclusive prefix for a and
-    // element a's own prefix for b.  The strip's first column (lane 0, a) has
-    // no P1[j0-1] in the strip (exclusive prefix VNEG), and its T2 term equals
-    // T1 (cQ = (j0-1) c + run1), so it needs no lane-0 special case.
-    auto gaps_w = [&](int32_t Hpa, int32_t Hpb, StripCarry& cr, ColW& A_, ColW& B_) {
-      const int32_t p1a = shr1_add(cr.cHpre + qjc_a, Hpb, qjc_a);  // Hpre[ja-1] + q - ja c
-      const int32_t p1b = Hpa + qjc_b;
-      const int32_t ua = p1a + k1_a, ub = p1b + k1_b;
-      int32_t w1 = imax(p1a, p1b), w2 = imax(ua, ub);
-      wave_prefix_max2(w1, w2);
-      const int32_t x1 = wave_shr1(w1, SVS_VNEG, lane), x2 = wave_shr1(w2, SVS_VNEG, lane);
-      const int32_t s1a = imax(x1, p1a);
-      const int32_t p2a = imax(imax(x2, ua), x1 + k2_a);
-      const int32_t p2b = imax(w2, s1a + k2_b);
-      const int32_t T1 = cr.cQ + P.g - j0 * P.e;
-      const int32_t r2 = imax(cr.run2, T1);
-      A_.Q = jc_a + imax(s1a, cr.run1);
-      B_.Q = jc_b + imax(w1, cr.run1);
-      A_.E = je_a + imax(imax(p2a, r2), cr.run1 + k2_a);
-      B_.E = je_b + imax(imax(p2b, r2), cr.run1 + k2_b);
-      A_.H = imax(Hpa, imax(A_.E, A_.Q));
-      B_.H = imax(Hpb, imax(B_.E, B_.Q));
-      A_.prevH = wave_shr1(B_.H, cr.cH, lane);
-      B_.prevH = A_.H;
-      A_.prevEe = shr1_add(cr.cE + P.e, B_.E, ve);
-      B_.prevEe = A_.E + P.e;
-      A_.prevQc = shr1_add(cr.cQ + P.c, B_.Q, vc);
-      B_.prevQc = A_.Q + P.c;
-      // carries into strip s+1, from lane 63's element b (column jl)
-      const int32_t jl = j0 + 127;
-      const int32_t p1l = readlane63(w1), p2l = readlane63(p2b), hl = readlane63(Hpb);
-      const int32_t T2l = cr.run1 + (jl - 1) * P.c + P.g - jl * P.e;
-      cr.run2 = imax(imax(cr.run2, p2l), imax(T1, T2l));
-      cr.run1 = imax(cr.run1, p1l);
-      cr.cQ = jl * P.c + cr.run1;
-      cr.cE = jl * P.e + cr.run2;
-      cr.cHpre = hl;
-      cr.cH = imax(hl, imax(cr.cE, cr.cQ));
-    };
-    // traceback code of a cell with at most one in-edge (sweep's np <= 1 tests)
-    auto code1 = [&](const ColW& c, int32_t D, int32_t F, int32_t O, int32_t hp, int32_t fp, int32_t op,
-                     uint32_t np) -> uint32_t {
-      const bool dg = c.H == D;
-      const bool up = c.H == imax(F, O);
-      const bool ua = c.H == fp + P.e, ub = c.H == hp + P.g, uc = c.H == op + P.c;
-      const bool lf = c.H == imax(c.E, c.Q);
-      const bool la = c.H == c.prevEe, lg = c.H == c.prevH + P.g, lc = c.H == c.prevQc;
-      const bool lbit = c.prevH + P.g == c.E || c.prevH + P.q == c.Q;
-      const bool va = F == hp + P.g, vb = F == fp + P.e, vq = O == hp + P.q;
-      const uint32_t upc = (ua || (!ub && uc)) ? 5u : 1u;
-      const uint32_t lfc = (la || (!lg && lc)) ? 6u : 2u;
-      uint32_t code = dg ? 0u : (up ? upc : (lf ? lfc : 3u));
-      code |= lbit ? 0x100u : 0u;
-      if (np != 0) code |= (va || (!vb && vq)) ? 0x200u : 0u;
-      else code |= 31u << 10;
-      return code;
-    };
-    // two in-edges (sweep's np == 2 tests)
-    auto code2 = [&](const ColW& c, int32_t F, int32_t O, int32_t F0k, int32_t O0k, int32_t F1k, int32_t O1k,
-                     int32_t D0, int32_t D1, int32_t hp0, int32_t fp0, int32_t op0, int32_t hp1, int32_t fp1,
-                     int32_t op1) -> uint32_t {
-      const bool up0 = c.H == imax(F0k, O0k), up1 = c.H == imax(F1k, O1k);
-      const int32_t hpu = up0 ? hp0 : hp1, fpu = up0 ? fp0 : fp1, opu = up0 ? op0 : op1;
-      const bool ua = c.H == fpu + P.e, ub = c.H == hpu + P.g, uc = c.H == opu + P.c;
-      const bool ch0 = F == F0k || O == O0k;
-      const int32_t hpc = ch0 ? hp0 : hp1, fpc = ch0 ? fp0 : fp1;
-      const bool va = F == hpc + P.g, vb = F == fpc + P.e, vq = O == hpc + P.q;
-      const bool lf = c.H == imax(c.E, c.Q);
-      const bool la = c.H == c.prevEe, lg = c.H == c.prevH + P.g, lc = c.H == c.prevQc;
-      const bool lbit = c.prevH + P.g == c.E || c.prevH + P.q == c.Q;
-      const uint32_t upc = ((ua || (!ub && uc)) ? 5u : 1u) | (up0 ? 0u : 8u);
-      const uint32_t lfc = (la || (!lg && lc)) ? 6u : 2u;
-      uint32_t code = c.H == D0 ? 0u : (c.H == D1 ? 8u : (up0 || up1 ? upc : (lf ? lfc : 3u)));
-      code |= lbit ? 0x100u : 0u;
-      code |= ((va || (!vb && vq)) ? 0x200u : 0u) | (ch0 ? 0u : (1u << 10));
-      return code;
-    };
-
-    auto step = [&](uint32_t r, const RowIn& d) {
-      const uint32_t w0 = __builtin_amdgcn_readfirstlane(d.w0);
-      const uint32_t nb = w0 & 0xFFu;
-      const bool sink = (w0 >> 8) & 1u;
-      const bool store = (w0 >> 9) & 1u;
-      const uint32_t np = (w0 >> 10) & 31u;
-      const uint32_t own = w0 >> 16;
-      auto slot_alive = [&](uint32_t ps) -> bool {
-        if (ps == kNoSlot) return (alive >> 31) != 0;
-        return ps >= 31u || ((alive >> ps) & 1u) != 0;
-      };
-      const uint32_t own_bit = (store && own < 31u) ? 1u << own : 0u;
-      auto publish = [&]() {
-        if (WPJ > 1 && write_bnd && ((r & 7u) == 7u || r + 1 == V) && lane == 0)
-          __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
-                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      };
-      const int32_t cH_in = __builtin_amdgcn_readfirstlane(d.b3);
-      if (prune) {
-        bool live = cH_in > SVS_VNEG / 2;
-        if (!live) {
-          const uint32_t wp = __builtin_amdgcn_readfirstlane(d.w1);
-          live = slot_alive(wp & 0xFFFFu) || (np >= 2 && slot_alive(wp >> 16));
-          if (!live && np > kInlinePreds) {
-            const uint32_t* __restrict__ spill = pslot + rps[r];
-            for (uint32_t k = kInlinePreds; k < np && !live; ++k)
-              live = slot_alive(__builtin_amdgcn_readfirstlane(spill[k]));
-          }
-        }
-        if (!live) {
-          if (store) {
-            int32_t* q = pool + own * kSlotIntsW;
-            *reinterpret_cast<svs_i32x2*>(q + 2 * lane + 2) = svs_i32x2{SVS_VNEG, SVS_VNEG};
-            q[2 * lane + 1] = SVS_VNEG;
-            reinterpret_cast<uint32_t*>(q + 130)[lane] = 0;  // F = O = H = VNEG
-          }
-          alive &= ~(__builtin_amdgcn_readfirstlane(d.w3) | own_bit | kRegBit);
-          pHa = pHb = pFa = pFb = pOa = pOb = pHma = SVS_VNEG;
-          if (write_bnd && lane == 0)
-            *reinterpret_cast<int4*>(bout + 4u * r) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
-          publish();
-          return;
-        }
-      }
-      if constexpr (PRUNE) rows_done += 2;  // in 64-column strip rows
-      uint2 w2w3 = make_uint2(0, 0);
-      if constexpr (PRUNE)
-        w2w3 = make_uint2(__builtin_amdgcn_readfirstlane(d.w2), __builtin_amdgcn_readfirstlane(d.w3));
-      StripCarry cr;
-      {
-        const int32_t jl = j0 - 1;
-        cr.run1 = __builtin_amdgcn_readfirstlane(d.b0);
-        cr.run2 = __builtin_amdgcn_readfirstlane(d.b1);
-        cr.cHpre = __builtin_amdgcn_readfirstlane(d.b2);
-        cr.cH = cH_in;
-        cr.cQ = jl * P.c + cr.run1;
-        cr.cE = jl * P.e + cr.run2;
-      }
-      const int32_t mca = rca == nb ? P.m : P.n, mcb = rcb == nb ? P.m : P.n;
-      // in-edge k: H, F, O at ja, jb and H at ja - 1 (H at jb - 1 is H at ja)
-      auto pred_w = [&](uint32_t ps, int32_t& hpa, int32_t& hpb, int32_t& fpa, int32_t& fpb, int32_t& opa,
-                        int32_t& opb, int32_t& hma) {
-        if (ps == kNoSlot) {
-          hpa = pHa; hpb = pHb; fpa = pFa; fpb = pFb; opa = pOa; opb = pOb; hma = pHma;
-        } else {
-          const int32_t* q = pool + ps * kSlotIntsW;
-          const svs_i32x2 hh = __builtin_nontemporal_load(reinterpret_cast<const svs_i32x2*>(q + 2 * lane + 2));
-          hma = __builtin_nontemporal_load(q + 2 * lane + 1);
-          const uint32_t dd = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(q + 130) + lane);
-          hpa = hh.x;
-          hpb = hh.y;
-          fpa = hpa - static_cast<int32_t>(dd & 0xFFu);
-          opa = hpa - static_cast<int32_t>((dd >> 8) & 0xFFu);
-          fpb = hpb - static_cast<int32_t>((dd >> 16) & 0xFFu);
-          opb = hpb - static_cast<int32_t>(dd >> 24);
-        }
-      };
-      ColW A_, B_;
-      int32_t Fa, Fb, Oa, Ob;
-      uint32_t ca, cb;
-      if (np <= 1) {
-        const uint32_t ps = __builtin_amdgcn_readfirstlane(d.w1) & 0xFFFFu;  // np == 0: slot 0 (virtual row)
-        int32_t hpa, hpb, fpa, fpb, opa, opb, hma;
-        pred_w(ps, hpa, hpb, fpa, fpb, opa, opb, hma);
-        Fa = imax(hpa + P.g, fpa + P.e);
-        Oa = imax(hpa + P.q, opa + P.c);
-        Fb = imax(hpb + P.g, fpb + P.e);
-        Ob = imax(hpb + P.q, opb + P.c);
-        const int32_t Da = hma + mca, Db = hpa + mcb;
-        gaps_w(imax(Da, imax(Fa, Oa)), imax(Db, imax(Fb, Ob)), cr, A_, B_);
-        ca = code1(A_, Da, Fa, Oa, hpa, fpa, opa, np);
-        cb = code1(B_, Db, Fb, Ob, hpb, fpb, opb, np);
-      } else if (np == 2) {
-        const uint32_t wp = __builtin_amdgcn_readfirstlane(d.w1);
-        int32_t hp0a, hp0b, fp0a, fp0b, op0a, op0b, hm0a, hp1a, hp1b, fp1a, fp1b, op1a, op1b, hm1a;
-        pred_w(wp & 0xFFFFu, hp0a, hp0b, fp0a, fp0b, op0a, op0b, hm0a);
-        pred_w(wp >> 16, hp1a, hp1b, fp1a, fp1b, op1a, op1b, hm1a);
-        const int32_t F0a = imax(hp0a + P.g, fp0a + P.e), O0a = imax(hp0a + P.q, op0a + P.c);
-        const int32_t F1a = imax(hp1a + P.g, fp1a + P.e), O1a = imax(hp1a + P.q, op1a + P.c);
-        const int32_t F0b = imax(hp0b + P.g, fp0b + P.e), O0b = imax(hp0b + P.q, op0b + P.c);
-        const int32_t F1b = imax(hp1b + P.g, fp1b + P.e), O1b = imax(hp1b + P.q, op1b + P.c);
-        Fa = imax(F0a, F1a);
-        Oa = imax(O0a, O1a);
-        Fb = imax(F0b, F1b);
-        Ob = imax(O0b, O1b);
-        const int32_t D0a = hm0a + mca, D1a = hm1a + mca, D0b = hp0a + mcb, D1b = hp1a + mcb;
-        gaps_w(imax(imax(D0a, D1a), imax(Fa, Oa)), imax(imax(D0b, D1b), imax(Fb, Ob)), cr, A_, B_);
-        ca = code2(A_, Fa, Oa, F0a, O0a, F1a, O1a, D0a, D1a, hp0a, fp0a, op0a, hp1a, fp1a, op1a);
-        cb = code2(B_, Fb, Ob, F0b, O0b, F1b, O1b, D0b, D1b, hp0b, fp0b, op0b, hp1b, fp1b, op1b);
-      } else {
-        const uint32_t* __restrict__ spill = pslot + rps[r];
-        Fa = Fb = Oa = Ob = SVS_VNEG;
-        int32_t Hda = SVS_VNEG, Hdb = SVS_VNEG;
-        for (uint32_t k = 0; k < np; ++k) {
-          int32_t hpa, hpb, fpa, fpb, opa, opb, hma;
-          pred_w(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hpa, hpb, fpa, fpb, opa, opb, hma);
-          Fa = imax(Fa, imax(hpa + P.g, fpa + P.e));
-          Oa = imax(Oa, imax(hpa + P.q, opa + P.c));
-          Fb = imax(Fb, imax(hpb + P.g, fpb + P.e));
-          Ob = imax(Ob, imax(hpb + P.q, opb + P.c));
-          Hda = imax(Hda, hma + mca);
-          Hdb = imax(Hdb, hpa + mcb);
-        }
-        gaps_w(imax(Hda, imax(Fa, Oa)), imax(Hdb, imax(Fb, Ob)), cr, A_, B_);
-        uint32_t dka = 31, uka = 31, uea = 0, cka = 31, csa = 0;
-        uint32_t dkb = 31, ukb = 31, ueb = 0, ckb = 31, csb = 0;
-        for (uint32_t k = 0; k < np; ++k) {
-          int32_t hpa, hpb, fpa, fpb, opa, opb, hma;
-          pred_w(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hpa, hpb, fpa, fpb, opa, opb, hma);
-          auto tests = [&](const ColW& c, int32_t F, int32_t O, int32_t hp, int32_t fp, int32_t op, int32_t D,
-                           uint32_t& dk, uint32_t& uk, uint32_t& ue, uint32_t& ck, uint32_t& cs) {
-            if (dk == 31 && c.H == D) dk = k;
-            if (uk == 31) {
-              const bool a = c.H == fp + P.e, b = c.H == hp + P.g, cc = c.H == op + P.c, dd = c.H == hp + P.q;
-              if (a || b || cc || dd) { uk = k; ue = (a || (!b && cc)) ? 1u : 0u; }
-            }
-            if (ck == 31) {
-              const bool a = F == hp + P.g, b = F == fp + P.e, cc = O == hp + P.q, dd = O == op + P.c;
-              if (a || b || cc || dd) { ck = k; cs = (a || (!b && cc)) ? 1u : 0u; }
-            }
-          };
-          tests(A_, Fa, Oa, hpa, fpa, opa, hma + mca, dka, uka, uea, cka, csa);
-          tests(B_, Fb, Ob, hpb, fpb, opb, hpa + mcb, dkb, ukb, ueb, ckb, csb);
-        }
-        auto left = [&](const ColW& c, uint32_t dk, uint32_t uk, uint32_t ue, uint32_t ck, uint32_t cs) {
-          const bool la = c.H == c.prevEe, lg = c.H == c.prevH + P.g;
-          const bool lc = c.H == c.prevQc, ld = c.H == c.prevH + P.q;
-          const bool lbit = c.prevH + P.g == c.E || c.prevH + P.q == c.Q;
-          return assemble_code(dk, uk, ue, la || lg || lc || ld, la || (!lg && lc), lbit, ck, cs);
-        };
-        ca = left(A_, dka, uka, uea, cka, csa);
-        cb = left(B_, dkb, ukb, ueb, ckb, csb);
-      }
-      *reinterpret_cast<uint32_t*>(tbj + static_cast<uint64_t>(r) * LS + ja) = (ca & 0xFFFFu) | (cb << 16);
-      bool any_alive = true;
-      if (prune) {
-        const int32_t uba = ub_of(w2w3.x, rra, mra), ubb = ub_of(w2w3.x, rrb, mrb);
-        any_alive = __builtin_amdgcn_ballot_w64((rra >= 0 && A_.H + uba >= lb) || (rrb >= 0 && B_.H + ubb >= lb)) != 0;
-        const bool out_alive = any_alive || cH_in > SVS_VNEG / 2;
-        const uint32_t ob = own_bit | kRegBit;
-        alive = ((alive & ~ob) | (out_alive ? ob : 0u)) & ~w2w3.y;
-      }
-      if (store) {
-        int32_t* q = pool + own * kSlotIntsW;
-        *reinterpret_cast<svs_i32x2*>(q + 2 * lane + 2) = svs_i32x2{A_.H, B_.H};
-        q[2 * lane + 1] = A_.prevH;
-        reinterpret_cast<uint32_t*>(q + 130)[lane] = pack_fo(A_.H, Fa, Oa, tF, tO) | (pack_fo(B_.H, Fb, Ob, tF, tO) << 16);
-      }
-      pHa = A_.H;
-      pHb = B_.H;
-      pFa = Fa;
-      pFb = Fb;
-      pOa = Oa;
-      pOb = Ob;
-      pHma = A_.prevH;
-      if (write_bnd && lane == 0) {
-        *reinterpret_cast<int4*>(bout + 4u * r) =
-            any_alive ? make_int4(cr.run1, cr.run2, cr.cHpre, cr.cH) : make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
-      }
-      publish();
-      if (sink && owns_L) {
-        const int32_t HL = L_b ? B_.H : A_.H;
-        if ((ja == L || jb == L) && HL > best) { best = HL; best_row = static_cast<int32_t>(r) + 1; }
-      }
-    };
-
-    // sweep's fast_forward for a strip after the first
-    auto fast_forward = [&](uint32_t r) -> uint32_t {
-      while (r < V) {
-        uint32_t lim = min(64u, V - r);
-        if (WPJ > 1) {
-          const int32_t least = need0 + static_cast<int32_t>(min(V, r + 8));
-          if (avail < least) avail = strip_wait_ge(&prog[pw], least, &s_err);
-          lim = min(lim, static_cast<uint32_t>(min(static_cast<int32_t>(V), avail - need0)) - r);
-        }
-        const uint32_t rr = r + static_cast<uint32_t>(lane);
-        const bool in = static_cast<uint32_t>(lane) < lim;
-        bool cand = false;
-        if (in) cand = __builtin_nontemporal_load(bin + 4ull * rr + 3) > SVS_VNEG / 2;
-        if ((alive & 1u) && in) cand = cand || ((rec[static_cast<uint64_t>(rr) * kRecWords] >> 10) & 31u) == 0;
-        const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
-        const uint32_t n = m ? static_cast<uint32_t>(__builtin_ctzll(m)) : lim;
-        if (write_bnd && static_cast<uint32_t>(lane) < n)
-          *reinterpret_cast<int4*>(bout + 4ull * rr) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
-        r += n;
-        if (m) break;
-      }
-      for (uint32_t p = 1; p < nslot; ++p) {
-        int32_t* q = pool + p * kSlotIntsW;
-        *reinterpret_cast<svs_i32x2*>(q + 2 * lane + 2) = svs_i32x2{SVS_VNEG, SVS_VNEG};
-        q[2 * lane + 1] = SVS_VNEG;
-        reinterpret_cast<uint32_t*>(q + 130)[lane] = 0;
-      }
-      pHa = pHb = pFa = pFb = pOa = pOb = pHma = SVS_VNEG;
-      if (WPJ > 1 && write_bnd && lane == 0) {
-        const uint32_t done = r >= V ? V : (r & ~7u);
-        __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(done),
-                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      return r;
-    };
-    auto dead_strip = [&]() { return (alive & ~1u) == 0; };
-
-    RowIn A, B;
-    uint32_t r = 0;
-    if (prune) r = fast_forward(0);
-    fetch(A, r);
-    fetch(B, r + 1);
-    while (r < V) {
-      step(r, A);
-      if (prune && dead_strip()) {
-        r = fast_forward(r + 1);
-        fetch(A, r);
-        fetch(B, r + 1);
-        continue;
-      }
-      fetch(A, r + 2);
-      if (r + 1 >= V) break;
-      step(r + 1, B);
-      if (prune && dead_strip()) {
-        r = fast_forward(r + 2);
-        fetch(A, r);
-        fetch(B, r + 1);
-        continue;
-      }
-      fetch(B, r + 3);
-      r += 2;
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-  };
-
   if (WPJ > 1) {
     if (lane == 0) {
       prog[wave] = -1;
@@ -1266,20 +703,9 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     using FalseT = std::integral_constant<bool, false>;
     for (int32_t s = wave; s < nstrips; s += WPJ) {
       if (s == 0) sweep(TrueT{}, 0);
-      else if constexpr (WIDE) sweep_w(s);
       else sweep(FalseT{}, s);
     }
   }
-#ifdef SVS_STRIP_PROF
-  SVS_PROF_ADD(0, SVS_PROF_T() - pr_t0);
-  SVS_PROF_ADD(1, pr_wait);
-  SVS_PROF_ADD(2, pr_ff);
-  SVS_PROF_ADD(3, pr_ffwait);
-  SVS_PROF_ADD(4, rows_done);
-  SVS_PROF_ADD(5, pr_ffn);
-  SVS_PROF_ADD(6, pr_slow);
-  SVS_PROF_ADD(7, 1);
-#endif
 
   // the owner of column L's strip holds the sink maximum; every wave's
   // traceback-code stores must be visible to wave 0's lane 0
@@ -1379,126 +805,59 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   if (lane == 0) aln_len[job_id] = nout;
 }
 
-namespace {
-
-template <bool LP>
-const void* strip_kernel_ptr(int w) {
-  switch (w) {
-    case 16: return LP ? reinterpret_cast<const void*>(&poa_strip_kernel<true, 16, false, false>) : nullptr;
-    case 8: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 8, false, false>);
-    case 7: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 7, false, false>);
-    case 6: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 6, false, false>);
-    case 5: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 5, false, false>);
-    case 4: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 4, false, false>);
-    case 3: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 3, false, false>);
-    case 2: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 2, false, false>);
-    default: return reinterpret_cast<const void*>(&poa_strip_kernel<LP, 1, false, false>);
-  }
-}
-
-}  // namespace
-
-// Waves per job for a launch: the largest WPJ (1..8, each wave keeping >= 6
-// strips) for which every job's workgroup is resident at once, from the
-// kernel's register count and the LDS its pool needs; jobs that do not all fit
-// even at WPJ = 1 run with WPJ = 1.  (Non-resident workgroups would start only
-// when others finish: a tail of whole job lengths.)
-int choose_strip_wpj(int device, size_t n_jobs, uint32_t lds_slots, uint32_t min_strips) {
-  static int n_cu = 0, lds_cu = 0;
-  if (n_cu == 0) {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 1;
-    n_cu = prop.multiProcessorCount;
-    lds_cu = static_cast<int>(prop.maxSharedMemoryPerMultiProcessor);
-    if (lds_cu <= 0) lds_cu = 160 * 1024;
-  }
-  const bool lds_pool = lds_slots > 0;
-  int best = 1;
-  for (int w = 1; w <= 8; ++w) {
-    if (!lds_pool && (w & (w - 1))) continue;
-    if (w > 1 && min_strips < static_cast<uint32_t>(6 * w)) break;
-    hipFuncAttributes attr;
-    if (hipFuncGetAttributes(&attr, lds_pool ? strip_kernel_ptr<true>(w) : strip_kernel_ptr<false>(w)) != hipSuccess)
-      break;
-    const int vg = std::max(8, (attr.numRegs + 7) / 8 * 8);
-    const int waves_cu = 4 * std::min(8, 512 / vg);
-    int blocks_cu = waves_cu / w;
-    if (lds_pool) {
-      const int lds_block = w * static_cast<int>(lds_slots * kStripSlotBytes) + static_cast<int>(attr.sharedSizeBytes);
-      blocks_cu = std::min(blocks_cu, lds_cu / std::max(1, lds_block));
-    }
-    if (blocks_cu <= 0) break;
-    if (n_jobs <= static_cast<size_t>(blocks_cu) * n_cu) best = w;
-  }
-  return best;
-}
-
-#ifdef SVS_STRIP_PROF
-extern "C" int svs_debug_strip_prof(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(svs_strip_prof), sizeof(svs_strip_prof)) != hipSuccess) return -1;
-  if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(svs_strip_prof), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif
-
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   if (a.n_jobs <= 0) return hipSuccess;
   const int w = a.waves_per_job;
   const bool lds_pool = a.lds_slots > 0;
-  if (a.wide && !lds_pool) return hipErrorInvalidValue;  // wide strips keep their pool in LDS
-  const size_t slot_bytes = a.wide ? kStripSlotBytesWide : kStripSlotBytes;
-  const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * slot_bytes : 0;
-#define SVS_STRIP3(LP, W, PR, WD)                                                                                  \
-  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR, WD>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs,         \
-                     a.n_jobs, a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, \
-                     a.bnd, a.pool, a.aln, a.aln_len, a.lds_slots)
-#define SVS_STRIP(LP, W)                 \
-  do {                                   \
-    if (a.prune) {                       \
-      SVS_STRIP3(LP, W, true, false);    \
-    } else {                             \
-      SVS_STRIP3(LP, W, false, false);   \
-    }                                    \
+  const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * kStripSlotBytes : 0;
+#define SVS_STRIP3(LP, W, PR)                                                                                     \
+  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, a.n_jobs,  \
+                     a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.bnd,     \
+                     a.pool, a.aln, a.aln_len, a.lds_slots)
+#define SVS_STRIP(LP, W)              \
+  do {                                \
+    if (a.prune) {                    \
+      SVS_STRIP3(LP, W, true);        \
+    } else {                          \
+      SVS_STRIP3(LP, W, false);       \
+    }                                 \
   } while (0)
-#define SVS_STRIPW(W)                    \
-  do {                                   \
-    if (a.prune) {                       \
-      SVS_STRIP3(true, W, true, true);   \
-    } else {                             \
-      SVS_STRIP3(true, W, false, true);  \
-    }                                    \
-  } while (0)
-  if (a.wide) {
-    // wide strips: 1, 2, 4, 8 or 16 waves per job (the host's choices)
-    if (w >= 16) SVS_STRIPW(16);
-    else if (w >= 8) SVS_STRIPW(8);
-    else if (w >= 4) SVS_STRIPW(4);
-    else if (w >= 2) SVS_STRIPW(2);
-    else SVS_STRIPW(1);
-  } else if (lds_pool) {
+  // the engine's choices: 1, 2, 4, 8 waves per job (16 with the pool in LDS)
+  if (lds_pool) {
     switch (w) {
       case 16: SVS_STRIP(true, 16); break;
       case 8: SVS_STRIP(true, 8); break;
-      case 7: SVS_STRIP(true, 7); break;
-      case 6: SVS_STRIP(true, 6); break;
-      case 5: SVS_STRIP(true, 5); break;
       case 4: SVS_STRIP(true, 4); break;
-      case 3: SVS_STRIP(true, 3); break;
       case 2: SVS_STRIP(true, 2); break;
-      default: SVS_STRIP(true, 1); break;
+      case 1: SVS_STRIP(true, 1); break;
+      default: return hipErrorInvalidValue;
     }
   } else {
-    if (w >= 8) SVS_STRIP(false, 8);
-    else if (w >= 4) SVS_STRIP(false, 4);
-    else if (w >= 2) SVS_STRIP(false, 2);
-    else SVS_STRIP(false, 1);
+    switch (w) {
+      case 8: SVS_STRIP(false, 8); break;
+      case 4: SVS_STRIP(false, 4); break;
+      case 2: SVS_STRIP(false, 2); break;
+      case 1: SVS_STRIP(false, 1); break;
+      default: return hipErrorInvalidValue;
+    }
   }
-#undef SVS_STRIPW
 #undef SVS_STRIP
 #undef SVS_STRIP3
+  return hipGetLastError();
+}
+
+// Primitive self-test (tests/test_poa_gpu.py): per wave, the DPP inclusive
+// prefix max and the wave_shr1 lane shift the strip kernel's scans are built of.
+__global__ void wave_scan_selftest_kernel(const int32_t* in, int32_t* out_scan, int32_t* out_shift) {
+  const int lane = threadIdx.x & 63;
+  const int32_t x = in[blockIdx.x * 64 + lane];
+  out_scan[blockIdx.x * 64 + lane] = wave_prefix_max(x);
+  out_shift[blockIdx.x * 64 + lane] = wave_shr1(x, -7, lane);
+}
+
+hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
+                                hipStream_t stream) {
+  hipLaunchKernelGGL(wave_scan_selftest_kernel, dim3(n_waves), dim3(64), 0, stream, in, scan, shift);
   return hipGetLastError();
 }
 

@@ -115,7 +115,15 @@ __device__ __forceinline__ void strip_gaps(const PoaScore& P, int lane, int32_t 
   cr.cH = imax(hl, imax(cr.cE, cr.cQ));
 }
 
-// Traceback-code assembly shared by both row paths (branch-free selects).
+// Traceback code of one DP cell (uint16; the strip kernel writes one per
+// evaluated cell, the backtrack below reads nothing else):
+//   bits 0-1  main move: 0 diagonal, 1 up, 2 left, 3 none
+//   bit  2    extend flag of the main move (extend_up / extend_left)
+//   bits 3-7  in-edge index of the main move (diag/up)
+//   bit  8    left-gap run opened here:  H[j-1]+g==E[j] || H[j-1]+q==Q[j]
+//   bit  9    up-gap run stop flag
+//   bits 10-14 in-edge index continuing an up-gap run (31 = none)
+// Assembly from the per-in-edge tests (branch-free selects).
 __device__ __forceinline__ uint32_t assemble_code(uint32_t diag_k, uint32_t up_k, uint32_t up_ext, bool left_ok,
                                                   bool left_ext, bool lbit, uint32_t uc_k, uint32_t uc_stop) {
   const uint32_t left = left_ok ? (2u | (left_ext ? 4u : 0u)) : 3u;

@@ -6,6 +6,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <sched.h>
 #include <thread>
 #include <vector>
 
@@ -49,7 +50,12 @@ unsigned host_threads() {
     const int v = std::atoi(s);
     if (v > 0) return static_cast<unsigned>(v);
   }
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  // the CPUs this process may run on (its affinity mask; svscope_amd/hostcpu.py
+  // pins each rank of a multi-GPU run to its slice and sets SVS_HOST_THREADS)
+  unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) hw = std::max(1, CPU_COUNT(&set));
   return std::min(hw, 16u);
 }
 }  // namespace
@@ -255,7 +261,8 @@ int svs_em_cluster_batch(svs_context* ctx, int32_t n_windows, const svs_em_windo
 }
 
 static int check_decision_windows(const char* fn, int32_t n_windows, const svs_decision_window* wins,
-                                  const int64_t* seq_byte_start, const char* text, const uint8_t* is_tlabel) {
+                                  const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
+                                  const uint8_t* is_tlabel) {
   if (n_windows < 0 || (n_windows > 0 && (!wins || !seq_byte_start)))
     return fail(SVS_E_INVALID, std::string(fn) + ": invalid argument");
   for (int32_t w = 0; w < n_windows; ++w) {
@@ -263,6 +270,14 @@ static int check_decision_windows(const char* fn, int32_t n_windows, const svs_d
     if (W.n_seqs < 1 || W.n_ids < 0 || W.seq_start < 0 || W.flank5_len < 0 || W.flank3_len < 0 || W.tag_off < 0 ||
         ((W.flank5_len || W.flank3_len) && !text) || (W.n_ids && !is_tlabel))
       return fail(SVS_E_INVALID, std::string(fn) + ": window " + std::to_string(w) + " is malformed");
+    // every sequence's byte range, checked here on the caller's thread: a bad
+    // batch fails its own submit, never the session's worker
+    for (int32_t k = 0; k < W.n_seqs; ++k) {
+      const int64_t x = seq_byte_start[W.seq_start + k], y = seq_byte_start[W.seq_start + k + 1];
+      if (x < 0 || y < x || (y > x && !seq_bytes))
+        return fail(SVS_E_INVALID, std::string(fn) + ": window " + std::to_string(w) +
+                                       ": seq_byte_start not monotone");
+    }
   }
   return SVS_OK;
 }
@@ -278,7 +293,8 @@ int svs_decision_batch(svs_context* ctx, int32_t n_windows, const svs_decision_w
                        const uint8_t* is_tlabel, const svs_decision_config* cfg, svs_decision_result** out) {
   if (!ctx || !cfg || !out) return fail(SVS_E_INVALID, "svs_decision_batch: invalid argument");
   *out = nullptr;
-  if (int rc = check_decision_windows("svs_decision_batch", n_windows, wins, seq_byte_start, text, is_tlabel)) return rc;
+  if (int rc = check_decision_windows("svs_decision_batch", n_windows, wins, seq_byte_start, seq_bytes, text,
+                                      is_tlabel)) return rc;
   if (int rc = check_decision_config("svs_decision_batch", cfg)) return rc;
   svs_decision_result* res = nullptr;
   const int rc = guarded([&] {
@@ -307,8 +323,8 @@ int svs_decision_session_submit(svs_decision_session* s, int32_t n_windows, cons
                                 const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
                                 const uint8_t* is_tlabel, int64_t* ticket) {
   if (!s || !ticket) return fail(SVS_E_INVALID, "svs_decision_session_submit: invalid argument");
-  if (int rc = check_decision_windows("svs_decision_session_submit", n_windows, wins, seq_byte_start, text,
-                                      is_tlabel))
+  if (int rc = check_decision_windows("svs_decision_session_submit", n_windows, wins, seq_byte_start, seq_bytes,
+                                      text, is_tlabel))
     return rc;
   return guarded([&] {
     *ticket = svs::submit_decision_batch(s, n_windows, wins, seq_byte_start, seq_bytes, text, is_tlabel);

@@ -113,7 +113,7 @@ struct PoaArena {
   bool own = false;                   // stream is this group's, copies ride on it too
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr, h2d = nullptr;
   hipEvent_t evp = nullptr, evp1 = nullptr;  // around the launch's poa_strip_prep_kernel
-  hipStream_t prep_stream = nullptr;          // SVS_POA_PREP_STREAM=1: that kernel's own stream
+  hipStream_t prep_stream = nullptr;          // SVS_POA_PREP_STREAM=1: that kernel's own stream (made on first use)
   // Staging of the next launch's strip tables in h_in: the fold exports each
   // job's tables straight into a block claimed with an atomic bump (st_cur), so
   // packing the launch copies nothing.  A new generation (st_gen) starts when
@@ -138,7 +138,6 @@ struct PoaArena {
     SVS_HIP(hipEventCreate(&ev1));
     SVS_HIP(hipEventCreate(&evp));
     SVS_HIP(hipEventCreate(&evp1));
-    SVS_HIP(hipStreamCreateWithFlags(&prep_stream, hipStreamNonBlocking));
     SVS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
     SVS_HIP(hipEventCreateWithFlags(&h2d, hipEventDisableTiming));
   }

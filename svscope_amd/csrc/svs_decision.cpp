@@ -25,6 +25,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -94,6 +95,7 @@ struct svs_decision_session {
   std::deque<std::unique_ptr<svs::Batch>> inbox;               // submitted, not yet queued
   std::map<int64_t, std::unique_ptr<svs::Batch>> in_flight;    // queued in the scheduler
   std::map<int64_t, std::unique_ptr<svs::Batch>> finished;     // complete, not yet waited for
+  std::set<int64_t> waited;                                    // tickets already returned by wait
   int64_t next_ticket = 1;
   bool closing = false;
   bool em_signal = false;  // the EM worker finished a launch
@@ -178,7 +180,7 @@ class Pipeline {
       t.tag = new_ref(TaskRef{&b, w, -1});
       for (int32_t k = 0; k < W.n_seqs; ++k) {
         const int64_t x = b.seq_byte_start[W.seq_start + k], y = b.seq_byte_start[W.seq_start + k + 1];
-        if (y < x || x < 0) throw SvsError(SVS_E_INVALID, "seq_byte_start not monotone");
+        // (ranges checked on submit, check_decision_windows)
         t.seqs.emplace_back(y > x ? b.seq_bytes + x : "", static_cast<size_t>(y - x));
         if (k > 0) b.read_lens[w].push_back(static_cast<int32_t>(y - x));
       }
@@ -239,6 +241,9 @@ class Pipeline {
       const WindowFeatures& f = e->windows[i].b->feats[e->windows[i].w];
       ew[i] = svs_em_window{f.rows, f.n_feat, xoff, 0};
       xoff += static_cast<int64_t>(f.rows) * f.n_feat;
+      // §8(d): sum over K = 1 .. kmax-1 of 41 x 2 N (5 nf) K
+      const double kk = std::max(0, std::min(ecfg.max_c + 1, f.rows) - 1);
+      st.em_flops += 410.0 * f.rows * f.n_feat * kk * (kk + 1) / 2;
     }
     std::vector<uint8_t> X(static_cast<size_t>(std::max<int64_t>(1, xoff)));
     for (size_t i = 0; i < e->windows.size(); ++i) {
@@ -483,6 +488,9 @@ int64_t submit_decision_batch(svs_decision_session* s, int32_t n, const svs_deci
 svs_decision_result* wait_decision_batch(svs_decision_session* s, int64_t ticket) {
   std::unique_lock<std::mutex> lk(s->mu);
   if (ticket <= 0 || ticket >= s->next_ticket) throw SvsError(SVS_E_INVALID, "unknown decision ticket");
+  // a ticket is returned once; waiting for it again would never wake
+  if (s->waited.count(ticket)) throw SvsError(SVS_E_INVALID, "decision ticket already waited for");
+  s->waited.insert(ticket);
   s->cv_done.wait(lk, [&] { return s->error || s->finished.count(ticket) != 0; });
   auto it = s->finished.find(ticket);
   if (it == s->finished.end()) std::rethrow_exception(s->error);

@@ -45,8 +45,6 @@ struct PoaLaunch {
   const PoaJob* jobs;
   int n_jobs;
   PoaScore score;
-  const uint32_t* row_info;
-  const uint32_t* row_slot;
   const uint32_t* row_pstart;
   const uint32_t* pred_row;
   const uint32_t* pred_slot;
@@ -57,33 +55,24 @@ struct PoaLaunch {
   int32_t* aln;
   int32_t* aln_len;    // per job: path length; strip kernel also [n_jobs + job] best
                        // sink score and [2 n_jobs + job] strip rows computed
-  int waves_per_job;  // 1, 2 or 4 (column-chunk waves per job)
-  // strip-major kernel
+  int waves_per_job;     // strip-pipeline waves per job: 1, 2, 4, 8 (16 with the pool in LDS)
   const uint32_t* rec;   // row records (export_strip_rows)
   int32_t* bnd;          // strip-boundary carries
   uint32_t lds_slots;    // pool slots per wave held in LDS (max n_slots of the launch)
   bool prune;            // some job has a pruning bound: the pruning kernel variant
-  bool wide;             // 128-column strips after strip 0 (PoaJob::ls from strip_ls_wide)
 };
 
-// Row stride of a strip job with wide strips: 64 + a multiple of 128, >= len + 1.
-inline uint32_t strip_ls_wide(uint32_t len) {
-  return len + 1 <= 64 ? 64u : 64u + (len + 1 - 64 + 127) / 128 * 128;
-}
+// Row stride of a strip job: len + 1 rounded up to whole 64-column strips.
+inline uint32_t strip_ls(uint32_t len) { return (len + 1 + 63) / 64 * 64; }
 
 // Strip-major kernel: LDS bytes per pool slot (65 int32 H incl. the boundary
 // column + 64 packed uint16 F/O distances), and the largest pool kept in LDS.
 constexpr uint32_t kStripSlotBytes = 65 * 4 + 64 * 2;
-// the same for wide strips (128 columns, two per lane)
-constexpr uint32_t kStripSlotBytesWide = 130 * 4 + 128 * 2;
 constexpr uint32_t kStripMaxLdsSlots = 80;
 // LDS a strip workgroup's pools may take (160 KiB per CU on gfx950, less the
 // kernel's own few static words)
 constexpr uint64_t kStripLdsBytes = 160 * 1024 - 256;
 
-constexpr uint32_t kPoaMaxSlotsMultiWave = 64;
-
-hipError_t launch_poa_nw_convex(const PoaLaunch& a, hipStream_t stream);
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream);
 // Device half of the strip row export (poa_prep.hip) for the jobs with
 // PoaJob::prep bit 0; every offset of those jobs indexes `base`.
@@ -92,7 +81,6 @@ constexpr uint32_t kStripPrepMaxSlots = 64;    // pool slots of a prep job (free
 size_t strip_prep_scratch_words(uint32_t n_rows);  // after the job's in-edge slots (rounded to 4)
 hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore& score, uint8_t* base,
                                  uint32_t max_rows, hipStream_t stream);
-int choose_strip_wpj(int device, size_t n_jobs, uint32_t lds_slots, uint32_t min_strips);
 hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
                                 hipStream_t stream);
 

@@ -37,39 +37,13 @@ void check_poa_config(const svs_poa_config& c) {
                                       "always calls poa(seqs, 1)");
   const bool convex = c.g < c.e && !(c.g <= c.q || c.e >= c.c);
   if (!convex) throw SvsError(SVS_E_UNSUPPORTED, "only spoa's convex gap subtype (g<e, g>q, e<c) is implemented");
-  // exactness conditions of the two-scan formulation (see poa_kernels.hip)
+  // exactness conditions of the two-scan formulation (see poa_wave.hpp strip_gaps)
   if (!(c.g <= c.e && c.q <= c.c && c.g <= c.c && c.e <= c.c && c.g + c.q <= 2 * c.c))
     throw SvsError(SVS_E_UNSUPPORTED, "gap parameters outside the exact scan formulation");
   // the strip kernel stores F and O as 8-bit distances to H clamped at e-g+1, c-q+1
   if (c.e - c.g + 1 > 255 || c.c - c.q + 1 > 255)
     throw SvsError(SVS_E_UNSUPPORTED, "gap parameters too far apart for the packed F/O pool");
 }
-
-namespace {
-
-// Waves per job: enough column-chunk waves to put ~4 waves on each SIMD
-// (1024 SIMDs on MI355X), only for jobs wide enough to split (>= 8 strips per
-// wave) and pools small enough for the LDS boundary table.
-int choose_waves_per_job(const std::vector<PoaJob>& jobs, size_t nj) {
-  if (const char* e = std::getenv("SVS_POA_WPJ")) {
-    const int w = std::atoi(e);
-    if (w == 1 || w == 2 || w == 4) {
-      for (size_t k = 0; k < nj; ++k)
-        if (w > 1 && jobs[k].n_slots > kPoaMaxSlotsMultiWave) return 1;
-      return w;
-    }
-  }
-  uint32_t min_strips = 0xFFFFFFFFu;
-  for (size_t k = 0; k < nj; ++k) {
-    if (jobs[k].n_slots > kPoaMaxSlotsMultiWave) return 1;
-    min_strips = std::min(min_strips, jobs[k].ls / 64);
-  }
-  int w = 1;
-  while (w < 4 && static_cast<size_t>(w) * nj < 4096 && min_strips >= static_cast<uint32_t>(16 * w)) w *= 2;
-  return w;
-}
-
-}  // namespace
 
 namespace {
 
@@ -127,13 +101,6 @@ struct PoaTrace {
 };
 PoaTrace g_trace;
 
-// Kernel selection: the strip-major kernel (poa_strip.hip) unless
-// SVS_POA_KERNEL=rows asks for the row-major one (poa_kernels.hip).
-bool use_strip_kernel() {
-  const char* e = std::getenv("SVS_POA_KERNEL");
-  return !(e && std::string(e) == "rows");
-}
-
 // SVS_POA_STRIP_GLOBAL_POOL=1 keeps the strip kernel's pool in global memory
 // even when it fits LDS (tests the path large graphs take).
 bool strip_pool_forced_global() {
@@ -187,27 +154,21 @@ int32_t prune_bound(const PoaTask& t, const PoaScore& P, uint32_t n_rows, uint32
   }
   if (cg > 0 || P.m < P.n || P.m < 0) return kNoPrune;
   const double lb = std::floor(t.rate * len - slack * P.m * len);
-  if (lb < -1e9 || lb > 1e9) return kNoPrune;
+  // real bounds stay far above kPruneAll, so that the strip kernel's lanes
+  // past column L (ub term VNEG/2) can never reach one (poa_strip.hip)
+  if (lb < -1e8 || lb > 1e9) return kNoPrune;
   return static_cast<int32_t>(lb);
 }
 
 // Kernel selection flags read from the environment once per call site
 // (not once per job: getenv scans the whole environment).
 struct KernelEnv {
-  bool strip = use_strip_kernel();
   bool global_pool = strip_pool_forced_global();
 };
 
 // Strip tables go straight into the group's pinned staging buffer
 // (PoaArena::st_*) unless SVS_POA_STAGING=vec keeps them in each task's
 // vectors, copied into the buffer when the launch is packed.
-// Strips after the first 128 columns wide, two per lane (poa_strip.hip,
-// sweep_w) with SVS_POA_WIDE=1.
-bool wide_strips() {
-  const char* e = std::getenv("SVS_POA_WIDE");
-  return e && std::string(e) == "1";
-}
-
 bool direct_staging() {
   const char* e = std::getenv("SVS_POA_STAGING");
   return !(e && std::string(e) == "vec");
@@ -236,8 +197,7 @@ void write_read(char* p, const std::string& s, uint32_t ls) {
 // buffer; false (nothing written) when the buffer is full.
 bool export_direct(PoaTask& t, const int32_t* gaps, PoaArena& A) {
   const std::string& s = t.seqs[t.next];
-  // the read's region is sized for either strip width (strip_ls_wide >= the 64-column stride)
-  const uint32_t ls = strip_ls_wide(static_cast<uint32_t>(s.size()));
+  const uint32_t ls = strip_ls(static_cast<uint32_t>(s.size()));
   const uint32_t V = t.graph.num_nodes(), E = t.graph.num_edges();
   if (device_prep() && V <= kStripPrepMaxRows && gaps[1] <= 0 && gaps[3] <= 0) {
     // host pass 1 only; the device derives the rest (poa_prep.hip)
@@ -274,15 +234,12 @@ bool export_direct(PoaTask& t, const int32_t* gaps, PoaArena& A) {
 }
 
 uint64_t job_bytes(const RowTables& tt, uint64_t L, const KernelEnv& ke) {
-  const uint64_t ls = strip_ls_wide(static_cast<uint32_t>(L)), V = tt.n_rows;
-  if (ke.strip) {
-    // traceback codes + two strip-boundary carry buffers (+ a global pool when
-    // the graph needs more slots than the LDS pool holds)
-    const uint64_t pool = (tt.n_slots > kStripMaxLdsSlots || ke.global_pool)
-                              ? 8ull * round_up(static_cast<uint64_t>(tt.n_slots) * 97, 64) * 4 : 0;
-    return V * ls * 2 + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
-  }
-  return V * ls * 2 + static_cast<uint64_t>(tt.n_slots) * 3 * ls * 4 + (V + L + 1) * 8;
+  const uint64_t ls = strip_ls(static_cast<uint32_t>(L)), V = tt.n_rows;
+  // traceback codes + two strip-boundary carry buffers (+ a global pool when
+  // the graph needs more slots than the LDS pool holds)
+  const uint64_t pool = (tt.n_slots > kStripMaxLdsSlots || ke.global_pool)
+                            ? 8ull * round_up(static_cast<uint64_t>(tt.n_slots) * 97, 64) * 4 : 0;
+  return V * ls * 2 + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
 }
 
 void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks);
@@ -309,25 +266,20 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   });
   for (size_t k = 0; k < nj; ++k) max_slots = std::max(max_slots, tasks[la.ids[k]].rows.n_slots);
   const bool lds_pool = max_slots <= kStripMaxLdsSlots && !strip_pool_forced_global();
-  const bool wide = lds_pool && wide_strips();
-  const uint64_t slot_bytes = wide ? kStripSlotBytesWide : kStripSlotBytes;
-  auto job_ls = [&](size_t len) -> uint32_t {
-    return wide ? strip_ls_wide(static_cast<uint32_t>(len)) : static_cast<uint32_t>(round_up(len + 1, 64));
-  };
+  const uint64_t slot_bytes = kStripSlotBytes;
+  auto job_ls = [&](size_t len) -> uint32_t { return strip_ls(static_cast<uint32_t>(len)); };
   // waves per job: enough strip-pipeline waves to fill the CUs, only for reads
   // wide enough to give every wave several strips; SVS_POA_WPJ overrides
   uint32_t min_strips = 0xFFFFFFFFu;
   for (size_t k = 0; k < nj; ++k) {
     const uint32_t ls = job_ls(tasks[la.ids[k]].seqs[tasks[la.ids[k]].next].size());
-    min_strips = std::min(min_strips, wide ? 1 + (ls - 64) / 128 : ls / 64);
+    min_strips = std::min(min_strips, ls / 64);
   }
   int wpj = 1;
   const char* we = std::getenv("SVS_POA_WPJ");
   const int wenv = we ? std::atoi(we) : 0;
-  if ((wenv >= 1 && wenv <= 8) || (wenv == 16 && lds_pool)) {
-    wpj = (lds_pool || (wenv & (wenv - 1)) == 0) ? wenv : 1;
-  } else if (std::getenv("SVS_POA_WPJ_RESIDENT")) {
-    wpj = choose_strip_wpj(ctx->device, nj, lds_pool ? max_slots : 0, min_strips);
+  if ((wenv == 1 || wenv == 2 || wenv == 4 || wenv == 8) || (wenv == 16 && lds_pool)) {
+    wpj = wenv;
   } else {
     // ~6 waves per SIMD (1024 SIMDs); each wave keeps >= 6 strips.  Measured
     // faster than keeping every workgroup resident (r01_v16): more waves per
@@ -335,14 +287,12 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     while (wpj < 8 && static_cast<size_t>(wpj) * nj < 6144 && min_strips >= static_cast<uint32_t>(6 * wpj)) wpj *= 2;
     // the small launches at the end of a batch: 16 waves per job (>= 2 strips
     // each), or the few remaining jobs leave most SIMDs idle
-    if (lds_pool && wpj == 8 && nj < 512 && min_strips >= (wide ? 16u : 32u)) wpj = 16;
+    if (lds_pool && wpj == 8 && nj < 512 && min_strips >= 32u) wpj = 16;
   }
-  if (wide)
-    while (wpj & (wpj - 1)) wpj &= wpj - 1;  // the wide kernel comes in 1, 2, 4, 8, 16 waves per job
   // the per-wave LDS pools of one workgroup must fit the CU's LDS
   while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * slot_bytes > kStripLdsBytes) wpj /= 2;
   if (std::getenv("SVS_POA_DEBUG"))
-    std::fprintf(stderr, "[svs] strip launch: %zu jobs, wpj %d, slots %u, wide %d\n", nj, wpj, max_slots, wide ? 1 : 0);
+    std::fprintf(stderr, "[svs] strip launch: %zu jobs, wpj %d, slots %u\n", nj, wpj, max_slots);
   const PruneEnv penv;
   for (size_t k = 0; k < nj; ++k) {
     const auto& tt = tasks[la.ids[k]].rows;
@@ -385,7 +335,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   size_t end = start;
   for (size_t k = 0; k < nj; ++k) {
     const PoaTask& t = tasks[la.ids[k]];
-    const uint32_t lsw = strip_ls_wide(la.jobs[k].len);
+    const uint32_t lsw = strip_ls(la.jobs[k].len);
     lay[k] = (t.rows_at == 2 && t.rows.lite) ? strip_block_lite(t.rows.n_rows, t.rows.n_edges, lsw)
                                               : strip_block_layout(t.rows.n_rows, t.rows.n_edges, lsw);
     if (t.rows_at == 2) {
@@ -446,7 +396,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
       std::memcpy(base + lay[k].pred_row, tt.pred_row.data(), 4 * tt.pred_row.size());
       std::memcpy(base + lay[k].pred_slot, tt.pred_slot.data(), 4 * tt.pred_slot.size());
     }
-    write_read(base + lay[k].seq, t.seqs[t.next], strip_ls_wide(J.len));
+    write_read(base + lay[k].seq, t.seqs[t.next], strip_ls(J.len));
   });
   host_ms += ms_since(th0);
 
@@ -470,6 +420,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
       const char* e = std::getenv("SVS_POA_PREP_STREAM");
       return e && std::string(e) == "1";
     }();
+    if (own && !A.prep_stream) SVS_HIP(hipStreamCreateWithFlags(&A.prep_stream, hipStreamNonBlocking));
     hipStream_t ps = own ? A.prep_stream : A.stream;
     if (own) SVS_HIP(hipStreamWaitEvent(ps, A.h2d, 0));
     SVS_HIP(hipEventRecord(A.evp, ps));
@@ -501,7 +452,6 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.aln_len = A.d_alen.as<int32_t>();
   pl.lds_slots = lds_pool ? max_slots : 0;
   pl.prune = any_prune;
-  pl.wide = wide;
   pl.waves_per_job = wpj;
   la.wpj = wpj;
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
@@ -519,124 +469,6 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   st.d2h_bytes += n_aln * 8 + nj * 12;
 }
 
-// Packs the launch's tables into the arena's pinned buffer and enqueues
-// H2D copy, kernel and D2H copies on the arena's stream (no host wait).
-void pack_and_launch(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, const PoaScore& score,
-                     svs_poa_stats& st, double& host_ms) {
-  if (use_strip_kernel()) {
-    pack_and_launch_strip(ctx, la, tasks, score, st, host_ms);
-    return;
-  }
-  auto th0 = Clock::now();
-  const size_t nj = la.ids.size();
-  la.jobs.assign(nj, PoaJob{});
-  uint64_t n_rows = 0, n_pstart = 0, n_pred = 0, n_seq = 0, n_tb = 0, n_pool = 0, n_aln = 0;
-  uint32_t max_preds = 0;
-  for (size_t k = 0; k < nj; ++k) {
-    const auto& tt = tasks[la.ids[k]].rows;
-    const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];
-    PoaJob& J = la.jobs[k];
-    J.n_rows = static_cast<uint32_t>(tt.info.size());
-    J.len = static_cast<uint32_t>(s.size());
-    J.ls = static_cast<uint32_t>(round_up(J.len + 1, 64));
-    J.n_slots = tt.n_slots;
-    J.row_off = static_cast<uint32_t>(n_rows);
-    J.pstart_off = static_cast<uint32_t>(n_pstart);
-    J.pred_off = static_cast<uint32_t>(n_pred);
-    J.pslot_off = J.pred_off;
-    J.seq_off = static_cast<uint32_t>(n_seq + 1);  // one zero pad byte precedes each read
-    J.tb_off = n_tb;
-    J.pool_off = n_pool;
-    J.aln_off = n_aln;
-    n_rows += J.n_rows;
-    n_pstart += J.n_rows + 1;
-    n_pred += tt.pred_row.size();
-    n_seq += J.ls + 64;  // pad byte + read + tail pad
-    n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
-    n_pool += static_cast<uint64_t>(J.n_slots) * 3 * J.ls;
-    n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
-    max_preds = std::max(max_preds, tt.max_preds);
-    st.dp_cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);
-  }
-  if (max_preds > 31)
-    throw SvsError(SVS_E_UNSUPPORTED, "a graph node has more than 31 in-edges (traceback code limit)");
-  if (n_rows > 0xFFFFFFFFull || n_pred > 0xFFFFFFFFull || n_seq > 0xFFFFFFFFull)
-    throw SvsError(SVS_E_UNSUPPORTED, "batch too large for 32-bit table offsets");
-  la.n_aln = n_aln;
-  size_t off = 0;
-  auto sec = [&](size_t bytes) {
-    const size_t o = off;
-    off = round_up(off + bytes, 256);
-    return o;
-  };
-  const size_t s_jobs = sec(nj * sizeof(PoaJob));
-  const size_t s_info = sec(n_rows * 4), s_slot = sec(n_rows * 4), s_ps = sec(n_pstart * 4);
-  const size_t s_col0 = sec(n_rows * 12);
-  const size_t s_prow = sec(n_pred * 4), s_pslot = sec(n_pred * 4), s_seq = sec(n_seq + 256);
-  PoaArena& A = *la.arena;
-  A.h_in.ensure(off);
-  char* hs = A.h_in.as<char>();
-  std::memcpy(hs + s_jobs, la.jobs.data(), nj * sizeof(PoaJob));
-  ctx->pool->parallel_for(nj, [&](size_t k) {
-    const auto& tt = tasks[la.ids[k]].rows;
-    const PoaJob& J = la.jobs[k];
-    std::memcpy(hs + s_info + 4ull * J.row_off, tt.info.data(), 4ull * J.n_rows);
-    std::memcpy(hs + s_slot + 4ull * J.row_off, tt.slot.data(), 4ull * J.n_rows);
-    std::memcpy(hs + s_ps + 4ull * J.pstart_off, tt.pstart.data(), 4ull * (J.n_rows + 1));
-    std::memcpy(hs + s_col0 + 12ull * J.row_off, tt.col0.data(), 12ull * J.n_rows);
-    if (!tt.pred_row.empty()) {
-      std::memcpy(hs + s_prow + 4ull * J.pred_off, tt.pred_row.data(), 4 * tt.pred_row.size());
-      std::memcpy(hs + s_pslot + 4ull * J.pred_off, tt.pred_slot.data(), 4 * tt.pred_slot.size());
-    }
-    const std::string& s = tasks[la.ids[k]].seqs[tasks[la.ids[k]].next];
-    std::memset(hs + s_seq + J.seq_off - 1, 0, J.ls + 64);
-    std::memcpy(hs + s_seq + J.seq_off, s.data(), s.size());
-  });
-  host_ms += ms_since(th0);
-
-  A.d_in.ensure(off);
-  A.d_tb.ensure(n_tb * 2 + 4096);
-  A.d_pool.ensure(n_pool * 4 + 4096);
-  A.d_aln.ensure(n_aln * 8);
-  A.d_alen.ensure(nj * 4);
-  A.h_aln.ensure(n_aln * 8);
-  A.h_alen.ensure(nj * 4);
-  char* dg = A.d_in.as<char>();
-  SVS_HIP(hipMemcpyAsync(dg, hs, off, hipMemcpyHostToDevice, A.copy_stream));
-  SVS_HIP(hipEventRecord(A.h2d, A.copy_stream));
-  SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
-  PoaLaunch pl;
-  pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
-  pl.n_jobs = static_cast<int>(nj);
-  pl.score = score;
-  pl.row_info = reinterpret_cast<const uint32_t*>(dg + s_info);
-  pl.row_slot = reinterpret_cast<const uint32_t*>(dg + s_slot);
-  pl.row_pstart = reinterpret_cast<const uint32_t*>(dg + s_ps);
-  pl.pred_row = reinterpret_cast<const uint32_t*>(dg + s_prow);
-  pl.pred_slot = reinterpret_cast<const uint32_t*>(dg + s_pslot);
-  pl.col0 = reinterpret_cast<const int32_t*>(dg + s_col0);
-  pl.seqs = reinterpret_cast<const uint8_t*>(dg + s_seq);
-  pl.tb = A.d_tb.as<uint16_t>();
-  pl.pool = A.d_pool.as<int32_t>();
-  pl.aln = A.d_aln.as<int32_t>();
-  pl.aln_len = A.d_alen.as<int32_t>();
-  pl.waves_per_job = choose_waves_per_job(la.jobs, nj);
-  SVS_HIP(hipEventRecord(A.ev0, A.stream));
-  SVS_HIP(launch_poa_nw_convex(pl, A.stream));
-  SVS_HIP(hipEventRecord(A.ev1, A.stream));
-  SVS_HIP(hipStreamWaitEvent(A.copy_stream, A.ev1, 0));
-  SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 4, hipMemcpyDeviceToHost, A.copy_stream));
-  SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, pl.aln, n_aln * 8, hipMemcpyDeviceToHost, A.copy_stream));
-  SVS_HIP(hipEventRecord(A.done, A.copy_stream));
-  st.launches += 1;
-  st.alignments += nj;
-  st.cells_computed += n_tb;  // the row-major kernel evaluates every cell
-  st.tb_bytes += n_tb * 2;
-  st.pool_bytes += n_pool * 4;
-  st.h2d_bytes += off;
-  st.d2h_bytes += n_aln * 8 + nj * 4;
-}
-
 // Readies a task's next step: sequences landing on an empty graph become a
 // fresh chain (no DP), empty ones are skipped; then either the row tables of
 // the next alignment are exported (returns 1) or, with every sequence in, the
@@ -649,15 +481,9 @@ uint8_t prep_task(PoaTask& t, const svs_poa_config& cfg, PoaArena* stage) {
     break;
   }
   if (t.next < t.seqs.size()) {
-    if (use_strip_kernel()) {
-      const int32_t gaps[4] = {cfg.g, cfg.e, cfg.q, cfg.c};
-      if (!stage || !export_direct(t, gaps, *stage)) {
-        t.graph.export_strip_rows(&t.rows, gaps);
-        t.rows_at = 1;
-      }
-    } else {
-      t.graph.export_rows(&t.rows);
-      fill_col0(&t.rows, cfg.g, cfg.e, cfg.q, cfg.c);
+    const int32_t gaps[4] = {cfg.g, cfg.e, cfg.q, cfg.c};
+    if (!stage || !export_direct(t, gaps, *stage)) {
+      t.graph.export_strip_rows(&t.rows, gaps);
       t.rows_at = 1;
     }
     return 1;
@@ -710,7 +536,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   st.gpu_wait_ms += ms_since(tw0);
   // the launch's staging copy is consumed: a new generation for the next one
   PoaArena* stage = nullptr;
-  if (use_strip_kernel() && direct_staging()) {
+  if (direct_staging()) {
     A.st_gen += 1;
     A.st_cur.store(0, std::memory_order_relaxed);
     A.h_in.ensure(A.st_peak + A.st_peak / 4);
@@ -735,8 +561,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   const int32_t* alen = A.h_alen.as<int32_t>();
   const int32_t* aout = A.h_aln.as<int32_t>();
   const size_t nj = la.ids.size();
-  const bool strip = use_strip_kernel();
-  if (strip) {
+  {
     for (size_t k = 0; k < nj; ++k) {
       st.cells_computed += 64ull * static_cast<uint32_t>(alen[2 * nj + k]);
       tasks[la.ids[k]].last_rows = static_cast<uint32_t>(alen[2 * nj + k]);
@@ -746,7 +571,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   ctx->pool->parallel_for(nj, [&](size_t k) {
     const int32_t n = alen[k];
     auto& t = tasks[la.ids[k]];
-    if (strip && n == kPruneRetry) {
+    if (n == kPruneRetry) {
       // the bound was above the optimum: the same sequence again, unpruned
       // (its row tables are still those of this step)
       t.retry = true;
@@ -756,7 +581,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
       return;
     }
     if (n < 0) throw SvsError(SVS_E_INTERNAL, "GPU traceback reported an inconsistent path");
-    if (strip) {
+    {
       const uint32_t len = la.jobs[k].len;
       if (!t.retry && len > 0) {
         t.rate = static_cast<double>(alen[nj + k]) / len;
@@ -860,7 +685,7 @@ struct PoaScheduler::Impl {
       if (g.active.empty()) return;
       auto th0 = Clock::now();
       needs.assign(g.active.size(), 0);
-      PoaArena* stage = use_strip_kernel() && direct_staging() ? g.arena : nullptr;
+      PoaArena* stage = direct_staging() ? g.arena : nullptr;
       // sequences landing on an empty graph become a fresh chain (no DP)
       ctx->pool->parallel_for(g.active.size(), [&](size_t i) {
         PoaTask& t = tasks[g.active[i]];
@@ -891,7 +716,7 @@ struct PoaScheduler::Impl {
         g.la.arena = g.arena;
         g.la.gid = gid(g);
         const auto tp0 = Clock::now();
-        pack_and_launch(ctx, g.la, tasks, score, st, host_ms);
+        pack_and_launch_strip(ctx, g.la, tasks, score, st, host_ms);
         g_trace.host("pack", gid(g), tp0, g.la.ids.size());
         g.pending = true;
         return;
@@ -911,7 +736,7 @@ struct PoaScheduler::Impl {
         sub.ids.assign(ids.begin() + first, ids.begin() + last);
         sub.arena = g.arena;
         sub.gid = gid(g);
-        pack_and_launch(ctx, sub, tasks, score, st, host_ms);
+        pack_and_launch_strip(ctx, sub, tasks, score, st, host_ms);
         finish(ctx, sub, tasks, st, host_ms, cfg);
         first = last;
       }
@@ -930,7 +755,7 @@ struct PoaScheduler::Impl {
       const char* e = std::getenv("SVS_POA_JOB_ORDER");
       return !(e && std::string(e) == "0");
     }();
-    if (!on || !use_strip_kernel()) return;
+    if (!on) return;
     std::vector<std::pair<uint64_t, uint32_t>> c(ids.size());
     for (size_t i = 0; i < ids.size(); ++i) {
       const PoaTask& t = tasks[ids[i]];

@@ -97,8 +97,14 @@ def FetchTDsubSeq(refFile, bamFileList, LabelList, TDRecord, offset=200, readers
             continue
         # min 5' start, max 3' end per read, the primary's sequence (:111-118),
         # in sorted read-name order (np.intersect1d order, kept by the concat)
+        # SeqDf.loc[spanReadIDs] then the axis-1 concat: a primary name seen
+        # twice fails only when it is one of the span names (pandas'
+        # InvalidIndexError); duplicates among the other primaries are ignored
+        span_set = set(span)
         by_name = {}
         for name, seq, mq in primary:
+            if name not in span_set:
+                continue
             if name in by_name:
                 raise ValueError("Reindexing only valid with uniquely valued Index objects")
             by_name[name] = (seq, mq)

@@ -199,6 +199,9 @@ def _dist_setup():
     rank = int(os.environ.get("RANK", "0"))
     if world <= 1:
         return world, rank, None, None
+    # this rank's CPU slice and pool size, before its context exists
+    from svscope_amd import hostcpu
+    hostcpu.apply()
     import torch
     import torch.distributed as dist
     local = int(os.environ.get("LOCAL_RANK", "0"))

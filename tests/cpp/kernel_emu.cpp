@@ -1,4 +1,5 @@
-// TEST INFRASTRUCTURE: scalar CPU emulation of svscope_amd/csrc/poa_kernels.hip
+// TEST INFRASTRUCTURE: scalar CPU emulation of the strip kernel (svscope_amd/csrc/poa_strip.hip) and of
+// a row-major sweep over the host planner's export_rows tables
 // (lanes become a loop) driven by the product's host graph engine
 // (poa_graph.cpp).  Lets the CPU test suite check the kernel's two-scan
 // recurrence, traceback codes and code-driven traceback against the oracle

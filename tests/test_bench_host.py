@@ -95,3 +95,25 @@ def test_local_graph_merges_stale_rank_journals(tmp_path, monkeypatch):
     assert len(seen) == 2
     assert not any(x.startswith(path.name + ".part") for x in os.listdir(tmp_path))
     assert open(path).read().splitlines() == _expected(rows)
+
+
+def test_rank_cpu_plan_splits_the_job_share():
+    """Eight ranks on one node (WORLD_SIZE=8): each gets a disjoint contiguous
+    slice of the job's CPUs and share // 8 (>= 2) engine pool threads, so the
+    ranks together stay within the job's CPU share."""
+    from svscope_amd import hostcpu
+    cpus = list(range(256))
+    slices = [hostcpu.rank_cpu_plan(r, 8, cpus=cpus, share=16) for r in range(8)]
+    assert {t for _, t in slices} == {2}
+    assert sorted(c for s, _ in slices for c in s) == cpus
+    assert all(s == list(range(32 * r, 32 * r + 32)) for r, (s, _) in enumerate(slices))
+    assert hostcpu.rank_cpu_plan(0, 1, cpus=cpus, share=16) == (cpus, 16)
+    assert hostcpu.rank_cpu_plan(1, 2, cpus=cpus, share=128)[1] == 16  # capped at 16
+    # apply() in a fresh process: the rank's env, pinned, SVS_HOST_THREADS exported
+    code = ("import os; from svscope_amd import hostcpu; n = hostcpu.apply(); "
+            "print(n, os.environ['SVS_HOST_THREADS'], len(os.sched_getaffinity(0)))")
+    env = dict(os.environ, LOCAL_RANK="3", LOCAL_WORLD_SIZE="8", WORLD_SIZE="8", OMP_NUM_THREADS="16")
+    env.pop("SVS_HOST_THREADS", None)
+    out = subprocess.check_output([sys.executable, "-c", code], env=env, cwd=ROOT, timeout=120).decode().split()
+    n_aff = len(os.sched_getaffinity(0))
+    assert out[:2] == ["2", "2"] and int(out[2]) == max(1, n_aff // 8)

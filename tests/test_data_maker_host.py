@@ -124,3 +124,45 @@ def test_local_graph_bam_plumbing_with_oracle_decisions(tmp_path, monkeypatch):
     monkeypatch.setattr(som_td_detector, "DecisionBatch", lambda *a, **k: pytest.fail("re-ran a finished window"))
     local_graph.localGraph(args, readers=READERS)
     assert open(path).read().splitlines() == exp
+
+
+class _ListReaders:
+    """readers hook over explicit read lists (one per BAM path)."""
+
+    def __init__(self, bams):
+        self.bams = bams
+
+    def alignment(self, path):
+        reads = self.bams[path]
+
+        class _F:
+            def fetch(self, contig, start=None, stop=None):
+                return [r for r in reads if r.reference_start < stop and r.reference_end > start]
+        return _F()
+
+
+def _linear_read(name, start, length, rs, secondary=False):
+    seq = "".join(rs.choice(list("ACGT"), length))
+    pairs = [(i, start + i) for i in range(length)]
+    return fake_bam.FakeRead(name, seq, 60, start, pairs, [(0, length)], secondary=secondary)
+
+
+def test_duplicate_primary_names_fail_only_when_spanning():
+    """DataScanner.py:113-117: SeqDf.loc[spanReadIDs] + the axis-1 concat fail
+    only when a span name has two primary rows; a duplicated primary name that
+    does not span both flanks is ignored."""
+    rs = np.random.RandomState(7)
+    rec = "chrF\t1000\t1100\tX\t0"
+    span = [_linear_read("s%d" % i, 700, 700, rs) for i in range(4)]
+    # a name with two primaries, neither spanning both flanks (F5 = 800..1000, F3 = 1100..1300)
+    dup = [_linear_read("d", 900, 300, rs), _linear_read("d", 1050, 200, rs)]
+    base = dmk.FetchTDsubSeq("ref", ["b0"], ["T1_tumor"], rec, offset=200,
+                             readers=_ListReaders({"b0": span}))
+    got = dmk.FetchTDsubSeq("ref", ["b0"], ["T1_tumor"], rec, offset=200,
+                            readers=_ListReaders({"b0": span + dup}))
+    assert got == base and len(got[0]) == 4
+    # one primary spans F5 only, the other F3 only: "d" is a span name with two
+    # primary rows -> the reference's concat raises
+    a, b = _linear_read("d", 700, 320, rs), _linear_read("d", 1080, 250, rs)
+    with pytest.raises(ValueError):
+        dmk.FetchTDsubSeq("ref", ["b0"], ["T1_tumor"], rec, offset=200, readers=_ListReaders({"b0": span + [a, b]}))

@@ -167,3 +167,34 @@ def test_decision_session_config3_matches_batch_path():
         while q:
             got += s.wait(q.popleft())
     assert [decision_oracle.record_line(g) for g in got] == exp
+
+
+def test_decision_session_bad_batch_is_isolated():
+    """A batch whose seq_byte_start is not monotone fails its own submit on the
+    caller's thread (SVS_E_INVALID); the good batches before and after it still
+    return the reference's records, and waiting twice for a ticket fails
+    instead of hanging."""
+    import ctypes
+    from svscope_amd import _abi
+    from svscope_amd.decision_maker import DecisionSession, _gate, _pack_windows
+    cases = json.load(open(GOLD))
+    wins = [(c["TDRecord"], c["sequenceList"], np.array(c["ReadIDs"]), c["flank_5"], c["flank_3"]) for c in cases]
+    lines = [c["line"] for c in cases]
+    s = DecisionSession()
+    t1 = s.submit(wins[:4])
+    # the same windows, packed, with two sequence starts swapped
+    _, gated = _gate(wins[4:8])
+    wpk, starts, blob, txt, tag_arr = _pack_windows(wins[4:8], gated, "tumor")
+    bad = starts.copy()
+    bad[2], bad[3] = starts[3], starts[2]
+    ticket = ctypes.c_int64()
+    with pytest.raises(_abi.SvsError, match="monotone"):
+        _abi.check(s.lib.svs_decision_session_submit(
+            s.handle, len(gated), wpk, bad.ctypes.data_as(ctypes.c_void_p), blob, txt,
+            tag_arr.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ticket)), "svs_decision_session_submit")
+    t2 = s.submit(wins[4:9])
+    assert ["\t".join(str(x) for x in r) for r in s.wait(t1)] == lines[:4]
+    assert ["\t".join(str(x) for x in r) for r in s.wait(t2)] == lines[4:9]
+    with pytest.raises(_abi.SvsError, match="already waited"):
+        _abi.check(s.lib.svs_decision_session_wait(s.handle, ctypes.c_int64(t2), ctypes_ptr()), "wait")
+    s.close()

@@ -86,15 +86,10 @@ def test_genmsa_false_and_min_coverage():
 
 
 @pytest.mark.parametrize("env", [
-    {"SVS_POA_KERNEL": "rows", "SVS_POA_WPJ": "1"},
-    {"SVS_POA_KERNEL": "rows", "SVS_POA_WPJ": "2"},
-    {"SVS_POA_KERNEL": "rows", "SVS_POA_WPJ": "4"},
     {"SVS_POA_WPJ": "1"},
     {"SVS_POA_WPJ": "2"},
     {"SVS_POA_WPJ": "4"},
     {"SVS_POA_WPJ": "8"},
-    {"SVS_POA_WPJ": "3"},
-    {"SVS_POA_WPJ": "7"},
     {"SVS_POA_WPJ": "16"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "1"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "4"},
@@ -103,35 +98,25 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_PRUNE_SLACK": "0", "SVS_POA_WPJ": "8"},
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_WPJ": "4"},
     {"SVS_POA_PRUNE_SLACK": "0", "SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "2"},
-    {"SVS_POA_WIDE": "1", "SVS_POA_WPJ": "1"},
-    {"SVS_POA_WIDE": "1", "SVS_POA_WPJ": "2"},
-    {"SVS_POA_WIDE": "1", "SVS_POA_WPJ": "4"},
-    {"SVS_POA_WIDE": "1", "SVS_POA_WPJ": "16"},
-    {"SVS_POA_WIDE": "1", "SVS_POA_PRUNE": "0"},
-    {"SVS_POA_WIDE": "1", "SVS_POA_PRUNE_SLACK": "0", "SVS_POA_WPJ": "8"},
-    {"SVS_POA_WIDE": "1", "SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_WPJ": "4"},
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "none"},
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "-0.3", "SVS_POA_PRUNE_MAX_RETRIES": "100"},
     {"SVS_POA_VERIFY_PREP": "1"},
     {"SVS_POA_VERIFY_PREP": "1", "SVS_POA_WPJ": "1"},
     {"SVS_POA_VERIFY_PREP": "1", "SVS_POA_PRUNE_SLACK": "-0.3"},
-    {"SVS_POA_VERIFY_PREP": "1", "SVS_POA_WIDE": "1"},
     {"SVS_POA_DEVICE_PREP": "0"},
     {"SVS_POA_STAGING": "vec"},
     {"SVS_POA_STAGING": "vec", "SVS_POA_PRUNE_SLACK": "-0.3"},
 ])
 def test_kernel_variants_match_oracle(env):
-    """Every POA kernel variant gives the oracle's result: row-major with 1/2/4
-    waves per job, strip-major with 1/2/3/4/7/8/16 pipelined waves per job, the
-    strip-major kernel with its pool in global memory, and the strip kernel's
+    """Every POA kernel instance the engine selects gives the oracle's result:
+    1/2/4/8/16 pipelined waves per job, the pool in global memory, and the
     exact pruning off, at its tightest slack, and with a bound above the
-    optimum (every pruned job retried: with the looser retry slack, unpruned, or
-    twice, the second time unpruned; with the tables exported straight
-    into the staging buffer a retried job's block is exported again), and with
-    the tables packed from per-task vectors (SVS_POA_STAGING=vec); and all of
-    that again with 128-column strips after strip 0 (SVS_POA_WIDE=1); with the
-    row tables completed on the device checked table for table against the
-    host's export (SVS_POA_VERIFY_PREP=1), and with the host export only
+    optimum (every pruned job retried: with the looser retry slack, unpruned,
+    or twice, the second time unpruned; with the tables exported straight into
+    the staging buffer a retried job's block is exported again), and with the
+    tables packed from per-task vectors (SVS_POA_STAGING=vec); with the row
+    tables completed on the device checked table for table against the host's
+    export (SVS_POA_VERIFY_PREP=1), and with the host export only
     (SVS_POA_DEVICE_PREP=0)."""
     import os
     from svscope_amd import synth

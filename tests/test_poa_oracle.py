@@ -28,7 +28,7 @@ def test_oracle_rejects_unsupported_modes():
 
 @pytest.fixture(scope="module", params=["rows", "strip", "strip-pruned"])
 def emu(request):
-    """The emulator in both kernel layouts: row-major tables (poa_kernels.hip)
+    """The emulator in both table layouts: row-major tables (export_rows)
     and the strip-major planner with register pass-through (poa_strip.hip);
     "strip-pruned" also re-runs every alignment with the exact pruning at its
     tightest bound (lb = the optimum: same alignment required) and just above
