@@ -23,6 +23,7 @@ ARCH = os.environ.get("SVS_OFFLOAD_ARCH", "gfx950")
 SOURCES = [
     "poa_strip.hip",
     "poa_prep.hip",
+    "poa_fold.hip",
     "em_kernels.hip",
     "misscore_kernels.hip",
     "poa_graph.cpp",

@@ -1,0 +1,792 @@
+// MI355X (gfx950) device half of the POA graph (poa_dgraph.hpp): the
+// per-alignment graph update, topological sort and row export, and the
+// heaviest-bundle consensus + MSA rows of a finished task.
+//
+// Replaces, for the device-resident graphs, what PoaGraph (poa_graph.cpp)
+// does on the host after every alignment: spoa 4.x Graph::AddAlignment,
+// Graph::TopologicalSort, the row export of the strip kernel's tables, and at
+// the end Graph::GenerateMultipleSequenceAlignment / GenerateConsensus, all
+// reached by the reference through `poa(seqs, 1)` (DataScanner.py:206,213,
+// DecisionMaker.py:160,171).  Results are identical to the host graph's, which
+// the engine can check table for table (SVS_POA_VERIFY_GRAPH=1).
+//
+// One wave per task and launch.  The work is latency-bound and mostly
+// sequential (a DFS, a heaviest-path scan), so the kernels are built to share
+// the CUs with the other task group's DP kernel, which they run beside on a
+// stream of their own: one wave per workgroup, no LDS in the update, a few KB
+// in the sort (two bit planes of node flags and the top of the DFS stack).
+//   poa_fold_update_kernel  AddAlignment: the alignment's nodes (matches,
+//       aligned-group members, new nodes; node ids in spoa's creation order),
+//       edges (existing ones gain weight), then both CSR adjacency lists
+//       rebuilt with each node's new edge appended (spoa's push_back order)
+//   poa_fold_sort_kernel    DFS topological sort (spoa's order), then either
+//       the next alignment's lite tables (export_strip_lite) or, for a finished
+//       task, the consensus and the MSA rows
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "poa_dgraph.hpp"
+#include "svs_device.hpp"
+
+namespace svs {
+
+namespace {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// Pointers into a task block are global memory: say so, or every access is a
+// flat one (generic address, counted in both vmcnt and lgkmcnt, never scalar).
+#define GLB __attribute__((address_space(1)))
+typedef GLB uint32_t gu32;
+typedef GLB int32_t gi32;
+typedef GLB uint8_t gu8;
+typedef GLB char gch;
+template <class T> __device__ __forceinline__ GLB T* glb(T* p) { return (GLB T*)(p); }
+template <class T> __device__ __forceinline__ const GLB T* glb(const T* p) { return (const GLB T*)(p); }
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t lanei() { return threadIdx.x & 63u; }
+__device__ __forceinline__ uint64_t below() { return (1ull << lanei()) - 1ull; }
+__device__ __forceinline__ uint32_t popc64(uint64_t m) { return static_cast<uint32_t>(__builtin_popcountll(m)); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint32_t lane_val(uint32_t v, uint32_t l) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(v), static_cast<int32_t>(l)));
+}
+
+// Loads past the vector L1 (agent scope): for words this wave stored earlier
+// in the same kernel (the L1 may still hold the line from before the store).
+__device__ __forceinline__ uint32_t ldc(const gu32* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t ldci(const gi32* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ldc_u8(const gu8* base, uint32_t i) {
+  const uint32_t w = ldc(reinterpret_cast<const gu32*>(base) + (i >> 2));
+  return (w >> (8 * (i & 3u))) & 0xFFu;
+}
+// This wave's stores done, and its L1 invalidated, so that plain loads after
+// it see them.
+__device__ __forceinline__ void wave_sync_mem() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+__device__ __forceinline__ uint32_t wave_add(uint32_t x) {
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+  for (int o = 32; o >= 1; o >>= 1) x = max(x, static_cast<uint32_t>(__shfl_xor(x, o, 64)));
+  return x;
+}
+__device__ __forceinline__ int32_t wave_min_i(int32_t x) {
+  for (int o = 32; o >= 1; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
+  return x;
+}
+__device__ __forceinline__ int32_t wave_max_i(int32_t x) {
+  for (int o = 32; o >= 1; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
+  return x;
+}
+// exclusive prefix sum over the wave; *total = the sum of all lanes
+__device__ __forceinline__ uint32_t wave_excl(uint32_t x, uint32_t* total) {
+  uint32_t s = x;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(s, o, 64);
+    if (static_cast<int>(lanei()) >= o) s += y;
+  }
+  *total = uni(__shfl(s, 63, 64));
+  return s - x;
+}
+
+// The block's arrays (poa_dgraph.hpp layout); b = CSR buffer.
+struct GPtr {
+  gu8* base;
+  gu32* al;
+  gu32 *in_off, *in_nbr, *in_eid, *out_off, *out_nbr, *out_eid;
+  gu32* ew;
+  gu32 *nin, *nout, *r2n, *n2r, *col, *last, *pstart, *pred, *info, *stk;
+};
+
+__device__ __forceinline__ GPtr gptr(uint8_t* blk, uint32_t cv, uint32_t ce, uint32_t b) {
+  const DGraphLayout L = dgraph_layout(cv, ce);
+  GPtr g;
+  gu8* gb = glb(blk);
+  auto u = [&](size_t off) { return reinterpret_cast<gu32*>(gb + off); };
+  g.base = gb + L.base;
+  g.al = u(L.al);
+  // (selects, not a dynamic index: the layout stays in registers)
+  g.in_off = u(b ? L.in_off[1] : L.in_off[0]);
+  g.in_nbr = u(b ? L.in_nbr[1] : L.in_nbr[0]);
+  g.in_eid = u(b ? L.in_eid[1] : L.in_eid[0]);
+  g.out_off = u(b ? L.out_off[1] : L.out_off[0]);
+  g.out_nbr = u(b ? L.out_nbr[1] : L.out_nbr[0]);
+  g.out_eid = u(b ? L.out_eid[1] : L.out_eid[0]);
+  g.ew = u(L.ew);
+  g.nin = u(L.nin);
+  g.nout = u(L.nout);
+  g.r2n = u(L.r2n);
+  g.n2r = u(L.n2r);
+  g.col = u(L.col);
+  g.last = u(L.last);
+  g.pstart = u(L.pstart);
+  g.pred = u(L.pred);
+  g.info = u(L.info);
+  g.stk = u(L.stk);
+  return g;
+}
+
+// One CSR list (in or out) rebuilt into buffer b1 from b0 for nodes
+// 0 .. V1-1, each node's new entry (nw[2v] = eid, nw[2v+1] = neighbour, eid
+// kNone = none) appended; the new-entry slots are reset.  Returns the number
+// of new entries found.
+__device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, const gu32* nbr0, const gu32* eid0,
+                                gu32* off1, gu32* nbr1, gu32* eid1, gu32* nw) {
+  const uint32_t lane = lanei();
+  uint32_t run = 0, found = 0;
+  for (uint32_t v0 = 0; v0 < V1; v0 += 64) {
+    const uint32_t v = v0 + lane;
+    uint32_t a = 0, d = 0, ne = kNone, nb = 0;
+    if (v < V1) {
+      if (v < V0) {
+        a = off0[v];
+        d = off0[v + 1] - a;
+      }
+      ne = nw[2 * v];
+      nb = nw[2 * v + 1];
+    }
+    const uint32_t has = ne != kNone ? 1u : 0u;
+    uint32_t tot;
+    const uint32_t o = run + wave_excl(d + has, &tot);
+    if (v < V1) {
+      off1[v] = o;
+      for (uint32_t k = 0; k < d; ++k) {
+        nbr1[o + k] = nbr0[a + k];
+        eid1[o + k] = eid0[a + k];
+      }
+      if (has) {
+        nbr1[o + d] = nb;
+        eid1[o + d] = ne;
+        nw[2 * v] = kNone;
+      }
+    }
+    found += wave_add(has);
+    run += tot;
+  }
+  if (lane == 0) off1[V1] = run;
+  return uni(found);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- update
+// spoa Graph::AddAlignment (poa_graph.cpp add_alignment_nodes): nodes of the
+// prefix chain, then the suffix chain, then the middle's new nodes in path
+// order; a middle position takes its aligned node when the letters match, else
+// a member of that node's aligned group with its letter, else a new node that
+// joins the group (spoa's aligned_nodes order: the anchor's list, then the
+// anchor; every member appends the newcomer).  Then one edge per consecutive
+// path pair, existing ones gaining weight.
+__global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __restrict__ jobs) {
+  const FoldJob J = jobs[blockIdx.x];
+  const uint32_t lane = lanei();
+  GLB FoldResult* res = glb(J.result);
+  int32_t n = 0;
+  if (!(J.flags & kFoldChain)) {
+    n = *glb(J.aln_status);
+    if (n == kPruneRetry) {
+      if (lane == 0) res->status = kFoldSkipped;
+      return;
+    }
+    if (n < 0) {
+      if (lane == 0) res->status = kFoldErrAln;
+      return;
+    }
+  }
+  const uint32_t V0 = J.V, E0 = J.E, len = J.len;
+  const uint32_t b0 = J.par, b1 = 1u - J.par;
+  const GPtr g = gptr(J.blk, J.cv, J.ce, b0);
+  const GPtr h = gptr(J.blk, J.cv, J.ce, b1);
+  gu32* __restrict__ path = glb(J.paths) + glb(J.path_off)[J.n_paths];
+  const gu8* __restrict__ seq = glb(J.seq);
+  const gi32* __restrict__ aln = glb(J.aln);
+  auto fail = [&](int32_t st) {
+    if (lane == 0) res->status = st;
+  };
+  if (V0 + len > J.cv || E0 + len + 1 > J.ce) return fail(kFoldErrCapacity);
+
+  // first / last aligned read position (positions increase along the path)
+  int32_t first = static_cast<int32_t>(len), last = static_cast<int32_t>(len) - 1;
+  if (n > 0) {
+    int32_t mn = INT32_MAX, mx = -1;
+    for (int32_t c0 = 0; c0 < n; c0 += 64) {
+      const int32_t i = c0 + static_cast<int32_t>(lane);
+      if (i < n) {
+        const int32_t pos = aln[2 * (n - 1 - i) + 1];
+        if (pos >= 0) {
+          mn = min(mn, pos);
+          mx = max(mx, pos);
+        }
+      }
+    }
+    mn = wave_min_i(mn);
+    mx = wave_max_i(mx);
+    if (mx < 0 || mx >= static_cast<int32_t>(len)) return fail(kFoldErrPath);
+    first = mn;
+    last = mx;
+  }
+  const uint32_t nsuf = len - 1u - static_cast<uint32_t>(last);
+  // prefix and suffix chains: fresh nodes V0 .. V0 + first - 1, then the suffix's
+  auto fresh = [&](uint32_t id, uint32_t p) {
+    g.base[id] = seq[p];
+    g.al[4 * id] = 0;
+    g.nin[2 * id] = kNone;
+    g.nout[2 * id] = kNone;
+    path[p] = id;
+  };
+  for (uint32_t p = lane; p < static_cast<uint32_t>(first); p += 64) fresh(V0 + p, p);
+  for (uint32_t p = static_cast<uint32_t>(last) + 1 + lane; p < len; p += 64)
+    fresh(V0 + static_cast<uint32_t>(first) + (p - static_cast<uint32_t>(last) - 1), p);
+  uint32_t next = V0 + static_cast<uint32_t>(first) + nsuf;
+
+  // the middle, 64 forward pairs at a time
+  for (int32_t c0 = 0; c0 < n; c0 += 64) {
+    const int32_t i = c0 + static_cast<int32_t>(lane);
+    int32_t row = -1, pos = -1;
+    if (i < n) {
+      row = aln[2 * (n - 1 - i)];
+      pos = aln[2 * (n - 1 - i) + 1];
+    }
+    const bool act = pos >= 0;
+    const uint32_t letter = act ? seq[pos] : 0u;
+    uint32_t nn = kNone, cur = kNone;
+    // kinds: matched (cur known), insertion (a new node), mismatch (resolved in order below)
+    bool ins = false, mis = false;
+    if (act) {
+      if (row < 0) {
+        ins = true;
+      } else {
+        nn = g.r2n[row];
+        if (nn >= V0) return fail(kFoldErrAln);
+        if (g.base[nn] == letter) cur = nn;  // an old node's letter: never written by this kernel
+        else mis = true;
+      }
+    }
+    const uint64_t ins_m = ballot(ins);
+    uint64_t mis_m = ballot(mis), creat_m = 0;
+    uint32_t created = 0;
+    // mismatches in path order: the aligned group as updated so far (coherent loads)
+    while (mis_m) {
+      const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(mis_m));
+      mis_m &= mis_m - 1;
+      const uint32_t nj = lane_val(nn, j), lt = lane_val(letter, j);
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's earlier group updates have landed
+      const uint32_t cnt = ldc(g.al + 4 * nj);
+      if (cnt > 3) return fail(kFoldErrAligned);
+      uint32_t mem[3] = {0, 0, 0};
+      uint32_t found = kNone;
+      for (uint32_t k = 0; k < cnt; ++k) {
+        mem[k] = ldc(g.al + 4 * nj + 1 + k);
+        if (found == kNone && ldc_u8(g.base, mem[k]) == lt) found = mem[k];
+      }
+      uint32_t cj = found;
+      if (found == kNone) {
+        if (cnt >= 3) return fail(kFoldErrAligned);  // a fifth letter in one column
+        const uint64_t bj = (1ull << j) - 1ull;
+        cj = next + popc64(ins_m & bj) + created;
+        ++created;
+        creat_m |= 1ull << j;
+        if (lane == 0) {
+          g.base[cj] = static_cast<uint8_t>(lt);
+          g.nin[2 * cj] = kNone;
+          g.nout[2 * cj] = kNone;
+          // newcomer's list: the anchor's list, then the anchor
+          g.al[4 * cj] = cnt + 1;
+          for (uint32_t k = 0; k < cnt; ++k) g.al[4 * cj + 1 + k] = mem[k];
+          g.al[4 * cj + 1 + cnt] = nj;
+        }
+        // every member, then the anchor, appends the newcomer
+        for (uint32_t k = 0; k <= cnt; ++k) {
+          const uint32_t a = k < cnt ? mem[k] : nj;
+          const uint32_t ca = ldc(g.al + 4 * a);
+          if (ca >= 3) return fail(kFoldErrAligned);
+          if (lane == 0) {
+            g.al[4 * a + 1 + ca] = cj;
+            g.al[4 * a] = ca + 1;
+          }
+          __builtin_amdgcn_s_waitcnt(0);
+        }
+      }
+      if (lane == j) cur = cj;
+    }
+    if (ins) {
+      cur = next + popc64(ins_m & below()) + popc64(creat_m & below());
+      g.base[cur] = static_cast<uint8_t>(letter);
+      g.al[4 * cur] = 0;
+      g.nin[2 * cur] = kNone;
+      g.nout[2 * cur] = kNone;
+    }
+    next += popc64(ins_m) + created;
+    if (act) path[pos] = cur;
+  }
+  if (next > J.cv || next - V0 > len) return fail(kFoldErrCapacity);
+  wave_sync_mem();
+
+  // edges along the path: existing ones gain weight, new ones are recorded at
+  // their head (nin) and tail (nout) for the CSR rebuild
+  uint32_t E1 = E0;
+  for (uint32_t c0 = 0; c0 + 1 < len; c0 += 64) {
+    const uint32_t p = c0 + lane;
+    const bool inb = p + 1 < len;
+    uint32_t prev = 0, cur = 0, eid = kNone;
+    if (inb) {
+      prev = path[p];
+      cur = path[p + 1];
+      if (prev < V0 && cur < V0) {
+        const uint32_t a = g.out_off[prev], b = g.out_off[prev + 1];
+        for (uint32_t x = a; x < b; ++x)
+          if (g.out_nbr[x] == cur) {
+            eid = g.out_eid[x];
+            break;
+          }
+      }
+    }
+    const bool isnew = inb && eid == kNone;
+    const uint64_t nm = ballot(isnew);
+    if (isnew) {
+      eid = E1 + popc64(nm & below());
+      g.ew[eid] = 1;
+      g.nin[2 * cur] = eid;
+      g.nin[2 * cur + 1] = prev;
+      g.nout[2 * prev] = eid;
+      g.nout[2 * prev + 1] = cur;
+    } else if (inb) {
+      g.ew[eid] += 1;
+    }
+    E1 += popc64(nm);
+  }
+  wave_sync_mem();
+  const uint32_t V1 = next;
+  // both adjacency lists into the other buffer, the new edge of each node last
+  const uint32_t fin = rebuild_csr(V0, V1, g.in_off, g.in_nbr, g.in_eid, h.in_off, h.in_nbr, h.in_eid, g.nin);
+  const uint32_t fout = rebuild_csr(V0, V1, g.out_off, g.out_nbr, g.out_eid, h.out_off, h.out_nbr, h.out_eid, g.nout);
+  // a node twice on the path would have lost one of its new edges
+  if (fin != E1 - E0 || fout != E1 - E0) return fail(kFoldErrPath);
+  if (lane == 0) {
+    res->status = kFoldOk;
+    res->V = V1;
+    res->E = E1;
+  }
+}
+
+// ---------------------------------------------------------------- sort
+// spoa Graph::TopologicalSort (poa_graph.cpp sort_ranks): roots in node-id
+// order; a node on top of the stack pushes its unfinished in-edge tails (in
+// in-edge order) and, unless it was itself pushed as an aligned node, its
+// unfinished aligned nodes (flagging them); once nothing was pushed it is done
+// and, unless flagged, emitted together with its aligned list, which also
+// makes one MSA column.
+//
+// Node flags live in LDS (two bit planes), the stack's top in LDS (the rest
+// spills to the block's stk array in blocks of half the LDS stack).
+namespace {
+
+struct SortState {
+  uint32_t* done;  // LDS bit plane
+  uint32_t* ign;   // LDS bit plane
+  uint32_t* st;    // LDS stack
+  uint32_t cap;    // LDS stack entries (even)
+  gu32* spill;     // global spill area
+  uint32_t spilled;  // entries in the spill area (below the LDS part)
+  uint32_t sp;       // entries in the LDS part
+};
+
+__device__ __forceinline__ bool bit_of(const uint32_t* plane, uint32_t v) { return (plane[v >> 5] >> (v & 31u)) & 1u; }
+
+}  // namespace
+
+// Emission, export and finalize helpers take the arrays as restrict
+// parameters so the compiler can read the CSR through the scalar cache.
+__device__ __forceinline__ void emit_node(uint32_t node, uint32_t r, uint32_t c, gu32* __restrict__ r2n,
+                                          gu32* __restrict__ n2r, gu32* __restrict__ col) {
+  if (lanei() == 0) {
+    r2n[r] = node;
+    n2r[node] = r;
+    col[node] = c;
+  }
+}
+
+__device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ in_off, const gu32* __restrict__ in_nbr,
+                            const gu32* __restrict__ al, gu32* __restrict__ r2n, gu32* __restrict__ n2r,
+                            gu32* __restrict__ col, SortState& S, uint32_t* ncol_out) {
+  const uint32_t lane = lanei();
+  const uint32_t W = (V + 31u) >> 5;
+  for (uint32_t w = lane; w < W; w += 64) {
+    S.done[w] = 0;
+    S.ign[w] = 0;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  uint32_t cnt = 0, ncol = 0;
+  // push / top / pop on the two-level stack (uniform control)
+  auto push = [&](uint32_t v) -> bool {
+    if (S.sp == S.cap) {
+      // spill the lower half of the LDS part
+      const uint32_t half = S.cap / 2;
+      for (uint32_t k = lane; k < half; k += 64) S.spill[S.spilled + k] = S.st[k];
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t k = lane; k < half; k += 64) S.st[k] = S.st[k + half];
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      S.spilled += half;
+      S.sp -= half;
+    }
+    if (lane == 0) S.st[S.sp] = v;
+    ++S.sp;
+    return true;
+  };
+  auto refill = [&]() {
+    // the LDS part is empty: bring back up to half of it from the spill area
+    const uint32_t half = S.cap / 2;
+    const uint32_t k0 = S.spilled > half ? S.spilled - half : 0u, m = S.spilled - k0;
+    __builtin_amdgcn_s_waitcnt(0);
+    for (uint32_t k = lane; k < m; k += 64) S.st[k] = ldc(S.spill + k0 + k);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    S.spilled = k0;
+    S.sp = m;
+  };
+  auto set_bit = [&](uint32_t* plane, uint32_t v) {
+    if (lane == 0) plane[v >> 5] |= 1u << (v & 31u);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  };
+  uint32_t root = 0;
+  while (root < V) {
+    const uint32_t fw = uni(~S.done[root >> 5]) >> (root & 31u);
+    if (fw == 0) {
+      root = (root | 31u) + 1u;
+      continue;
+    }
+    root += static_cast<uint32_t>(__builtin_ctz(fw));
+    if (root >= V) break;
+    push(root);
+    while (S.sp + S.spilled > 0) {
+      if (S.sp == 0) refill();
+      const uint32_t cur = uni(S.st[S.sp - 1]);
+      if (bit_of(S.done, cur)) {
+        --S.sp;
+        continue;
+      }
+      bool valid = true;
+      const uint32_t a = in_off[cur], b = in_off[cur + 1];
+      for (uint32_t x = a; x < b; ++x) {
+        const uint32_t t = in_nbr[x];
+        if (!bit_of(S.done, t)) {
+          push(t);
+          valid = false;
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      const bool ig = bit_of(S.ign, cur);
+      const uint32_t alc = al[4 * cur];
+      if (!ig) {
+        for (uint32_t k = 0; k < alc; ++k) {
+          const uint32_t m = al[4 * cur + 1 + k];
+          if (!bit_of(S.done, m)) {
+            push(m);
+            set_bit(S.ign, m);
+            valid = false;
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      if (valid) {
+        set_bit(S.done, cur);
+        if (!ig) {
+          emit_node(cur, cnt++, ncol, r2n, n2r, col);
+          for (uint32_t k = 0; k < alc; ++k) emit_node(al[4 * cur + 1 + k], cnt++, ncol, r2n, n2r, col);
+          ++ncol;
+        }
+        // the entry popped is cur's (pushes above only happen when !valid)
+        if (S.sp == 0) refill();
+        --S.sp;
+      }
+    }
+    ++root;
+  }
+  *ncol_out = ncol;
+  return cnt == V ? kFoldOk : kFoldErrStack;
+}
+
+// Lite export of the next alignment's row tables (PoaGraph::export_strip_lite):
+// per rank row its in-edge rows (CSR, in-edge order; bit 31: this in-edge is
+// its tail row's last pool read), base | sink << 8 | store << 9 | in-degree
+// << 10; the planner's slot count and the largest in-degree.
+__device__ void export_lite(uint32_t V, const gu8* __restrict__ base, const gu32* __restrict__ in_off,
+                            const gu32* __restrict__ in_nbr, const gu32* __restrict__ out_off,
+                            const gu32* __restrict__ r2n, const gu32* __restrict__ n2r, gu32* __restrict__ last,
+                            gu32* __restrict__ pstart, gu32* __restrict__ pred, gu32* __restrict__ info,
+                            uint32_t* n_slots, uint32_t* max_preds) {
+  const uint32_t lane = lanei();
+  // pass 1: pstart, in-edge rows, per row words without the store bit; last
+  // pool reader of every row (an in-edge from the row just above is served
+  // from registers and does not count)
+  for (uint32_t r = lane; r < V; r += 64) last[r] = 0;
+  wave_sync_mem();
+  uint32_t run = 0, mp = 0;
+  for (uint32_t r0 = 0; r0 < V; r0 += 64) {
+    const uint32_t r = r0 + lane;
+    uint32_t node = 0, a = 0, d = 0;
+    if (r < V) {
+      node = r2n[r];
+      a = in_off[node];
+      d = in_off[node + 1] - a;
+    }
+    uint32_t tot;
+    const uint32_t o = run + wave_excl(d, &tot);
+    if (r < V) {
+      pstart[r] = o;
+      const bool sink = out_off[node + 1] == out_off[node];
+      info[r] = static_cast<uint32_t>(base[node]) | (sink ? 0x100u : 0u) | (d << 10);
+      for (uint32_t k = 0; k < d; ++k) {
+        const uint32_t pr = n2r[in_nbr[a + k]];
+        pred[o + k] = pr + 1;
+        if (pr + 1 != r) __hip_atomic_fetch_max(last + pr, r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    mp = max(mp, d);
+    run += tot;
+  }
+  if (lane == 0) pstart[V] = run;
+  wave_sync_mem();
+  // pass 2: store bits, last-read flags, and the slot count of the planner
+  // (slots in use after row r's own: stores so far - frees before r)
+  int32_t live_max = 0, carry = 0;  // carry: stores - frees before the chunk
+  for (uint32_t r0 = 0; r0 < V; r0 += 64) {
+    const uint32_t r = r0 + lane;
+    uint32_t st = 0, fr = 0;
+    if (r < V) {
+      st = last[r] != 0 ? 1u : 0u;
+      if (st) info[r] |= 0x200u;
+      const uint32_t a = pstart[r], b = (r + 1 < V) ? pstart[r + 1] : run;
+      for (uint32_t x = a; x < b; ++x) {
+        const uint32_t pr = pred[x] - 1;
+        if (pr + 1 != r && last[pr] == r + 1) {
+          pred[x] = (pr + 1) | 0x80000000u;
+          ++fr;
+        }
+      }
+    }
+    uint32_t tst, tfr;
+    const uint32_t est = wave_excl(st, &tst), efr = wave_excl(fr, &tfr);
+    const int32_t live = carry + static_cast<int32_t>(est + st) - static_cast<int32_t>(efr);
+    live_max = max(live_max, wave_max_i(r < V ? live : 0));
+    carry += static_cast<int32_t>(tst) - static_cast<int32_t>(tfr);
+  }
+  *n_slots = 1u + static_cast<uint32_t>(max(0, live_max));
+  *max_preds = uni(wave_max(mp));
+}
+
+// Heaviest-bundle consensus (PoaGraph::consensus, spoa GenerateConsensus with
+// min_coverage <= 0).  Edge weights are kept halved (spoa adds 2 per
+// sequence); with score' = (score - 1) / 2 every comparison is the same.
+// Written into out reversed; returns its length.
+__device__ uint32_t consensus_rev(uint32_t V, const gu8* __restrict__ base, const gu32* __restrict__ in_off,
+                                  const gu32* __restrict__ in_nbr, const gu32* __restrict__ in_eid,
+                                  const gu32* __restrict__ out_off, const gu32* __restrict__ out_nbr,
+                                  const gu32* __restrict__ ew, const gu32* __restrict__ r2n,
+                                  const gu32* __restrict__ n2r, gi32* __restrict__ score, gi32* __restrict__ predn,
+                                  gch* __restrict__ out) {
+  const uint32_t lane = lanei();
+  auto sc = [&](int32_t v) -> int32_t { return ldci(score + v); };
+  for (uint32_t v = lane; v < V; v += 64) {
+    score[v] = -1;
+    predn[v] = -1;
+  }
+  wave_sync_mem();
+  int32_t best = -1, best_sc = 0;
+  for (uint32_t r = 0; r < V; ++r) {
+    const uint32_t node = r2n[r];
+    int32_t s = -1, p = -1, sp = 0;
+    for (uint32_t x = in_off[node]; x < in_off[node + 1]; ++x) {
+      const int32_t t = static_cast<int32_t>(in_nbr[x]);
+      const int32_t w = static_cast<int32_t>(ew[in_eid[x]]);
+      const int32_t st = sc(t);
+      if (s < w || (s == w && sp <= st)) {
+        s = w;
+        p = t;
+        sp = st;
+      }
+    }
+    if (p != -1) s += sp;
+    if (lane == 0) {
+      score[node] = s;
+      predn[node] = p;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    if (best == -1 || best_sc < s) {
+      best = static_cast<int32_t>(node);
+      best_sc = s;
+    }
+  }
+  // branch completion while the best node has successors
+  while (out_off[best + 1] != out_off[best]) {
+    const uint32_t start = static_cast<uint32_t>(best), rank = n2r[start];
+    for (uint32_t e = out_off[start]; e < out_off[start + 1]; ++e) {
+      const uint32_t hd = out_nbr[e];
+      for (uint32_t f = in_off[hd]; f < in_off[hd + 1]; ++f)
+        if (in_nbr[f] != start && lane == 0) score[in_nbr[f]] = -1;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    best = -1;
+    best_sc = 0;
+    for (uint32_t r = rank + 1; r < V; ++r) {
+      const uint32_t node = r2n[r];
+      int32_t s = -1, p = -1, sp = 0;
+      for (uint32_t x = in_off[node]; x < in_off[node + 1]; ++x) {
+        const int32_t t = static_cast<int32_t>(in_nbr[x]);
+        const int32_t st = sc(t);
+        if (st == -1) continue;
+        const int32_t w = static_cast<int32_t>(ew[in_eid[x]]);
+        if (s < w || (s == w && sp <= st)) {
+          s = w;
+          p = t;
+          sp = st;
+        }
+      }
+      if (p != -1) s += sp;
+      if (lane == 0) {
+        score[node] = s;
+        predn[node] = p;
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      if (best == -1 || best_sc < s) {
+        best = static_cast<int32_t>(node);
+        best_sc = s;
+      }
+    }
+  }
+  uint32_t n = 0;
+  for (int32_t x = best; x != -1; x = ldci(predn + x)) {
+    if (lane == 0) out[n] = static_cast<char>(base[x]);
+    ++n;
+  }
+  return n;
+}
+
+// MSA rows: every sequence's path nodes at their columns, '-' elsewhere.
+__device__ void msa_rows(uint32_t n_paths, const gu32* __restrict__ paths, const gu32* __restrict__ path_off,
+                         const gu32* __restrict__ colv, const gu8* __restrict__ base, uint32_t ncol,
+                         gch* __restrict__ out, uint32_t stride) {
+  const uint32_t lane = lanei();
+  for (uint32_t s = 0; s < n_paths; ++s) {
+    gch* row = out + static_cast<uint64_t>(s) * stride;
+    for (uint32_t c = lane; c < ncol; c += 64) row[c] = '-';
+  }
+  wave_sync_mem();
+  for (uint32_t s = 0; s < n_paths; ++s) {
+    gch* row = out + static_cast<uint64_t>(s) * stride;
+    const uint32_t a = path_off[s], b = path_off[s + 1];
+    for (uint32_t k = a + lane; k < b; k += 64) {
+      const uint32_t node = paths[k];
+      row[colv[node]] = static_cast<char>(base[node]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __restrict__ jobs, uint32_t lds_words) {
+  extern __shared__ uint32_t lds[];
+  const FoldJob J = jobs[blockIdx.x];
+  GLB FoldResult* res = glb(J.result);
+  if (uni(static_cast<uint32_t>(res->status)) != static_cast<uint32_t>(kFoldOk)) return;
+  const uint32_t V = uni(res->V);
+  const uint32_t b1 = 1u - J.par;
+  const GPtr g = gptr(J.blk, J.cv, J.ce, b1);
+  const uint32_t W = (V + 31u) >> 5;
+  SortState S;
+  S.done = lds;
+  S.ign = lds + W;
+  S.st = lds + 2 * W;
+  S.cap = ((lds_words - 2 * W) / 2) * 2;
+  S.spill = g.stk;
+  S.spilled = 0;
+  S.sp = 0;
+  uint32_t ncol = 0;
+  if (S.cap < 64) {
+    if (lanei() == 0) res->status = kFoldErrStack;
+    return;
+  }
+  const int32_t st = dfs_sort(V, g.in_off, g.in_nbr, g.al, g.r2n, g.n2r, g.col, S, &ncol);
+  if (st != kFoldOk) {
+    if (lanei() == 0) res->status = st;
+    return;
+  }
+  wave_sync_mem();
+  uint32_t n_slots = 0, max_preds = 0;
+  if (J.flags & kFoldExport)
+    export_lite(V, g.base, g.in_off, g.in_nbr, g.out_off, g.r2n, g.n2r, g.last, g.pstart, g.pred, g.info, &n_slots,
+                &max_preds);
+  if (J.flags & kFoldFinal) {
+    const uint32_t nc = consensus_rev(V, g.base, g.in_off, g.in_nbr, g.in_eid, g.out_off, g.out_nbr, g.ew, g.r2n,
+                                      g.n2r, reinterpret_cast<gi32*>(g.last), reinterpret_cast<gi32*>(g.pstart),
+                                      glb(J.cons_out));
+    if (J.flags & kFoldMsa)
+      msa_rows(J.n_paths + 1, glb(J.paths), glb(J.path_off), g.col, g.base, ncol, glb(J.msa_out), J.msa_stride);
+    if (lanei() == 0) res->pad0 = nc;
+  }
+  if (lanei() == 0) {
+    res->n_slots = n_slots;
+    res->max_preds = max_preds;
+    res->ncol = ncol;
+  }
+}
+
+// Block growth: the graph of a task moved into a larger block (capacities
+// cv1 >= cv0, ce1 >= ce0), both CSR buffers' current one only.
+__global__ __launch_bounds__(256) void poa_dgraph_move_kernel(const uint8_t* __restrict__ src, uint32_t cv0,
+                                                              uint32_t ce0, uint8_t* __restrict__ dst, uint32_t cv1,
+                                                              uint32_t ce1, uint32_t V, uint32_t E, uint32_t par) {
+  const DGraphLayout A = dgraph_layout(cv0, ce0), B = dgraph_layout(cv1, ce1);
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+  auto cp = [&](size_t a, size_t b, size_t bytes) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src + a);
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst + b);
+    for (size_t k = t; k < (bytes + 3) / 4; k += nt) d[k] = s[k];
+  };
+  cp(A.base, B.base, V);
+  cp(A.al, B.al, 16ull * V);
+  auto pick = [&](const size_t* x) { return par ? x[1] : x[0]; };
+  cp(pick(A.in_off), pick(B.in_off), 4ull * (V + 1));
+  cp(pick(A.in_nbr), pick(B.in_nbr), 4ull * E);
+  cp(pick(A.in_eid), pick(B.in_eid), 4ull * E);
+  cp(pick(A.out_off), pick(B.out_off), 4ull * (V + 1));
+  cp(pick(A.out_nbr), pick(B.out_nbr), 4ull * E);
+  cp(pick(A.out_eid), pick(B.out_eid), 4ull * E);
+  cp(A.ew, B.ew, 4ull * E);
+  cp(A.nin, B.nin, 8ull * V);
+  cp(A.nout, B.nout, 8ull * V);
+  cp(A.r2n, B.r2n, 4ull * V);
+  cp(A.n2r, B.n2r, 4ull * V);
+  cp(A.col, B.col, 4ull * V);
+  cp(A.pstart, B.pstart, 4ull * (V + 1));
+  cp(A.pred, B.pred, 4ull * E);
+  cp(A.info, B.info, 4ull * V);
+}
+
+hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, hipStream_t stream) {
+  if (n_jobs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(poa_fold_update_kernel, dim3(n_jobs), dim3(64), 0, stream, jobs);
+  hipLaunchKernelGGL(poa_fold_sort_kernel, dim3(n_jobs), dim3(64), lds_words * 4, stream, jobs, lds_words);
+  return hipGetLastError();
+}
+
+hipError_t launch_dgraph_move(const uint8_t* src, uint32_t cv0, uint32_t ce0, uint8_t* dst, uint32_t cv1, uint32_t ce1,
+                              uint32_t V, uint32_t E, uint32_t par, hipStream_t stream) {
+  hipLaunchKernelGGL(poa_dgraph_move_kernel, dim3(64), dim3(256), 0, stream, src, cv0, ce0, dst, cv1, ce1, V, E, par);
+  return hipGetLastError();
+}
+
+}  // namespace svs

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "poa_dgraph.hpp"
 #include "poa_graph.hpp"
 #include "svs_device.hpp"
 
@@ -60,22 +61,16 @@ struct Chunk {
 // Each keeps the words of its current chunk in a VGPR and writes finished
 // chunks to a per-job scratch area (`scr`, 3 words per row) that the rare
 // references further back read.
-__global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __restrict__ jobs, PoaScore P,
-                                                            uint8_t* __restrict__ base) {
+// One job's tables: V rows, in-edge CSR (gps, gpr) and per-row words (ginfo)
+// in; records, in-edge slots and column 0 out; per-wave scratch after the
+// in-edge slots; pool slots handed out from slot_base.
+__device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base, const uint32_t* __restrict__ gps,
+                               const uint32_t* __restrict__ gpr, const uint32_t* __restrict__ ginfo,
+                               uint32_t* __restrict__ rec, uint32_t* __restrict__ pslot, int32_t* __restrict__ c0) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = uni(threadIdx.x >> 6);
-  const PoaJob J = jobs[blockIdx.x];
-  if (!(J.prep & 1u)) return;
-  const uint32_t V = J.n_rows;
-  const uint32_t* __restrict__ gps = reinterpret_cast<const uint32_t*>(base) + J.pstart_off;
-  const uint32_t* __restrict__ gpr = reinterpret_cast<const uint32_t*>(base) + J.pred_off;
-  const uint32_t* __restrict__ ginfo = reinterpret_cast<const uint32_t*>(base) + J.info_off;
-  uint32_t* __restrict__ rec = reinterpret_cast<uint32_t*>(base) + 4ull * J.rec_off;
-  uint32_t* __restrict__ pslot = reinterpret_cast<uint32_t*>(base) + J.pslot_off;
-  int32_t* __restrict__ c0 = reinterpret_cast<int32_t*>(base) + 3ull * J.row_off;
   // this wave's scratch words, one per row (after the job's in-edge slots)
-  uint32_t* scr = reinterpret_cast<uint32_t*>(base) + J.pslot_off + ((uni(gps[V]) + 3u) & ~3u) +
-                  static_cast<uint64_t>(wave) * ((V + 3u) & ~3u);
+  uint32_t* scr = pslot + ((uni(gps[V]) + 3u) & ~3u) + static_cast<uint64_t>(wave) * ((V + 3u) & ~3u);
   const uint32_t E = uni(gps[V]);
 
   auto load = [&](uint32_t r0) -> Chunk {
@@ -120,7 +115,7 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
 
   if (wave == 0) {
     // pool slots, record words w0 w1 w3, in-edge slots
-    uint32_t next = J.prep >> 1, fsp = 0;
+    uint32_t next = slot_base, fsp = 0;
     uint32_t fstack = 0;  // free list: lane i = entry i
     uint32_t ebuf = 0, ebase = 0;  // in-edge slots of edges ebase + lane
     uint32_t pwin = 0;             // lane i: pool slot of row r0 - 64 + i (the chunk before)
@@ -260,15 +255,44 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
   }
 }
 
+__global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __restrict__ jobs, PoaScore P) {
+  const PoaJob J = jobs[blockIdx.x];
+  if (!(J.prep & 1u)) return;
+  strip_prep_job(P, J.n_rows, J.prep >> 1, J.pstart, J.pred, J.info, const_cast<uint32_t*>(J.rec),
+                 const_cast<uint32_t*>(J.pslot), const_cast<int32_t*>(J.col0));
+}
+
+// The same for the device-resident graphs (poa_dgraph.hpp): the jobs whose
+// fold exported the next alignment's lite tables into their block.
+__global__ __launch_bounds__(192) void poa_dgraph_prep_kernel(const FoldJob* __restrict__ jobs, PoaScore P) {
+  const FoldJob J = jobs[blockIdx.x];
+  if (!(J.flags & kFoldExport)) return;
+  const FoldResult* res = J.result;
+  if (uni(static_cast<uint32_t>(res->status)) != static_cast<uint32_t>(kFoldOk)) return;
+  const uint32_t V = uni(res->V);
+  if (V == 0 || V > kStripPrepMaxRows || uni(res->n_slots) > kStripPrepMaxSlots || uni(res->max_preds) > 31u) return;
+  const DGraphLayout L = dgraph_layout(J.cv, J.ce);
+  uint8_t* b = J.blk;
+  strip_prep_job(P, V, 1u, reinterpret_cast<const uint32_t*>(b + L.pstart), reinterpret_cast<const uint32_t*>(b + L.pred),
+                 reinterpret_cast<const uint32_t*>(b + L.info), reinterpret_cast<uint32_t*>(b + L.rec),
+                 reinterpret_cast<uint32_t*>(b + L.pslot), reinterpret_cast<int32_t*>(b + L.col0));
+}
+
 }  // namespace
 
 size_t strip_prep_scratch_words(uint32_t V) { return 3ull * ((V + 3u) & ~3u); }
 
-hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore& score, uint8_t* base,
-                                 uint32_t max_rows, hipStream_t stream) {
+hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore& score, uint32_t max_rows,
+                                 hipStream_t stream) {
   if (n_jobs <= 0) return hipSuccess;
   if (max_rows > kStripPrepMaxRows) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(poa_strip_prep_kernel, dim3(n_jobs), dim3(192), 0, stream, jobs, score, base);
+  hipLaunchKernelGGL(poa_strip_prep_kernel, dim3(n_jobs), dim3(192), 0, stream, jobs, score);
+  return hipGetLastError();
+}
+
+hipError_t launch_dgraph_prep(const FoldJob* jobs, int n_jobs, const PoaScore& score, hipStream_t stream) {
+  if (n_jobs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(poa_dgraph_prep_kernel, dim3(n_jobs), dim3(192), 0, stream, jobs, score);
   return hipGetLastError();
 }
 

@@ -181,9 +181,7 @@ template <bool LDSP, int WPJ, bool PRUNE>
 #endif
 #define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? SVS_PRUNE_OCC : 1)))
 __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
-    const PoaJob* __restrict__ jobs, int n_jobs, PoaScore Parg, const uint32_t* __restrict__ rec_all,
-    const uint32_t* __restrict__ row_pstart, const uint32_t* __restrict__ pred_row,
-    const uint32_t* __restrict__ pred_slot, const int32_t* __restrict__ col0, const uint8_t* __restrict__ seqs,
+    const PoaJob* __restrict__ jobs, int n_jobs, PoaScore Parg,
     uint16_t* __restrict__ tb, int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
     int32_t* __restrict__ gpool, int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
   extern __shared__ int32_t lds[];
@@ -212,12 +210,12 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * kStride;
   else pool = gpool + J.pool_off + static_cast<uint64_t>(wave) * ((nslot * kSlotInts + 63) / 64 * 64);
   uint16_t* __restrict__ tbj = tb + J.tb_off;
-  const uint32_t* __restrict__ rec = rec_all + static_cast<uint64_t>(J.rec_off) * kRecWords;
-  const uint32_t* __restrict__ rps = row_pstart + J.pstart_off;
-  const uint32_t* __restrict__ prow = pred_row + J.pred_off;
-  const uint32_t* __restrict__ pslot = pred_slot + J.pslot_off;
-  const int32_t* __restrict__ rc0 = col0 + 3ull * J.row_off;
-  const uint8_t* __restrict__ seq = seqs + J.seq_off;
+  const uint32_t* __restrict__ rec = J.rec;
+  const uint32_t* __restrict__ rps = J.pstart;
+  const uint32_t* __restrict__ prow = J.pred;
+  const uint32_t* __restrict__ pslot = J.pslot;
+  const int32_t* __restrict__ rc0 = J.col0;
+  const uint8_t* __restrict__ seq = J.seq;
   int32_t* __restrict__ bnd = bnd_all + J.bnd_off;
   // The same carry buffer, read-only: loads through it are uniform and never
   // clobbered by this kernel's stores (those go through bnd), so they become
@@ -259,7 +257,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     constexpr bool FIRST = decltype(first_tag)::value;
     const int32_t j0 = s << 6;
     const int32_t j = j0 + lane;
-    const uint8_t rc = seq[j - 1];  // seqs[seq_off - 1] is a zero pad byte (column 0)
+    const uint8_t rc = seq[j - 1];  // seq[-1] is a zero pad byte (column 0)
     uint16_t* __restrict__ tbl = tbj + j;  // this lane's column of the traceback codes
     const int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
     int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
@@ -812,7 +810,7 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * kStripSlotBytes : 0;
 #define SVS_STRIP3(LP, W, PR)                                                                                     \
   hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, a.n_jobs,  \
-                     a.score, a.rec, a.row_pstart, a.pred_row, a.pred_slot, a.col0, a.seqs, a.tb, a.bnd, a.bnd,     \
+                     a.score, a.tb, a.bnd, a.bnd,                                                                    \
                      a.pool, a.aln, a.aln_len, a.lds_slots)
 #define SVS_STRIP(LP, W)              \
   do {                                \

@@ -9,27 +9,29 @@ struct PoaScore {
   int32_t m, n, g, e, q, c;
 };
 
-// One read-vs-graph NW alignment (one wave).  Offsets are element offsets into
-// the batch-wide buffers of PoaLaunch.
+// One read-vs-graph NW alignment (one workgroup of the strip kernel).  The
+// row tables are device pointers: into the launch's staging copy (host-built
+// graphs) or into the task's graph block (device-resident graphs,
+// poa_dgraph.hpp); the outputs are element offsets into the launch buffers.
 struct PoaJob {
-  uint64_t tb_off;    // uint16 traceback codes, rows 1..n_rows, stride ls
-  uint64_t pool_off;  // int32 row pool: n_slots x {H,F,O} x ls
-  uint64_t aln_off;   // output pairs (2 x int32), capacity n_rows + len + 1
-  uint32_t row_off;   // into row_info / row_slot
-  uint32_t pstart_off;  // into row_pstart (n_rows + 1 entries)
-  uint32_t pred_off;  // base of this job's pred_row / pred_slot entries
-  uint32_t seq_off;   // into seqs: read start; seqs[seq_off-1] is a zero pad byte, region ls+64 bytes
-  uint32_t n_rows;    // graph nodes
-  uint32_t len;       // read length
-  uint32_t ls;        // row stride (>= len + 1, multiple of 64)
-  uint32_t n_slots;   // pool slots (slot 0 = virtual row 0)
-  uint64_t bnd_off;   // strip kernel: int32 strip-boundary carries, 2 x n_rows x 4
-  uint32_t rec_off;   // strip kernel: row records (kRecWords uint32 per row), in rows
-  int32_t lb;         // strip kernel: pruning bound (kNoPrune = off), see poa_strip.hip
-  uint32_t pslot_off;  // strip kernel: base of this job's pred_slot entries
-  uint32_t info_off;   // strip kernel, prep jobs: per-row words (export_strip_lite)
-  uint32_t prep;       // bit 0: row records, in-edge slots and column 0 come from
-                       // poa_strip_prep_kernel; bits 1..: the first pool slot
+  const uint32_t* rec;    // row records, kRecWords per row (export_strip_rows)
+  const uint32_t* pstart; // n_rows + 1 CSR offsets of the in-edge rows, rank order
+  const uint32_t* pred;   // 1-based in-edge rows (bit 31: export_strip_lite's last-read flag)
+  const uint32_t* pslot;  // pool slots of the in-edges
+  const int32_t* col0;    // H, F, O of DP column 0 per row
+  const uint8_t* seq;     // the read; seq[-1] is a zero pad byte, region ls + 64 bytes
+  const uint32_t* info;   // prep jobs: per-row words (export_strip_lite)
+  uint64_t tb_off;        // uint16 traceback codes, rows 1..n_rows, stride ls
+  uint64_t bnd_off;       // int32 strip-boundary carries
+  uint64_t pool_off;      // int32 global row pool (pools that do not fit LDS)
+  uint64_t aln_off;       // output pairs (2 x int32), capacity n_rows + len + 1
+  uint32_t n_rows;        // graph nodes
+  uint32_t len;           // read length
+  uint32_t ls;            // row stride (>= len + 1, multiple of 64)
+  uint32_t n_slots;       // pool slots (slot 0 = virtual row 0)
+  int32_t lb;             // pruning bound (kNoPrune = off), see poa_strip.hip
+  uint32_t prep;          // bit 0: rec, pslot and col0 come from poa_strip_prep_kernel;
+                          // bits 1..: the first pool slot
 };
 
 // PoaJob::lb value that turns the strip kernel's exact pruning off.
@@ -45,19 +47,13 @@ struct PoaLaunch {
   const PoaJob* jobs;
   int n_jobs;
   PoaScore score;
-  const uint32_t* row_pstart;
-  const uint32_t* pred_row;
-  const uint32_t* pred_slot;
-  const int32_t* col0;
-  const uint8_t* seqs;
   uint16_t* tb;
-  int32_t* pool;
-  int32_t* aln;
-  int32_t* aln_len;    // per job: path length; strip kernel also [n_jobs + job] best
-                       // sink score and [2 n_jobs + job] strip rows computed
-  int waves_per_job;     // strip-pipeline waves per job: 1, 2, 4, 8 (16 with the pool in LDS)
-  const uint32_t* rec;   // row records (export_strip_rows)
   int32_t* bnd;          // strip-boundary carries
+  int32_t* pool;         // global row pools
+  int32_t* aln;
+  int32_t* aln_len;      // per job: path length; also [n_jobs + job] best sink score
+                         // and [2 n_jobs + job] strip rows computed
+  int waves_per_job;     // strip-pipeline waves per job: 1, 2, 4, 8 (16 with the pool in LDS)
   uint32_t lds_slots;    // pool slots per wave held in LDS (max n_slots of the launch)
   bool prune;            // some job has a pruning bound: the pruning kernel variant
 };
@@ -75,12 +71,12 @@ constexpr uint64_t kStripLdsBytes = 160 * 1024 - 256;
 
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream);
 // Device half of the strip row export (poa_prep.hip) for the jobs with
-// PoaJob::prep bit 0; every offset of those jobs indexes `base`.
+// PoaJob::prep bit 0.
 constexpr uint32_t kStripPrepMaxRows = 16384;  // rows of a prep job (16-bit path lengths and slots)
 constexpr uint32_t kStripPrepMaxSlots = 64;    // pool slots of a prep job (free list in one VGPR)
 size_t strip_prep_scratch_words(uint32_t n_rows);  // after the job's in-edge slots (rounded to 4)
-hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore& score, uint8_t* base,
-                                 uint32_t max_rows, hipStream_t stream);
+hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore& score, uint32_t max_rows,
+                                 hipStream_t stream);
 hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
                                 hipStream_t stream);
 

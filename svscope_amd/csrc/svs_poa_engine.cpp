@@ -348,10 +348,14 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   const size_t s_jobs = round_up(end, 256), off = s_jobs + nj * sizeof(PoaJob);
   if (off > A.h_in.cap) A.h_in.grow_keep(off, start);
   A.st_peak = std::max(A.st_peak, off);
-  if (off > 0xFFFFFFFFull) throw SvsError(SVS_E_UNSUPPORTED, "batch too large for 32-bit table offsets");
   char* hs = A.h_in.as<char>();
   // the device-derived tables of lite jobs: a region after the staging copy
-  // in the same device buffer, never copied from the host
+  // in the same device buffer, never copied from the host.  Byte offsets of
+  // every table from the buffer's start; pointers once the buffer is sized.
+  struct TabOff {
+    size_t rec, pstart, pred, pslot, col0, seq, info;
+  };
+  std::vector<TabOff> to(nj);
   size_t dev_end = round_up(off, 48);
   uint32_t prep_rows = 0;
   size_t n_prep = 0;
@@ -359,30 +363,29 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     PoaJob& J = la.jobs[k];
     const PoaTask& t = tasks[la.ids[k]];
     const size_t b = boff[k];
-    J.pstart_off = static_cast<uint32_t>((b + lay[k].pstart) / 4);
-    J.pred_off = static_cast<uint32_t>((b + lay[k].pred_row) / 4);
-    J.seq_off = static_cast<uint32_t>(b + lay[k].seq);
+    to[k].pstart = b + lay[k].pstart;
+    to[k].pred = b + lay[k].pred_row;
+    to[k].seq = b + lay[k].seq;
     if (t.rows_at == 2 && t.rows.lite) {
       const StripBlock o = strip_prep_out_layout(t.rows.n_rows, t.rows.n_edges);
-      J.info_off = static_cast<uint32_t>((b + lay[k].info) / 4);
-      J.row_off = static_cast<uint32_t>((dev_end + o.col0) / 12);
-      J.rec_off = static_cast<uint32_t>((dev_end + o.rec) / 16);
-      J.pslot_off = static_cast<uint32_t>((dev_end + o.pred_slot) / 4);
+      to[k].info = b + lay[k].info;
+      to[k].col0 = dev_end + o.col0;
+      to[k].rec = dev_end + o.rec;
+      to[k].pslot = dev_end + o.pred_slot;
       J.prep = 1u | (t.rows.slot_base << 1);
       dev_end += o.bytes;
       prep_rows = std::max(prep_rows, t.rows.n_rows);
       ++n_prep;
     } else {
-      J.row_off = static_cast<uint32_t>((b + lay[k].col0) / 12);
-      J.rec_off = static_cast<uint32_t>((b + lay[k].rec) / 16);
-      J.pslot_off = static_cast<uint32_t>((b + lay[k].pred_slot) / 4);
+      to[k].info = 0;
+      to[k].col0 = b + lay[k].col0;
+      to[k].rec = b + lay[k].rec;
+      to[k].pslot = b + lay[k].pred_slot;
       J.prep = 0;
     }
   }
-  if (dev_end / 16 > 0xFFFFFFFFull) throw SvsError(SVS_E_UNSUPPORTED, "batch too large for 32-bit table offsets");
   la.prep_jobs = n_prep;
   for (int x = 0; x < 4; ++x) la.gaps[x] = gaps[x];
-  std::memcpy(hs + s_jobs, la.jobs.data(), nj * sizeof(PoaJob));
   ctx->pool->parallel_for(nj, [&](size_t k) {
     const PoaTask& t = tasks[la.ids[k]];
     if (t.rows_at == 2) return;
@@ -410,6 +413,17 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   A.h_aln.ensure(n_aln * 8);
   A.h_alen.ensure(nj * 12);
   char* dg = A.d_in.as<char>();
+  for (size_t k = 0; k < nj; ++k) {
+    PoaJob& J = la.jobs[k];
+    J.rec = reinterpret_cast<const uint32_t*>(dg + to[k].rec);
+    J.pstart = reinterpret_cast<const uint32_t*>(dg + to[k].pstart);
+    J.pred = reinterpret_cast<const uint32_t*>(dg + to[k].pred);
+    J.pslot = reinterpret_cast<const uint32_t*>(dg + to[k].pslot);
+    J.col0 = reinterpret_cast<const int32_t*>(dg + to[k].col0);
+    J.seq = reinterpret_cast<const uint8_t*>(dg + to[k].seq);
+    J.info = reinterpret_cast<const uint32_t*>(dg + to[k].info);
+  }
+  std::memcpy(hs + s_jobs, la.jobs.data(), nj * sizeof(PoaJob));
   SVS_HIP(hipMemcpyAsync(dg, hs, off, hipMemcpyHostToDevice, A.copy_stream));
   SVS_HIP(hipEventRecord(A.h2d, A.copy_stream));
   SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
@@ -425,7 +439,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     if (own) SVS_HIP(hipStreamWaitEvent(ps, A.h2d, 0));
     SVS_HIP(hipEventRecord(A.evp, ps));
     SVS_HIP(launch_poa_strip_prep(reinterpret_cast<const PoaJob*>(dg + s_jobs), static_cast<int>(nj), score,
-                                  reinterpret_cast<uint8_t*>(dg), prep_rows, ps));
+                                  prep_rows, ps));
     SVS_HIP(hipEventRecord(A.evp1, ps));
     if (own) SVS_HIP(hipStreamWaitEvent(A.stream, A.evp1, 0));
     if (verify_prep()) {
@@ -438,13 +452,6 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
   pl.n_jobs = static_cast<int>(nj);
   pl.score = score;
-  // every table indexes the staging copy from its start (PoaJob offsets)
-  pl.rec = reinterpret_cast<const uint32_t*>(dg);
-  pl.row_pstart = reinterpret_cast<const uint32_t*>(dg);
-  pl.pred_row = reinterpret_cast<const uint32_t*>(dg);
-  pl.pred_slot = reinterpret_cast<const uint32_t*>(dg);
-  pl.col0 = reinterpret_cast<const int32_t*>(dg);
-  pl.seqs = reinterpret_cast<const uint8_t*>(dg);
   pl.tb = A.d_tb.as<uint16_t>();
   pl.bnd = A.d_pool.as<int32_t>();
   pl.pool = A.d_pool.as<int32_t>() + n_bnd;
@@ -496,7 +503,6 @@ uint8_t prep_task(PoaTask& t, const svs_poa_config& cfg, PoaArena* stage) {
 // SVS_POA_VERIFY_PREP=1: the device-completed tables of a finished launch
 // against the host's full export of the same graphs (still unfolded).
 void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks) {
-  const PoaArena& A = *la.arena;
   for (size_t k = 0; k < la.ids.size(); ++k) {
     const PoaJob& J = la.jobs[k];
     if (!(J.prep & 1u)) continue;
@@ -506,10 +512,9 @@ void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks) {
     const uint32_t V = J.n_rows, E = static_cast<uint32_t>(h.pred_row.size());
     std::vector<uint32_t> rec(4ull * V), ps(E);
     std::vector<int32_t> c0(3ull * V);
-    const char* d = A.d_in.as<char>();
-    SVS_HIP(hipMemcpy(rec.data(), d + 16ull * J.rec_off, rec.size() * 4, hipMemcpyDeviceToHost));
-    if (E) SVS_HIP(hipMemcpy(ps.data(), d + 4ull * J.pslot_off, ps.size() * 4, hipMemcpyDeviceToHost));
-    SVS_HIP(hipMemcpy(c0.data(), d + 12ull * J.row_off, c0.size() * 4, hipMemcpyDeviceToHost));
+    SVS_HIP(hipMemcpy(rec.data(), J.rec, rec.size() * 4, hipMemcpyDeviceToHost));
+    if (E) SVS_HIP(hipMemcpy(ps.data(), J.pslot, ps.size() * 4, hipMemcpyDeviceToHost));
+    SVS_HIP(hipMemcpy(c0.data(), J.col0, c0.size() * 4, hipMemcpyDeviceToHost));
     if (rec != h.rec || ps != h.pred_slot || c0 != h.col0 || h.n_slots != t.rows.n_slots)
       throw SvsError(SVS_E_INTERNAL, "device strip tables differ from the host export (job " + std::to_string(k) + ")");
   }
