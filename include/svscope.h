@@ -62,6 +62,9 @@ typedef struct svs_poa_stats {
   uint64_t prune_retries;   /* pruned alignments re-run (bound above the optimum) */
   double prep_ms;           /* device half of the row export (poa_strip_prep_kernel), HIP events */
   uint64_t prep_jobs;       /* alignments whose row tables the device completed */
+  double fold_ms;           /* device-resident graphs: graph update + sort + export + table
+                               completion (poa_fold.hip, poa_prep.hip) per launch, HIP events */
+  uint64_t fold_jobs;       /* alignments (and first reads) folded into device-resident graphs */
 } svs_poa_stats;
 
 /* One context per host thread; owns a HIP stream and device arenas. */

@@ -262,17 +262,19 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
     const uint32_t letter = act ? seq[pos] : 0u;
     uint32_t nn = kNone, cur = kNone;
     // kinds: matched (cur known), insertion (a new node), mismatch (resolved in order below)
-    bool ins = false, mis = false;
+    bool ins = false, mis = false, bad = false;
     if (act) {
       if (row < 0) {
         ins = true;
+      } else if (static_cast<uint32_t>(row) >= V0) {
+        bad = true;
       } else {
         nn = g.r2n[row];
-        if (nn >= V0) return fail(kFoldErrAln);
         if (g.base[nn] == letter) cur = nn;  // an old node's letter: never written by this kernel
         else mis = true;
       }
     }
+    if (ballot(bad)) return fail(kFoldErrAln);
     const uint64_t ins_m = ballot(ins);
     uint64_t mis_m = ballot(mis), creat_m = 0;
     uint32_t created = 0;
@@ -400,6 +402,8 @@ struct SortState {
   gu32* spill;     // global spill area
   uint32_t spilled;  // entries in the spill area (below the LDS part)
   uint32_t sp;       // entries in the LDS part
+  uint32_t spill_cap;  // entries the spill area holds
+  bool err;            // the stack outgrew its spill area
 };
 
 __device__ __forceinline__ bool bit_of(const uint32_t* plane, uint32_t v) { return (plane[v >> 5] >> (v & 31u)) & 1u; }
@@ -434,6 +438,10 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ in_off, const g
     if (S.sp == S.cap) {
       // spill the lower half of the LDS part
       const uint32_t half = S.cap / 2;
+      if (S.spilled + half > S.spill_cap) {
+        S.err = true;
+        return false;
+      }
       for (uint32_t k = lane; k < half; k += 64) S.spill[S.spilled + k] = S.st[k];
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
@@ -464,7 +472,10 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ in_off, const g
     __builtin_amdgcn_wave_barrier();
   };
   uint32_t root = 0;
-  while (root < V) {
+  // every examination pops or pushes: a bound on them stops a corrupt graph
+  uint64_t steps = 0;
+  const uint64_t max_steps = 64ull * (V + S.spill_cap) + 4096;
+  while (root < V && !S.err) {
     const uint32_t fw = uni(~S.done[root >> 5]) >> (root & 31u);
     if (fw == 0) {
       root = (root | 31u) + 1u;
@@ -473,7 +484,11 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ in_off, const g
     root += static_cast<uint32_t>(__builtin_ctz(fw));
     if (root >= V) break;
     push(root);
-    while (S.sp + S.spilled > 0) {
+    while (S.sp + S.spilled > 0 && !S.err) {
+      if (++steps > max_steps) {
+        S.err = true;
+        break;
+      }
       if (S.sp == 0) refill();
       const uint32_t cur = uni(S.st[S.sp - 1]);
       if (bit_of(S.done, cur)) {
@@ -518,7 +533,7 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ in_off, const g
     ++root;
   }
   *ncol_out = ncol;
-  return cnt == V ? kFoldOk : kFoldErrStack;
+  return (cnt == V && !S.err) ? kFoldOk : kFoldErrStack;
 }
 
 // Lite export of the next alignment's row tables (PoaGraph::export_strip_lite):
@@ -714,6 +729,8 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
   S.spill = g.stk;
   S.spilled = 0;
   S.sp = 0;
+  S.spill_cap = J.ce + 2 * J.cv + 64;
+  S.err = false;
   uint32_t ncol = 0;
   if (S.cap < 64) {
     if (lanei() == 0) res->status = kFoldErrStack;
@@ -774,6 +791,10 @@ __global__ __launch_bounds__(256) void poa_dgraph_move_kernel(const uint8_t* __r
   cp(A.pstart, B.pstart, 4ull * (V + 1));
   cp(A.pred, B.pred, 4ull * E);
   cp(A.info, B.info, 4ull * V);
+  // the next alignment's completed tables (a pruning retry reuses them)
+  cp(A.col0, B.col0, 12ull * V);
+  cp(A.rec, B.rec, 16ull * V);
+  cp(A.pslot, B.pslot, 4ull * E);
 }
 
 hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, hipStream_t stream) {

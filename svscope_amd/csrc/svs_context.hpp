@@ -108,11 +108,16 @@ struct PinnedBuf {
 struct PoaArena {
   DeviceBuf d_in, d_tb, d_pool, d_aln, d_alen;
   PinnedBuf h_in, h_aln, h_alen;
+  // device-resident graphs: the launch's job / fold descriptors and fold
+  // results, and the finished tasks' consensus + MSA rows
+  DeviceBuf d_desc, d_fin;
+  PinnedBuf h_desc, h_fin;
   hipStream_t stream = nullptr;       // kernel stream (shared, or this group's own)
   hipStream_t copy_stream = nullptr;  // this group's copies
   bool own = false;                   // stream is this group's, copies ride on it too
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr, h2d = nullptr;
   hipEvent_t evp = nullptr, evp1 = nullptr;  // around the launch's poa_strip_prep_kernel
+  hipEvent_t evf0 = nullptr, evf1 = nullptr;  // around the launch's fold kernels (device-resident graphs)
   hipStream_t prep_stream = nullptr;          // SVS_POA_PREP_STREAM=1: that kernel's own stream (made on first use)
   // Staging of the next launch's strip tables in h_in: the fold exports each
   // job's tables straight into a block claimed with an atomic bump (st_cur), so
@@ -138,18 +143,22 @@ struct PoaArena {
     SVS_HIP(hipEventCreate(&ev1));
     SVS_HIP(hipEventCreate(&evp));
     SVS_HIP(hipEventCreate(&evp1));
+    SVS_HIP(hipEventCreate(&evf0));
+    SVS_HIP(hipEventCreate(&evf1));
     SVS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
     SVS_HIP(hipEventCreateWithFlags(&h2d, hipEventDisableTiming));
   }
   ~PoaArena() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
-    for (DeviceBuf* b : {&d_in, &d_tb, &d_pool, &d_aln, &d_alen}) b->release();
-    for (PinnedBuf* b : {&h_in, &h_aln, &h_alen}) b->release();
+    for (DeviceBuf* b : {&d_in, &d_tb, &d_pool, &d_aln, &d_alen, &d_desc, &d_fin}) b->release();
+    for (PinnedBuf* b : {&h_in, &h_aln, &h_alen, &h_desc, &h_fin}) b->release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (evp) (void)hipEventDestroy(evp);
     if (evp1) (void)hipEventDestroy(evp1);
+    if (evf0) (void)hipEventDestroy(evf0);
+    if (evf1) (void)hipEventDestroy(evf1);
     if (prep_stream) {
       (void)hipStreamSynchronize(prep_stream);
       (void)hipStreamDestroy(prep_stream);
@@ -162,6 +171,8 @@ struct PoaArena {
   PoaArena& operator=(const PoaArena&) = delete;
 };
 
+class DevArena;
+
 }  // namespace svs
 
 struct svs_context {
@@ -173,6 +184,8 @@ struct svs_context {
   size_t device_budget = 0;  // bytes usable for traceback + row pool per launch
   // POA arenas, one per concurrently in-flight task group
   std::vector<std::unique_ptr<svs::PoaArena>> poa_arenas;
+  // blocks of the device-resident POA graphs (svs_devarena.hpp)
+  std::unique_ptr<svs::DevArena> dgraph_arena;
   // EM arenas
   svs::DeviceBuf d_em_in, d_em_ws, d_em_out, d_rng;
   svs::PinnedBuf h_em_in, h_em_out;

@@ -77,6 +77,12 @@ constexpr uint32_t kStripPrepMaxSlots = 64;    // pool slots of a prep job (free
 size_t strip_prep_scratch_words(uint32_t n_rows);  // after the job's in-edge slots (rounded to 4)
 hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore& score, uint32_t max_rows,
                                  hipStream_t stream);
+// Device-resident graphs (poa_fold.hip, poa_prep.hip; poa_dgraph.hpp).
+struct FoldJob;
+hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, hipStream_t stream);
+hipError_t launch_dgraph_prep(const FoldJob* jobs, int n_jobs, const PoaScore& score, hipStream_t stream);
+hipError_t launch_dgraph_move(const uint8_t* src, uint32_t cv0, uint32_t ce0, uint8_t* dst, uint32_t cv1, uint32_t ce1,
+                              uint32_t V, uint32_t E, uint32_t par, hipStream_t stream);
 hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
                                 hipStream_t stream);
 

@@ -7,6 +7,7 @@
 
 #include "../../include/svscope.h"
 #include "features.hpp"
+#include "poa_dgraph.hpp"
 #include "poa_graph.hpp"
 
 // EM results of one batch (opaque to ABI users).
@@ -55,6 +56,20 @@ struct PoaTask {
   uint8_t n_retries = 0;     // retried alignments of this task
   uint8_t read_retries = 0;  // retries of the current sequence
   uint32_t last_rows = 0;    // strip rows (64 columns) the last alignment computed
+
+  // device-resident graph (poa_dgraph.hpp, the default; SVS_POA_HOST_GRAPH=1
+  // keeps the graph in `graph` on the host instead)
+  DGraphRef dg;
+  uint8_t* d_static = nullptr;    // the task's reads (padded) + path offsets + node paths
+  size_t static_bytes = 0;
+  size_t dg_bytes = 0;            // the graph block's allocation size
+  std::vector<uint64_t> seq_at;   // byte offset of read k in d_static (its first base)
+  uint32_t* d_path_off = nullptr; // non-empty reads + 1 offsets into d_paths
+  uint32_t* d_paths = nullptr;
+  uint32_t n_paths = 0;           // non-empty reads folded so far
+  uint32_t last_nonempty = 0;     // index of the last non-empty read + 1
+  uint32_t n_slots_next = 0, max_preds_next = 0;  // the exported tables of the next read
+  bool tables_ok = false;         // rec / pslot / col0 / lite tables valid for seqs[next]
 
   std::string consensus;
   std::vector<std::string> msa;

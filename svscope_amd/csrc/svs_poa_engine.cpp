@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <chrono>
 #include <cstdio>
@@ -21,8 +22,10 @@
 #include <string>
 #include <vector>
 
+#include "poa_dgraph.hpp"
 #include "poa_graph.hpp"
 #include "svs_context.hpp"
+#include "svs_devarena.hpp"
 #include "svs_device.hpp"
 #include "svs_internal.hpp"
 
@@ -244,6 +247,28 @@ uint64_t job_bytes(const RowTables& tt, uint64_t L, const KernelEnv& ke) {
 
 void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks);
 
+// Waves per job of a strip launch: enough strip-pipeline waves to fill the
+// CUs, only for reads wide enough to give every wave several strips, and only
+// as many as the per-wave LDS pools of one workgroup fit; SVS_POA_WPJ overrides.
+int choose_wpj(size_t nj, uint32_t max_slots, uint32_t min_strips, bool lds_pool) {
+  int wpj = 1;
+  const char* we = std::getenv("SVS_POA_WPJ");
+  const int wenv = we ? std::atoi(we) : 0;
+  if ((wenv == 1 || wenv == 2 || wenv == 4 || wenv == 8) || (wenv == 16 && lds_pool)) {
+    wpj = wenv;
+  } else {
+    // ~6 waves per SIMD (1024 SIMDs); each wave keeps >= 6 strips.  Measured
+    // faster than keeping every workgroup resident (r01_v16): more waves per
+    // job shorten each job even when some workgroups start late.
+    while (wpj < 8 && static_cast<size_t>(wpj) * nj < 6144 && min_strips >= static_cast<uint32_t>(6 * wpj)) wpj *= 2;
+    // the small launches at the end of a batch: 16 waves per job (>= 2 strips
+    // each), or the few remaining jobs leave most SIMDs idle
+    if (lds_pool && wpj == 8 && nj < 512 && min_strips >= 32u) wpj = 16;
+  }
+  while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * kStripSlotBytes > kStripLdsBytes) wpj /= 2;
+  return wpj;
+}
+
 void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, const PoaScore& score,
                            svs_poa_stats& st, double& host_ms) {
   auto th0 = Clock::now();
@@ -266,31 +291,13 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   });
   for (size_t k = 0; k < nj; ++k) max_slots = std::max(max_slots, tasks[la.ids[k]].rows.n_slots);
   const bool lds_pool = max_slots <= kStripMaxLdsSlots && !strip_pool_forced_global();
-  const uint64_t slot_bytes = kStripSlotBytes;
   auto job_ls = [&](size_t len) -> uint32_t { return strip_ls(static_cast<uint32_t>(len)); };
-  // waves per job: enough strip-pipeline waves to fill the CUs, only for reads
-  // wide enough to give every wave several strips; SVS_POA_WPJ overrides
   uint32_t min_strips = 0xFFFFFFFFu;
   for (size_t k = 0; k < nj; ++k) {
     const uint32_t ls = job_ls(tasks[la.ids[k]].seqs[tasks[la.ids[k]].next].size());
     min_strips = std::min(min_strips, ls / 64);
   }
-  int wpj = 1;
-  const char* we = std::getenv("SVS_POA_WPJ");
-  const int wenv = we ? std::atoi(we) : 0;
-  if ((wenv == 1 || wenv == 2 || wenv == 4 || wenv == 8) || (wenv == 16 && lds_pool)) {
-    wpj = wenv;
-  } else {
-    // ~6 waves per SIMD (1024 SIMDs); each wave keeps >= 6 strips.  Measured
-    // faster than keeping every workgroup resident (r01_v16): more waves per
-    // job shorten each job even when some workgroups start late.
-    while (wpj < 8 && static_cast<size_t>(wpj) * nj < 6144 && min_strips >= static_cast<uint32_t>(6 * wpj)) wpj *= 2;
-    // the small launches at the end of a batch: 16 waves per job (>= 2 strips
-    // each), or the few remaining jobs leave most SIMDs idle
-    if (lds_pool && wpj == 8 && nj < 512 && min_strips >= 32u) wpj = 16;
-  }
-  // the per-wave LDS pools of one workgroup must fit the CU's LDS
-  while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * slot_bytes > kStripLdsBytes) wpj /= 2;
+  const int wpj = choose_wpj(nj, max_slots, min_strips, lds_pool);
   if (std::getenv("SVS_POA_DEBUG"))
     std::fprintf(stderr, "[svs] strip launch: %zu jobs, wpj %d, slots %u\n", nj, wpj, max_slots);
   const PruneEnv penv;
@@ -609,13 +616,44 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   g_trace.host("fold", la.gid, th0, la.ids.size());
 }
 
+// One launch of the device-resident graphs (poa_dgraph.hpp): DP jobs, then
+// the fold jobs (the DP jobs' alignments first, in the same order, then the
+// tasks whose first read lands on an empty graph).
+struct DevLaunch {
+  std::vector<uint32_t> dp_ids, fold_ids;
+  std::vector<PoaJob> jobs;
+  std::vector<FoldJob> folds;
+  std::vector<uint8_t> moved;                    // fold i's graph moved to a larger block
+  std::vector<std::pair<void*, size_t>> old_blocks;  // freed once the launch is done
+  std::vector<size_t> cons_off, msa_off;         // fold i's final outputs in the fin buffer
+  size_t n_aln = 0, s_fold = 0, s_res = 0, fin_bytes = 0;
+  int wpj = 0;
+  bool timed_dp = false;
+};
+
 // Task group: a disjoint subset of the active tasks with its own arena.
 struct Group {
   std::vector<uint32_t> active;
   Launch la;
+  DevLaunch dl;
+  std::vector<uint32_t> completed;  // device graphs finished by the last launch
   bool pending = false;
   PoaArena* arena = nullptr;
 };
+
+// Device-resident graphs unless SVS_POA_HOST_GRAPH=1 (or a consensus with a
+// minimum coverage, which only the host graph implements).
+bool device_graphs(const svs_poa_config& c) {
+  const char* e = std::getenv("SVS_POA_HOST_GRAPH");
+  return !(e && std::string(e) == "1") && c.min_coverage <= 0;
+}
+// SVS_POA_VERIFY_GRAPH=1: a host PoaGraph of every task replays the device's
+// folds; the device's rank order, row tables, consensus and MSA are checked
+// against it after every fold (tests).
+bool verify_graph() {
+  const char* e = std::getenv("SVS_POA_VERIFY_GRAPH");
+  return e && std::string(e) == "1";
+}
 
 size_t active_jobs_per_group() {
   if (const char* e = std::getenv("SVS_POA_ACTIVE_JOBS")) {
@@ -642,9 +680,17 @@ struct PoaScheduler::Impl {
   std::vector<uint32_t> free_ids;  // released task slots, reused by add()
   bool queue_dirty = false;      // tasks were queued since the last sort
 
+  bool dev;      // device-resident graphs (poa_dgraph.hpp)
+  bool verify;   // SVS_POA_VERIFY_GRAPH
+  DevArena* darena = nullptr;
+
   Impl(svs_context* c, const svs_poa_config& k, svs_poa_stats& s)
       : ctx(c), cfg(k), score{k.m, k.n, k.g, k.e, k.q, k.c}, st(s), cap(active_jobs_per_group()),
-        budget(c->device_budget / 2) {
+        budget(c->device_budget / 2), dev(device_graphs(k)), verify(verify_graph()) {
+    if (dev) {
+      if (!ctx->dgraph_arena) ctx->dgraph_arena.reset(new DevArena());
+      darena = ctx->dgraph_arena.get();
+    }
     // Both groups' kernels alternate on the context's one stream.
     // SVS_POA_STREAMS=2 gives each group a stream of its own so the next
     // launch can overlap the other's tail: measured no faster (196.9 vs 202.0
@@ -682,8 +728,525 @@ struct PoaScheduler::Impl {
     }
   }
 
+  // ------------------------------------------------ device-resident graphs
+  // A task's reads (each as the DP kernel reads it: a zero pad byte, the read,
+  // zeros up to ls + 64), the path offsets of its non-empty reads and room for
+  // their node paths: one block, uploaded once (from the launch's pinned
+  // staging, `up`), read by every DP and fold of the task.
+  void activate_dev(PoaTask& t, std::vector<char>& up, std::vector<std::pair<size_t, PoaTask*>>& uploads) {
+    const size_t n = t.seqs.size();
+    t.seq_at.assign(n, 0);
+    size_t o = 64;
+    uint32_t n_ne = 0;
+    uint64_t path_total = 0;
+    t.last_nonempty = 0;
+    for (size_t k = 0; k < n; ++k) {
+      const uint32_t L = static_cast<uint32_t>(t.seqs[k].size());
+      t.seq_at[k] = o;
+      o = round_up(o + strip_ls(L) + 64, 64) + 64;
+      if (L) {
+        ++n_ne;
+        path_total += L;
+        t.last_nonempty = static_cast<uint32_t>(k) + 1;
+      }
+    }
+    const size_t po = round_up(o, 64), pa = round_up(po + 4ull * (n_ne + 1), 64);
+    t.static_bytes = pa + 4 * path_total + 64;
+    t.d_static = static_cast<uint8_t*>(darena->alloc(t.static_bytes));
+    t.d_path_off = reinterpret_cast<uint32_t*>(t.d_static + po);
+    t.d_paths = reinterpret_cast<uint32_t*>(t.d_static + pa);
+    // host image of the reads + path offsets (the paths are written by the folds)
+    const size_t at = up.size();
+    up.resize(at + pa);
+    char* h = up.data() + at;
+    std::memset(h, 0, pa);
+    for (size_t k = 0; k < n; ++k)
+      if (!t.seqs[k].empty()) std::memcpy(h + t.seq_at[k], t.seqs[k].data(), t.seqs[k].size());
+    uint32_t* poff = reinterpret_cast<uint32_t*>(h + po);
+    uint32_t acc = 0, i = 0;
+    for (size_t k = 0; k < n; ++k)
+      if (!t.seqs[k].empty()) {
+        poff[i++] = acc;
+        acc += static_cast<uint32_t>(t.seqs[k].size());
+      }
+    poff[i] = acc;
+    uploads.emplace_back(at, &t);
+    t.n_paths = 0;
+    t.dg = DGraphRef{};
+    t.tables_ok = false;
+  }
+
+  void release_dev(PoaTask& t) {
+    if (t.d_static) darena->free(t.d_static, t.static_bytes);
+    if (t.dg.blk) darena->free(t.dg.blk, t.dg_bytes);
+    t.d_static = nullptr;
+    t.dg.blk = nullptr;
+  }
+
+  // Prepares the group's next device launch, completing the tasks with nothing
+  // left to align, and launches it.
+  void advance_dev(Group& g, const DoneFn& done) {
+    for (;;) {
+      if (!g.completed.empty()) {
+        const auto td0 = Clock::now();
+        done(g.completed);
+        for (uint32_t id : g.completed) graves.push_back(id);
+        g_trace.host("done", gid(g), td0, g.completed.size());
+        g.completed.clear();
+      }
+      refill(g);
+      if (g.active.empty()) return;
+      const auto th0 = Clock::now();
+      std::vector<uint32_t> dp, chain, keep, fin;
+      for (uint32_t id : g.active) {
+        PoaTask& t = tasks[id];
+        while (t.next < t.seqs.size() && t.seqs[t.next].empty()) ++t.next;
+        if (t.next >= t.seqs.size()) {
+          // every read empty (a finished graph completes in finish_dev)
+          t.consensus.clear();
+          t.msa.clear();
+          fin.push_back(id);
+          continue;
+        }
+        keep.push_back(id);
+        if (t.dg.V == 0) chain.push_back(id);
+        else dp.push_back(id);
+      }
+      g.active = keep;
+      host_ms += ms_since(th0);
+      if (!fin.empty()) {
+        for (uint32_t id : fin) release_dev(tasks[id]);
+        g.completed = fin;
+        continue;
+      }
+      // the launch's DP jobs within the group's device budget (longest first;
+      // the rest wait for the next launch)
+      order_by_cost(dp);
+      const KernelEnv ke;
+      uint64_t total = 0;
+      size_t fit = 0;
+      for (; fit < dp.size(); ++fit) {
+        const PoaTask& t = tasks[dp[fit]];
+        const uint64_t b = job_bytes_dev(t, ke);
+        if (fit > 0 && total + b > budget) break;
+        total += b;
+      }
+      dp.resize(fit);
+      const auto tp0 = Clock::now();
+      pack_and_launch_dev(g, dp, chain);
+      g_trace.host("pack", gid(g), tp0, dp.size() + chain.size());
+      g.pending = true;
+      return;
+    }
+  }
+
+  uint64_t job_bytes_dev(const PoaTask& t, const KernelEnv& ke) const {
+    const uint64_t L = t.seqs[t.next].size(), ls = strip_ls(static_cast<uint32_t>(L)), V = t.dg.V;
+    const uint64_t pool = (t.n_slots_next > kStripMaxLdsSlots || ke.global_pool)
+                              ? 8ull * round_up(static_cast<uint64_t>(t.n_slots_next) * 97, 64) * 4 : 0;
+    return V * ls * 2 + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
+  }
+
+  void pack_and_launch_dev(Group& g, const std::vector<uint32_t>& dp, const std::vector<uint32_t>& chain) {
+    auto th0 = Clock::now();
+    PoaArena& A = *g.arena;
+    DevLaunch& D = g.dl;
+    D = DevLaunch{};
+    D.dp_ids = dp;
+    D.fold_ids = dp;
+    D.fold_ids.insert(D.fold_ids.end(), chain.begin(), chain.end());
+    const size_t nj = dp.size(), nf = D.fold_ids.size();
+    // reads of the tasks that start with this launch
+    std::vector<char> up;
+    std::vector<std::pair<size_t, PoaTask*>> uploads;
+    for (uint32_t id : D.fold_ids)
+      if (!tasks[id].d_static) activate_dev(tasks[id], up, uploads);
+    // DP jobs: the tables the last fold exported, in the task's block
+    D.jobs.assign(nj, PoaJob{});
+    uint64_t n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
+    uint32_t max_slots = 1, min_strips = 0xFFFFFFFFu;
+    bool any_prune = false;
+    for (uint32_t id : dp) {
+      const PoaTask& t = tasks[id];
+      if (!t.tables_ok) throw SvsError(SVS_E_INTERNAL, "device graph: no row tables for the next read");
+      if (t.max_preds_next > 31)
+        throw SvsError(SVS_E_UNSUPPORTED, "a graph node has more than 31 in-edges (traceback code limit)");
+      max_slots = std::max(max_slots, t.n_slots_next);
+      min_strips = std::min(min_strips, strip_ls(static_cast<uint32_t>(t.seqs[t.next].size())) / 64);
+    }
+    const bool lds_pool = max_slots <= kStripMaxLdsSlots && !strip_pool_forced_global();
+    const int wpj = nj ? choose_wpj(nj, max_slots, min_strips, lds_pool) : 1;
+    const PruneEnv penv;
+    for (size_t k = 0; k < nj; ++k) {
+      const PoaTask& t = tasks[dp[k]];
+      PoaJob& J = D.jobs[k];
+      const DGraphLayout L = dgraph_layout(t.dg.cv, t.dg.ce);
+      uint8_t* b = t.dg.blk;
+      J.rec = reinterpret_cast<const uint32_t*>(b + L.rec);
+      J.pstart = reinterpret_cast<const uint32_t*>(b + L.pstart);
+      J.pred = reinterpret_cast<const uint32_t*>(b + L.pred);
+      J.pslot = reinterpret_cast<const uint32_t*>(b + L.pslot);
+      J.col0 = reinterpret_cast<const int32_t*>(b + L.col0);
+      J.seq = t.d_static + t.seq_at[t.next];
+      J.info = nullptr;
+      J.prep = 0;
+      J.n_rows = t.dg.V;
+      J.len = static_cast<uint32_t>(t.seqs[t.next].size());
+      J.ls = strip_ls(J.len);
+      J.n_slots = t.n_slots_next;
+      if (static_cast<uint64_t>(J.n_rows) * J.ls > 0x7FFFFFFFull)
+        throw SvsError(SVS_E_UNSUPPORTED, "a job's traceback matrix exceeds 2^31 cells");
+      J.tb_off = n_tb;
+      J.bnd_off = n_bnd;
+      J.pool_off = n_pool;
+      J.aln_off = n_aln;
+      J.lb = prune_bound(t, score, J.n_rows, J.len, penv);
+      if (J.n_slots > 31) J.lb = kNoPrune;
+      any_prune = any_prune || J.lb != kNoPrune;
+      n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
+      n_bnd += round_up(round_up(J.n_rows, 8) * (J.ls / 64) * 4, 64);
+      if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 97, 64);
+      n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
+      st.dp_cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);
+    }
+    if (any_prune)
+      for (PoaJob& J : D.jobs)
+        if (J.lb == kNoPrune) J.lb = kPruneAll;
+    D.n_aln = n_aln;
+    D.wpj = wpj;
+    A.d_tb.ensure(n_tb * 2 + 4096, ctx->device_budget / 2);
+    A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096);
+    A.d_aln.ensure(n_aln * 8 + 64);
+    A.d_alen.ensure(nj * 12 + 64);
+    // fold jobs, growing blocks that could not hold this fold
+    D.folds.assign(nf, FoldJob{});
+    D.moved.assign(nf, 0);
+    D.cons_off.assign(nf, 0);
+    D.msa_off.assign(nf, 0);
+    size_t fin = 0;
+    std::vector<std::array<uint64_t, 9>> moves;  // src, cv0, ce0, dst, cv1, ce1, V, E, par
+    for (size_t i = 0; i < nf; ++i) {
+      PoaTask& t = tasks[D.fold_ids[i]];
+      FoldJob& F = D.folds[i];
+      const uint32_t len = static_cast<uint32_t>(t.seqs[t.next].size());
+      const bool chain_job = i >= nj;
+      if (!t.dg.blk || t.dg.V + len > t.dg.cv || t.dg.E + len + 1 > t.dg.ce) {
+        const uint32_t cv1 = std::max<uint32_t>(2 * t.dg.cv, t.dg.V + 2 * len + 4096);
+        const uint32_t ce1 = std::max<uint32_t>(2 * t.dg.ce, t.dg.E + 3 * len + 4096);
+        const size_t bytes = dgraph_layout(cv1, ce1).bytes;
+        uint8_t* nb = static_cast<uint8_t*>(darena->alloc(bytes));
+        if (t.dg.blk) {
+          moves.push_back({reinterpret_cast<uint64_t>(t.dg.blk), t.dg.cv, t.dg.ce, reinterpret_cast<uint64_t>(nb), cv1,
+                           ce1, t.dg.V, t.dg.E, t.dg.par});
+          D.old_blocks.emplace_back(t.dg.blk, t.dg_bytes);
+          D.moved[i] = 1;
+        }
+        t.dg.blk = nb;
+        t.dg.cv = cv1;
+        t.dg.ce = ce1;
+        t.dg_bytes = bytes;
+      }
+      F.blk = t.dg.blk;
+      F.cv = t.dg.cv;
+      F.ce = t.dg.ce;
+      F.V = t.dg.V;
+      F.E = t.dg.E;
+      F.par = t.dg.par;
+      const bool last = t.next + 1 >= t.last_nonempty;
+      F.flags = (chain_job ? kFoldChain : 0u) | (last ? (kFoldFinal | (t.genmsa ? kFoldMsa : 0u)) : kFoldExport);
+      F.seq = t.d_static + t.seq_at[t.next];
+      F.len = len;
+      F.n_paths = t.n_paths;
+      F.paths = t.d_paths;
+      F.path_off = t.d_path_off;
+      if (last) {
+        const size_t bound = t.dg.V + len;
+        D.cons_off[i] = fin;
+        fin = round_up(fin + bound, 64);
+        F.msa_stride = static_cast<uint32_t>(round_up(bound, 64));
+        if (t.genmsa) {
+          D.msa_off[i] = fin;
+          fin += static_cast<size_t>(t.n_paths + 1) * F.msa_stride;
+        }
+      }
+    }
+    D.fin_bytes = fin;
+    // descriptors: DP jobs, fold jobs, fold results; then the new tasks' reads
+    const size_t s_fold = round_up(nj * sizeof(PoaJob), 256);
+    const size_t s_res = round_up(s_fold + nf * sizeof(FoldJob), 256);
+    const size_t s_up = round_up(s_res + nf * sizeof(FoldResult), 256);
+    const size_t total = s_up + up.size();
+    D.s_fold = s_fold;
+    D.s_res = s_res;
+    A.h_desc.ensure(total);
+    A.d_desc.ensure(total);
+    A.d_fin.ensure(fin + 64);
+    A.h_fin.ensure(fin + 64);
+    char* dd = A.d_desc.as<char>();
+    for (size_t i = 0; i < nf; ++i) {
+      FoldJob& F = D.folds[i];
+      F.result = reinterpret_cast<FoldResult*>(dd + s_res) + i;
+      if (i < nj) {
+        F.aln = A.d_aln.as<int32_t>() + 2 * D.jobs[i].aln_off;
+        F.aln_status = A.d_alen.as<int32_t>() + i;
+      }
+      if (F.flags & kFoldFinal) {
+        F.cons_out = A.d_fin.as<char>() + D.cons_off[i];
+        F.msa_out = A.d_fin.as<char>() + D.msa_off[i];
+      }
+    }
+    char* hd = A.h_desc.as<char>();
+    if (nj) std::memcpy(hd, D.jobs.data(), nj * sizeof(PoaJob));
+    std::memcpy(hd + s_fold, D.folds.data(), nf * sizeof(FoldJob));
+    std::memset(hd + s_res, 0, nf * sizeof(FoldResult));
+    if (!up.empty()) std::memcpy(hd + s_up, up.data(), up.size());
+    host_ms += ms_since(th0);
+
+    hipStream_t side = A.copy_stream;
+    SVS_HIP(hipMemcpyAsync(dd, hd, total, hipMemcpyHostToDevice, side));
+    for (const auto& u : uploads) {
+      PoaTask& t = *u.second;
+      const size_t bytes = static_cast<size_t>(reinterpret_cast<uint8_t*>(t.d_paths) - t.d_static);
+      SVS_HIP(hipMemcpyAsync(t.d_static, dd + s_up + u.first, bytes, hipMemcpyDeviceToDevice, side));
+    }
+    for (const auto& m : moves)
+      SVS_HIP(launch_dgraph_move(reinterpret_cast<const uint8_t*>(m[0]), static_cast<uint32_t>(m[1]),
+                                 static_cast<uint32_t>(m[2]), reinterpret_cast<uint8_t*>(m[3]),
+                                 static_cast<uint32_t>(m[4]), static_cast<uint32_t>(m[5]), static_cast<uint32_t>(m[6]),
+                                 static_cast<uint32_t>(m[7]), static_cast<uint32_t>(m[8]), side));
+    SVS_HIP(hipEventRecord(A.h2d, side));
+    D.timed_dp = nj > 0;
+    if (nj) {
+      PoaLaunch pl{};
+      pl.jobs = reinterpret_cast<const PoaJob*>(dd);
+      pl.n_jobs = static_cast<int>(nj);
+      pl.score = score;
+      pl.tb = A.d_tb.as<uint16_t>();
+      pl.bnd = A.d_pool.as<int32_t>();
+      pl.pool = A.d_pool.as<int32_t>() + n_bnd;
+      pl.aln = A.d_aln.as<int32_t>();
+      pl.aln_len = A.d_alen.as<int32_t>();
+      pl.lds_slots = lds_pool ? max_slots : 0;
+      pl.prune = any_prune;
+      pl.waves_per_job = wpj;
+      SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
+      SVS_HIP(hipEventRecord(A.ev0, A.stream));
+      SVS_HIP(launch_poa_strip(pl, A.stream));
+      SVS_HIP(hipEventRecord(A.ev1, A.stream));
+      SVS_HIP(hipStreamWaitEvent(side, A.ev1, 0));
+    }
+    // graph update, sort, export and table completion beside the other group's DP
+    uint32_t lds_words = 0;
+    for (const FoldJob& F : D.folds) {
+      const uint32_t W = (F.V + F.len + 31) / 32;
+      lds_words = std::max(lds_words, 2 * W);
+    }
+    lds_words += 2048;  // the DFS stack's LDS part
+    SVS_HIP(hipEventRecord(A.evf0, side));
+    SVS_HIP(launch_poa_fold(reinterpret_cast<const FoldJob*>(dd + s_fold), static_cast<int>(nf), lds_words, side));
+    SVS_HIP(launch_dgraph_prep(reinterpret_cast<const FoldJob*>(dd + s_fold), static_cast<int>(nf), score, side));
+    SVS_HIP(hipEventRecord(A.evf1, side));
+    A.h_alen.ensure(nj * 12 + 64);
+    if (nj) SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, A.d_alen.ptr, nj * 12, hipMemcpyDeviceToHost, side));
+    SVS_HIP(hipMemcpyAsync(hd + s_res, dd + s_res, nf * sizeof(FoldResult), hipMemcpyDeviceToHost, side));
+    if (fin) SVS_HIP(hipMemcpyAsync(A.h_fin.ptr, A.d_fin.ptr, fin, hipMemcpyDeviceToHost, side));
+    if (verify) {
+      A.h_aln.ensure(n_aln * 8 + 64);
+      if (nj) SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, A.d_aln.ptr, n_aln * 8, hipMemcpyDeviceToHost, side));
+    }
+    SVS_HIP(hipEventRecord(A.done, side));
+    st.launches += nj ? 1 : 0;
+    st.alignments += nj;
+    st.tb_bytes += n_tb * 2;
+    st.pool_bytes += (n_bnd + n_pool) * 4;
+    st.h2d_bytes += total;
+    st.d2h_bytes += nj * 12 + nf * sizeof(FoldResult) + fin;
+    st.fold_jobs += nf;
+  }
+
+  // Waits for the group's device launch and takes its results: DP statistics
+  // and retries, the folded graphs' new counts, and the finished tasks.
+  void finish_dev(Group& g) {
+    PoaArena& A = *g.arena;
+    DevLaunch& D = g.dl;
+    const auto tw0 = Clock::now();
+    for (;;) {
+      const hipError_t q = hipEventQuery(A.done);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) SVS_HIP(q);
+      if (!reap()) break;
+    }
+    SVS_HIP(hipEventSynchronize(A.done));
+    st.gpu_wait_ms += ms_since(tw0);
+    const size_t nj = D.dp_ids.size(), nf = D.fold_ids.size();
+    if (D.timed_dp) {
+      float ms = 0.f;
+      SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
+      st.kernel_ms += ms;
+    }
+    {
+      float ms = 0.f;
+      SVS_HIP(hipEventElapsedTime(&ms, A.evf0, A.evf1));
+      st.fold_ms += ms;
+    }
+    if (g_trace.f) {
+      uint64_t cells = 0;
+      for (const PoaJob& J : D.jobs) cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);
+      g_trace.host("wait", gid(g), tw0, nf);
+      if (D.timed_dp) g_trace.kernel(gid(g), A.ev0, A.ev1, nj, D.wpj, cells);
+    }
+    const auto th0 = Clock::now();
+    const int32_t* alen = A.h_alen.as<int32_t>();
+    const FoldResult* res = reinterpret_cast<const FoldResult*>(A.h_desc.as<char>() + D.s_res);
+    for (size_t k = 0; k < nj; ++k) {
+      PoaTask& t = tasks[D.dp_ids[k]];
+      st.cells_computed += 64ull * static_cast<uint32_t>(alen[2 * nj + k]);
+      t.last_rows = static_cast<uint32_t>(alen[2 * nj + k]);
+      const int32_t n = alen[k];
+      if (n == kPruneRetry) {
+        st.prune_retries += 1;
+        t.retry = true;
+        t.n_retries += 1;
+        t.read_retries += 1;
+        continue;
+      }
+      if (n < 0) throw SvsError(SVS_E_INTERNAL, "GPU traceback reported an inconsistent path");
+      const uint32_t len = D.jobs[k].len;
+      if (!t.retry && len > 0) {
+        t.rate = static_cast<double>(alen[nj + k]) / len;
+        t.have_rate = true;
+      }
+      t.retry = false;
+      t.read_retries = 0;
+    }
+    for (auto& b : D.old_blocks) darena->free(b.first, b.second);
+    D.old_blocks.clear();
+    for (size_t i = 0; i < nf; ++i) {
+      PoaTask& t = tasks[D.fold_ids[i]];
+      const FoldResult& r = res[i];
+      const FoldJob& F = D.folds[i];
+      if (r.status == kFoldSkipped) continue;  // a pruning retry: graph and tables unchanged
+      if (r.status != kFoldOk)
+        throw SvsError(SVS_E_INTERNAL, "device POA graph fold failed (status " + std::to_string(r.status) + ")");
+      if (verify) verify_fold(g, i, r);
+      t.dg.V = r.V;
+      t.dg.E = r.E;
+      t.dg.par ^= 1u;
+      t.dg.ncol = r.ncol;
+      t.n_paths += 1;
+      t.next += 1;
+      if (F.flags & kFoldExport) {
+        t.n_slots_next = r.n_slots;
+        t.max_preds_next = r.max_preds;
+        // the device planner's limits (poa_prep.hip); beyond them the tables are incomplete
+        if (r.V > kStripPrepMaxRows || r.n_slots > kStripPrepMaxSlots)
+          throw SvsError(SVS_E_UNSUPPORTED, "device POA graph beyond the row-table planner's limits");
+        t.tables_ok = true;
+      }
+      if (F.flags & kFoldFinal) {
+        const char* h = A.h_fin.as<char>();
+        const uint32_t nc = r.pad0;
+        t.consensus.assign(h + D.cons_off[i], nc);
+        std::reverse(t.consensus.begin(), t.consensus.end());
+        t.msa.clear();
+        if (F.flags & kFoldMsa) {
+          t.msa.reserve(t.n_paths);
+          for (uint32_t s = 0; s < t.n_paths; ++s)
+            t.msa.emplace_back(h + D.msa_off[i] + static_cast<size_t>(s) * F.msa_stride, r.ncol);
+        }
+        if (verify) verify_final(t);
+        release_dev(t);
+        g.completed.push_back(D.fold_ids[i]);
+      }
+    }
+    if (!g.completed.empty()) {
+      std::vector<uint32_t> keep;
+      keep.reserve(g.active.size());
+      std::vector<uint8_t> gone(tasks.size(), 0);
+      for (uint32_t id : g.completed) gone[id] = 1;
+      for (uint32_t id : g.active)
+        if (!gone[id]) keep.push_back(id);
+      g.active.swap(keep);
+    }
+    host_ms += ms_since(th0);
+    g_trace.host("fold", gid(g), th0, nf);
+  }
+
+  // SVS_POA_VERIFY_GRAPH: replay fold i on the task's host graph and compare
+  // the device's rank order and exported tables with the host's.
+  void verify_fold(Group& g, size_t i, const FoldResult& r) {
+    PoaArena& A = *g.arena;
+    DevLaunch& D = g.dl;
+    PoaTask& t = tasks[D.fold_ids[i]];
+    const FoldJob& F = D.folds[i];
+    const std::string& s = t.seqs[t.next];
+    if (F.flags & kFoldChain) {
+      t.graph.add_alignment_nodes({}, s);
+    } else {
+      const int32_t n = A.h_alen.as<int32_t>()[i];
+      const int32_t* p = A.h_aln.as<int32_t>() + 2 * D.jobs[i].aln_off;
+      std::vector<int32_t> fwd(2 * static_cast<size_t>(n));
+      for (int32_t x = 0; x < n; ++x) {
+        fwd[2 * x] = p[2 * (n - 1 - x)];
+        fwd[2 * x + 1] = p[2 * (n - 1 - x) + 1];
+      }
+      t.graph.add_alignment_ranks(fwd, s);
+    }
+    const uint32_t V = t.graph.num_nodes(), E = t.graph.num_edges();
+    auto fail = [&](const std::string& what) {
+      throw SvsError(SVS_E_INTERNAL, "device graph differs from the host graph after fold (" + what + "), read " +
+                                         std::to_string(t.next) + ", V " + std::to_string(V));
+    };
+    if (r.V != V || r.E != E) fail("node/edge counts " + std::to_string(r.V) + "/" + std::to_string(r.E));
+    const DGraphLayout L = dgraph_layout(F.cv, F.ce);
+    std::vector<uint32_t> r2n(V);
+    SVS_HIP(hipMemcpy(r2n.data(), F.blk + L.r2n, 4ull * V, hipMemcpyDeviceToHost));
+    if (r2n != t.graph.rank_to_node()) fail("rank order");
+    if (F.flags & kFoldExport) {
+      RowTables h;
+      std::vector<uint32_t> ps(V + 1), pr(E), inf(V);
+      const StripLiteDst dst{ps.data(), pr.data(), inf.data()};
+      t.graph.export_strip_lite(&h, &dst);
+      std::vector<uint32_t> dps(V + 1), dpr(E), dinf(V);
+      SVS_HIP(hipMemcpy(dps.data(), F.blk + L.pstart, 4ull * (V + 1), hipMemcpyDeviceToHost));
+      if (E) SVS_HIP(hipMemcpy(dpr.data(), F.blk + L.pred, 4ull * E, hipMemcpyDeviceToHost));
+      SVS_HIP(hipMemcpy(dinf.data(), F.blk + L.info, 4ull * V, hipMemcpyDeviceToHost));
+      if (dps != ps) fail("pstart");
+      if (dpr != pr) fail("in-edge rows");
+      if (dinf != inf) fail("row words");
+      if (h.n_slots != r.n_slots) fail("slot count " + std::to_string(r.n_slots) + " vs " + std::to_string(h.n_slots));
+      if (h.max_preds != r.max_preds) fail("max in-degree");
+      // the completed tables against the host's full export
+      if (r.V <= kStripPrepMaxRows && r.n_slots <= kStripPrepMaxSlots && r.max_preds <= 31) {
+        RowTables full;
+        const int32_t gaps[4] = {score.g, score.e, score.q, score.c};
+        t.graph.export_strip_rows(&full, gaps);
+        std::vector<uint32_t> rec(4ull * V), psl(E);
+        std::vector<int32_t> c0(3ull * V);
+        SVS_HIP(hipMemcpy(rec.data(), F.blk + L.rec, rec.size() * 4, hipMemcpyDeviceToHost));
+        if (E) SVS_HIP(hipMemcpy(psl.data(), F.blk + L.pslot, psl.size() * 4, hipMemcpyDeviceToHost));
+        SVS_HIP(hipMemcpy(c0.data(), F.blk + L.col0, c0.size() * 4, hipMemcpyDeviceToHost));
+        if (rec != full.rec) fail("row records");
+        if (psl != full.pred_slot) fail("in-edge slots");
+        if (c0 != full.col0) fail("column 0");
+      }
+    }
+  }
+
+  void verify_final(PoaTask& t) {
+    const std::string cons = t.graph.consensus(cfg.min_coverage);
+    if (cons != t.consensus)
+      throw SvsError(SVS_E_INTERNAL, "device consensus differs from the host graph's (" +
+                                         std::to_string(t.consensus.size()) + " vs " + std::to_string(cons.size()) + ")");
+    if (t.genmsa && t.graph.msa() != t.msa) throw SvsError(SVS_E_INTERNAL, "device MSA differs from the host graph's");
+  }
+
   // Prepares the group's next launch (or completes its tasks) and launches it.
   void advance(Group& g, const DoneFn& done) {
+    if (dev) {
+      advance_dev(g, done);
+      return;
+    }
     std::vector<uint8_t> needs;
     for (;;) {
       refill(g);
@@ -764,7 +1327,8 @@ struct PoaScheduler::Impl {
     std::vector<std::pair<uint64_t, uint32_t>> c(ids.size());
     for (size_t i = 0; i < ids.size(); ++i) {
       const PoaTask& t = tasks[ids[i]];
-      const uint64_t full = static_cast<uint64_t>(t.rows.n_rows) * ((t.seqs[t.next].size() + 64) / 64);
+      const uint64_t rows = dev ? t.dg.V : t.rows.n_rows;
+      const uint64_t full = rows * ((t.seqs[t.next].size() + 64) / 64);
       c[i] = {t.last_rows == 0 || t.retry ? full : t.last_rows, ids[i]};
     }
     std::stable_sort(c.begin(), c.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
@@ -798,7 +1362,8 @@ struct PoaScheduler::Impl {
       bool progressed = false;
       for (Group& g : groups) {
         if (!g.pending) continue;
-        finish(ctx, g.la, tasks, st, host_ms, cfg, [this] { return reap(); });
+        if (dev) finish_dev(g);
+        else finish(ctx, g.la, tasks, st, host_ms, cfg, [this] { return reap(); });
         g.pending = false;
         advance(g, done);
         progressed = true;
@@ -807,7 +1372,7 @@ struct PoaScheduler::Impl {
       const bool outside = poll(false);
       g_trace.host("poll", -1, tq0, 0);
       for (Group& g : groups)
-        if (!g.pending && !queue.empty()) advance(g, done);
+        if (!g.pending && (!queue.empty() || !g.completed.empty() || (dev && !g.active.empty()))) advance(g, done);
       const bool busy = groups[0].pending || groups[1].pending;
       if (progressed || busy) continue;
       if (outside) {

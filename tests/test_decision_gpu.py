@@ -198,3 +198,31 @@ def test_decision_session_bad_batch_is_isolated():
     with pytest.raises(_abi.SvsError, match="already waited"):
         _abi.check(s.lib.svs_decision_session_wait(s.handle, ctypes.c_int64(t2), ctypes_ptr()), "wait")
     s.close()
+
+
+def test_bench_windows_match_oracle_digests():
+    """bench.py's own workload pinned against the CPU oracle: its first 256
+    timed windows (config 3: 64 reads x 3 kb, window ids 0..255) through the
+    streaming session exactly as bench.py runs them (batches of 64, 4 in
+    flight), record for record against the SHA-256 of the oracle's Raw.bed
+    line (tests/golden/bench_config3_digests.json, gen_bench_goldens.py)."""
+    import hashlib
+    from collections import deque
+    from svscope_amd import synth
+    from svscope_amd.decision_maker import DecisionSession
+    from svscope_amd.local_graph import _window, record_line
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_config3_digests.json")))
+    rows = [synth.make_window(w, 64, 3000) for w in range(gold["n"])]
+    got = []
+    with DecisionSession() as s:
+        q = deque()
+        for k in range(0, len(rows), 64):
+            q.append(s.submit([_window(r) for r in rows[k:k + 64]]))
+            if len(q) >= 4:
+                got += s.wait(q.popleft())
+        while q:
+            got += s.wait(q.popleft())
+    digests = [hashlib.sha256(record_line(r).encode()).hexdigest() for r in got]
+    bad = [k for k, (a, b) in enumerate(zip(digests, gold["digests"])) if a != b]
+    assert not bad, f"{len(bad)} windows differ from the oracle, first {bad[:8]}"
+    assert hashlib.sha256("\n".join(digests).encode()).hexdigest() == gold["all"]

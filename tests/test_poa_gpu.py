@@ -100,12 +100,14 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_PRUNE_SLACK": "0", "SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "2"},
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "none"},
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "-0.3", "SVS_POA_PRUNE_MAX_RETRIES": "100"},
-    {"SVS_POA_VERIFY_PREP": "1"},
-    {"SVS_POA_VERIFY_PREP": "1", "SVS_POA_WPJ": "1"},
-    {"SVS_POA_VERIFY_PREP": "1", "SVS_POA_PRUNE_SLACK": "-0.3"},
-    {"SVS_POA_DEVICE_PREP": "0"},
-    {"SVS_POA_STAGING": "vec"},
-    {"SVS_POA_STAGING": "vec", "SVS_POA_PRUNE_SLACK": "-0.3"},
+    {"SVS_POA_VERIFY_GRAPH": "1"},
+    {"SVS_POA_VERIFY_GRAPH": "1", "SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_WPJ": "2"},
+    {"SVS_POA_HOST_GRAPH": "1"},
+    {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_VERIFY_PREP": "1"},
+    {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_VERIFY_PREP": "1", "SVS_POA_PRUNE_SLACK": "-0.3"},
+    {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_DEVICE_PREP": "0"},
+    {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_STAGING": "vec"},
+    {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_STAGING": "vec", "SVS_POA_PRUNE_SLACK": "-0.3"},
 ])
 def test_kernel_variants_match_oracle(env):
     """Every POA kernel instance the engine selects gives the oracle's result:
@@ -114,10 +116,13 @@ def test_kernel_variants_match_oracle(env):
     optimum (every pruned job retried: with the looser retry slack, unpruned,
     or twice, the second time unpruned; with the tables exported straight into
     the staging buffer a retried job's block is exported again), and with the
-    tables packed from per-task vectors (SVS_POA_STAGING=vec); with the row
-    tables completed on the device checked table for table against the host's
-    export (SVS_POA_VERIFY_PREP=1), and with the host export only
-    (SVS_POA_DEVICE_PREP=0)."""
+    tables packed from per-task vectors (SVS_POA_STAGING=vec); with the
+    device-resident graphs (the default) checked fold by fold against a host
+    replay (SVS_POA_VERIFY_GRAPH=1: rank order, row tables, consensus, MSA),
+    pruned retries included; and with the host graphs (SVS_POA_HOST_GRAPH=1),
+    their row tables completed on the device and checked table for table
+    against the host's export (SVS_POA_VERIFY_PREP=1), or exported on the host
+    only (SVS_POA_DEVICE_PREP=0)."""
     import os
     from svscope_amd import synth
     from svscope_amd.poa import poa_batch
@@ -191,3 +196,23 @@ def test_wide_slot_jobs_share_pruned_launches():
     for seqs, g in zip(cases, got):
         assert g == oracle_poa(seqs, 1)
     assert st["cells_computed"] < st["dp_cells"], st  # the bounded jobs were pruned
+
+
+def test_device_graphs_verified_against_host_replay():
+    """Device-resident graphs (poa_fold.hip) on the random edge cases and on
+    longer windows: every fold checked against a host PoaGraph replay (rank
+    order, lite and completed row tables, consensus, MSA rows), and the
+    results equal to the oracle's."""
+    import os
+    from svscope_amd import synth
+    from svscope_amd.poa import poa_batch
+    cases = helpers.random_cases(211, 300) + helpers.random_cases(9, 30, max_seqs=12, max_len=300, edits=25)
+    cases += [synth.make_window(w, 24, 2000)[0] for w in range(2)]
+    cases += [["", "ACGT", "", "ACGA", ""], ["", ""], ["A"], ["ACGTACGT"] * 5]
+    os.environ["SVS_POA_VERIFY_GRAPH"] = "1"
+    try:
+        got = poa_batch(cases)
+    finally:
+        os.environ.pop("SVS_POA_VERIFY_GRAPH", None)
+    for seqs, g in zip(cases, got):
+        assert g == oracle_poa(seqs, 1), seqs
