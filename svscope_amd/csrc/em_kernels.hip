@@ -139,13 +139,12 @@ struct EmShared {
 };
 
 constexpr int kMaxK = 15;      // K = 1..max_C, max_C <= 15 (host check)
-constexpr int kMaxReads = 256;  // reads per window (host check); XT rows padded to 64
 
-// Per-workgroup LDS: gamma staged for the M-step, E-step partial sums
-// (4/chunks feature slices x N reads x K).
+// gamma staged for the M-step, E-step partial sums (4/chunks feature slices x
+// N reads x K): LDS for windows of up to kEmLdsReads reads, workspace beyond.
 struct EmLds {
-  double g[kMaxReads * kMaxK];
-  double part[kMaxReads * kMaxK];
+  double* g;
+  double* part;
 };
 
 __device__ __forceinline__ int read_pad(int N) { return (N + 63) & ~63; }
@@ -317,26 +316,31 @@ __device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xr,
     return;
   }
   const int lane = tid & 63, wave = tid >> 6;
-  const int NP = read_pad(N), chunks = NP >> 6;       // 64-read chunks (1..4)
-  const int slices = 4 / chunks;                       // feature slices per chunk
-  const int chunk = wave % chunks, slice = wave / chunks;
-  const int i = chunk * 64 + lane;
+  const int NP = read_pad(N), chunks = NP >> 6;       // 64-read chunks
+  // up to 4 chunks: every wave one chunk and a 4/chunks share of the
+  // features; more: every wave whole reads of chunks wave, wave + 4, ...
+  const int slices = chunks <= 4 ? 4 / chunks : 1;    // feature slices per chunk
   // feature slices in whole 16-feature blocks: one 16-B load of the read's
   // symbols, then 16 x K independent LT gathers in flight (K is a template
   // constant so the loads are not split by per-k branches)
   const int nfp = (nf + 15) & ~15;
   const int fs = ((nfp / 16 + slices - 1) / slices) * 16;
-  if (slice < slices && i < N) {
-    const int f0 = slice * fs, f1 = min(nf, f0 + fs);
-    const uint8_t* xi = xr + static_cast<int64_t>(i) * nfp;
-    double* out = L->part + (slice * N + i) * K;
-    switch (K) {
+  for (int c = chunks <= 4 ? wave % chunks : wave; c < chunks; c += chunks <= 4 ? chunks : 4) {
+    const int slice = chunks <= 4 ? wave / chunks : 0;
+    const int i = c * 64 + lane;
+    if (slice < slices && i < N) {
+      const int f0 = slice * fs, f1 = min(nf, f0 + fs);
+      const uint8_t* xi = xr + static_cast<int64_t>(i) * nfp;
+      double* out = L->part + (slice * N + i) * K;
+      switch (K) {
 #define SVS_EK(KK) case KK: e_accumulate<KK>(xi, lt, f0, f1, out); break;
-      SVS_EK(1) SVS_EK(2) SVS_EK(3) SVS_EK(4) SVS_EK(5) SVS_EK(6) SVS_EK(7) SVS_EK(8)
-      SVS_EK(9) SVS_EK(10) SVS_EK(11) SVS_EK(12) SVS_EK(13) SVS_EK(14) SVS_EK(15)
+        SVS_EK(1) SVS_EK(2) SVS_EK(3) SVS_EK(4) SVS_EK(5) SVS_EK(6) SVS_EK(7) SVS_EK(8)
+        SVS_EK(9) SVS_EK(10) SVS_EK(11) SVS_EK(12) SVS_EK(13) SVS_EK(14) SVS_EK(15)
 #undef SVS_EK
-      default: break;
+        default: break;
+      }
     }
+    if (chunks <= 4) break;
   }
   __syncthreads();
   for (int r = tid; r < N * K; r += blockDim.x) {
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
                                                          EmConfig cfg, double* __restrict__ ws,
                                                          double* __restrict__ outd, int32_t* __restrict__ outi) {
   __shared__ EmShared sh;
-  __shared__ EmLds lds;
+  __shared__ double lds_g[kEmLdsReads * kMaxK], lds_part[kEmLdsReads * kMaxK];
   const EmWindow W = wins[blockIdx.x];
   const int N = W.n_reads, nf = W.n_feat, kmax = W.kmax, tid = threadIdx.x;
   const uint8_t* x = X + W.x_off;
@@ -394,6 +398,14 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
   for (int64_t r = tid; r < static_cast<int64_t>(N) * nfp; r += blockDim.x) {
     const int i = static_cast<int>(r / nfp), f = static_cast<int>(r % nfp);
     xr[r] = f < nf ? x[static_cast<int64_t>(i) * nf + f] : 0;
+  }
+  // gamma / E-step partials: LDS, or (deep windows) after XR in the workspace
+  EmLds lds{lds_g, lds_part};
+  if (N > kEmLdsReads) {
+    double* big = reinterpret_cast<double*>(
+        (reinterpret_cast<uintptr_t>(xr + static_cast<int64_t>(N) * nfp) + 63) & ~static_cast<uintptr_t>(63));
+    lds.g = big;
+    lds.part = big + static_cast<int64_t>(N) * 16;
   }
   if (tid == 0) { sh.rng_off = 0; sh.error = 0; sh.reinit = 0; }
   __threadfence_block();

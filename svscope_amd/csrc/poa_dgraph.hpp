@@ -20,6 +20,9 @@
 //            off u32[cv+1], nbr u32[ce] (tail / head), eid u32[ce]
 //   ew       u32  [ce]       edge weight / 2 (spoa adds 2 per sequence: 1 + 1)
 //   nin,nout u32  [cv][2]    this fold's new in / out edge of a node (eid, nbr)
+//   nrec     u32  [cv][8]    the sort's node record: in-edge CSR start,
+//                            in-degree | aligned count << 24, aligned list,
+//                            first three in-edge tails (one scalar load)
 //   r2n, n2r u32  [cv]       rank order
 //   col      u32  [cv]       MSA column of a node (rank group index)
 //   last     u32  [cv]       export scratch: last pool reader of a row
@@ -38,7 +41,7 @@ namespace svs {
 
 struct DGraphLayout {
   size_t base, al, in_off[2], in_nbr[2], in_eid[2], out_off[2], out_nbr[2], out_eid[2], ew, nin, nout;
-  size_t r2n, n2r, col, last, pstart, pred, info, col0, rec, pslot, stk, bytes;
+  size_t nrec, r2n, n2r, col, last, pstart, pred, info, col0, rec, pslot, stk, bytes;
 };
 
 __host__ __device__ inline DGraphLayout dgraph_layout(uint32_t cv, uint32_t ce) {
@@ -63,6 +66,7 @@ __host__ __device__ inline DGraphLayout dgraph_layout(uint32_t cv, uint32_t ce) 
   L.ew = take(4 * E);
   L.nin = take(8 * V);
   L.nout = take(8 * V);
+  L.nrec = take(32 * V);
   L.r2n = take(4 * V);
   L.n2r = take(4 * V);
   L.col = take(4 * V);
@@ -95,6 +99,7 @@ constexpr int32_t kFoldErrPath = -2;      // a node twice on one sequence's path
 constexpr int32_t kFoldErrAligned = -3;   // an aligned group of more than 4 nodes (letters outside ACGT)
 constexpr int32_t kFoldErrAln = -4;       // the DP traceback reported an inconsistent path
 constexpr int32_t kFoldErrStack = -5;     // DFS stack beyond its spill area
+constexpr int32_t kFoldNotRun = -100;     // the host's initial value: no fold kernel wrote the result
 
 // What the host reads back per fold job.
 struct FoldResult {

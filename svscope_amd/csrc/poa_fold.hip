@@ -41,6 +41,7 @@ typedef GLB uint32_t gu32;
 typedef GLB int32_t gi32;
 typedef GLB uint8_t gu8;
 typedef GLB char gch;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <class T> __device__ __forceinline__ GLB T* glb(T* p) { return (GLB T*)(p); }
 template <class T> __device__ __forceinline__ const GLB T* glb(const T* p) { return (const GLB T*)(p); }
 
@@ -106,7 +107,7 @@ struct GPtr {
   gu32* al;
   gu32 *in_off, *in_nbr, *in_eid, *out_off, *out_nbr, *out_eid;
   gu32* ew;
-  gu32 *nin, *nout, *r2n, *n2r, *col, *last, *pstart, *pred, *info, *stk;
+  gu32 *nin, *nout, *nrec, *r2n, *n2r, *col, *last, *pstart, *pred, *info, *stk;
 };
 
 __device__ __forceinline__ GPtr gptr(uint8_t* blk, uint32_t cv, uint32_t ce, uint32_t b) {
@@ -126,6 +127,7 @@ __device__ __forceinline__ GPtr gptr(uint8_t* blk, uint32_t cv, uint32_t ce, uin
   g.ew = u(L.ew);
   g.nin = u(L.nin);
   g.nout = u(L.nout);
+  g.nrec = u(L.nrec);
   g.r2n = u(L.r2n);
   g.n2r = u(L.n2r);
   g.col = u(L.col);
@@ -139,10 +141,11 @@ __device__ __forceinline__ GPtr gptr(uint8_t* blk, uint32_t cv, uint32_t ce, uin
 
 // One CSR list (in or out) rebuilt into buffer b1 from b0 for nodes
 // 0 .. V1-1, each node's new entry (nw[2v] = eid, nw[2v+1] = neighbour, eid
-// kNone = none) appended; the new-entry slots are reset.  Returns the number
-// of new entries found.
+// kNone = none) appended; the new-entry slots are reset.  For the in-list
+// (nrec given) also every node's sort record (poa_dgraph.hpp).  Returns the
+// number of new entries found.
 __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, const gu32* nbr0, const gu32* eid0,
-                                gu32* off1, gu32* nbr1, gu32* eid1, gu32* nw) {
+                                gu32* off1, gu32* nbr1, gu32* eid1, gu32* nw, gu32* nrec, const gu32* al) {
   const uint32_t lane = lanei();
   uint32_t run = 0, found = 0;
   for (uint32_t v0 = 0; v0 < V1; v0 += 64) {
@@ -169,6 +172,13 @@ __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, cons
         nbr1[o + d] = nb;
         eid1[o + d] = ne;
         nw[2 * v] = kNone;
+      }
+      if (nrec) {
+        auto tail = [&](uint32_t k) -> uint32_t { return k < d ? nbr0[a + k] : (k == d && has ? nb : 0u); };
+        const u32x4 alw = *reinterpret_cast<const GLB u32x4*>(al + 4 * v);
+        GLB u32x4* nr = reinterpret_cast<GLB u32x4*>(nrec + 8 * v);
+        nr[0] = u32x4{o, (d + has) | (alw.x << 24), alw.y, alw.z};
+        nr[1] = u32x4{alw.w, tail(0), tail(1), tail(2)};
       }
     }
     found += wave_add(has);
@@ -371,8 +381,10 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
   wave_sync_mem();
   const uint32_t V1 = next;
   // both adjacency lists into the other buffer, the new edge of each node last
-  const uint32_t fin = rebuild_csr(V0, V1, g.in_off, g.in_nbr, g.in_eid, h.in_off, h.in_nbr, h.in_eid, g.nin);
-  const uint32_t fout = rebuild_csr(V0, V1, g.out_off, g.out_nbr, g.out_eid, h.out_off, h.out_nbr, h.out_eid, g.nout);
+  const uint32_t fin =
+      rebuild_csr(V0, V1, g.in_off, g.in_nbr, g.in_eid, h.in_off, h.in_nbr, h.in_eid, g.nin, g.nrec, g.al);
+  const uint32_t fout =
+      rebuild_csr(V0, V1, g.out_off, g.out_nbr, g.out_eid, h.out_off, h.out_nbr, h.out_eid, g.nout, nullptr, nullptr);
   // a node twice on the path would have lost one of its new edges
   if (fin != E1 - E0 || fout != E1 - E0) return fail(kFoldErrPath);
   if (lane == 0) {
@@ -410,50 +422,41 @@ __device__ __forceinline__ bool bit_of(const uint32_t* plane, uint32_t v) { retu
 
 }  // namespace
 
-// Emission, export and finalize helpers take the arrays as restrict
-// parameters so the compiler can read the CSR through the scalar cache.
-__device__ __forceinline__ void emit_node(uint32_t node, uint32_t r, uint32_t c, gu32* __restrict__ r2n,
-                                          gu32* __restrict__ n2r, gu32* __restrict__ col) {
-  if (lanei() == 0) {
-    r2n[r] = node;
-    n2r[node] = r;
-    col[node] = c;
-  }
-}
-
-__device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ in_off, const gu32* __restrict__ in_nbr,
-                            const gu32* __restrict__ al, gu32* __restrict__ r2n, gu32* __restrict__ n2r,
-                            gu32* __restrict__ col, SortState& S, uint32_t* ncol_out) {
+// The sort, export and finalize helpers take the arrays as restrict
+// parameters so the compiler can read the read-only ones through the scalar
+// cache.
+__device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu32* __restrict__ in_nbr,
+                            gu32* __restrict__ r2n, gu32* __restrict__ n2r, gu32* __restrict__ col, SortState& S,
+                            uint32_t* ncol_out) {
   const uint32_t lane = lanei();
   const uint32_t W = (V + 31u) >> 5;
   for (uint32_t w = lane; w < W; w += 64) {
     S.done[w] = 0;
     S.ign[w] = 0;
   }
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
   uint32_t cnt = 0, ncol = 0;
-  // push / top / pop on the two-level stack (uniform control)
-  auto push = [&](uint32_t v) -> bool {
+  // Uniform control throughout.  LDS operations of one wave complete in
+  // order, so a bit set or a push is seen by the next read without a wait;
+  // only the spill area (global memory) needs its stores drained.
+  auto push = [&](uint32_t v) {
     if (S.sp == S.cap) {
       // spill the lower half of the LDS part
       const uint32_t half = S.cap / 2;
       if (S.spilled + half > S.spill_cap) {
         S.err = true;
-        return false;
+        return;
       }
       for (uint32_t k = lane; k < half; k += 64) S.spill[S.spilled + k] = S.st[k];
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_wave_barrier();
-      for (uint32_t k = lane; k < half; k += 64) S.st[k] = S.st[k + half];
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_wave_barrier();
+      for (uint32_t k = lane; k < half; k += 64) {
+        const uint32_t x = S.st[k + half];
+        __builtin_amdgcn_wave_barrier();
+        S.st[k] = x;
+      }
       S.spilled += half;
       S.sp -= half;
     }
     if (lane == 0) S.st[S.sp] = v;
     ++S.sp;
-    return true;
   };
   auto refill = [&]() {
     // the LDS part is empty: bring back up to half of it from the spill area
@@ -461,15 +464,19 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ in_off, const g
     const uint32_t k0 = S.spilled > half ? S.spilled - half : 0u, m = S.spilled - k0;
     __builtin_amdgcn_s_waitcnt(0);
     for (uint32_t k = lane; k < m; k += 64) S.st[k] = ldc(S.spill + k0 + k);
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
     S.spilled = k0;
     S.sp = m;
   };
   auto set_bit = [&](uint32_t* plane, uint32_t v) {
     if (lane == 0) plane[v >> 5] |= 1u << (v & 31u);
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
+  };
+  auto emit = [&](uint32_t node) {
+    if (lane == 0) {
+      r2n[cnt] = node;
+      n2r[node] = cnt;
+      col[node] = ncol;
+    }
+    ++cnt;
   };
   uint32_t root = 0;
   // every examination pops or pushes: a bound on them stops a corrupt graph
@@ -495,21 +502,24 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ in_off, const g
         --S.sp;
         continue;
       }
+      // the node record: CSR start, in-degree | aligned count, aligned list,
+      // first three tails (one scalar load of 32 B)
+      const gu32* nr = nrec + 8 * cur;
+      const uint32_t off = nr[0], w1 = nr[1];
+      const uint32_t deg = w1 & 0xFFFFFFu, alc = w1 >> 24;
+      const uint32_t m0 = nr[2], m1 = nr[3], m2 = nr[4], t0 = nr[5], t1 = nr[6], t2 = nr[7];
       bool valid = true;
-      const uint32_t a = in_off[cur], b = in_off[cur + 1];
-      for (uint32_t x = a; x < b; ++x) {
-        const uint32_t t = in_nbr[x];
+      for (uint32_t x = 0; x < deg; ++x) {
+        const uint32_t t = x == 0 ? t0 : (x == 1 ? t1 : (x == 2 ? t2 : in_nbr[off + x]));
         if (!bit_of(S.done, t)) {
           push(t);
           valid = false;
         }
       }
-      __builtin_amdgcn_s_waitcnt(0);
       const bool ig = bit_of(S.ign, cur);
-      const uint32_t alc = al[4 * cur];
       if (!ig) {
         for (uint32_t k = 0; k < alc; ++k) {
-          const uint32_t m = al[4 * cur + 1 + k];
+          const uint32_t m = k == 0 ? m0 : (k == 1 ? m1 : m2);
           if (!bit_of(S.done, m)) {
             push(m);
             set_bit(S.ign, m);
@@ -517,12 +527,11 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ in_off, const g
           }
         }
       }
-      __builtin_amdgcn_s_waitcnt(0);
       if (valid) {
         set_bit(S.done, cur);
         if (!ig) {
-          emit_node(cur, cnt++, ncol, r2n, n2r, col);
-          for (uint32_t k = 0; k < alc; ++k) emit_node(al[4 * cur + 1 + k], cnt++, ncol, r2n, n2r, col);
+          emit(cur);
+          for (uint32_t k = 0; k < alc; ++k) emit(k == 0 ? m0 : (k == 1 ? m1 : m2));
           ++ncol;
         }
         // the entry popped is cur's (pushes above only happen when !valid)
@@ -736,7 +745,7 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
     if (lanei() == 0) res->status = kFoldErrStack;
     return;
   }
-  const int32_t st = dfs_sort(V, g.in_off, g.in_nbr, g.al, g.r2n, g.n2r, g.col, S, &ncol);
+  const int32_t st = dfs_sort(V, g.nrec, g.in_nbr, g.r2n, g.n2r, g.col, S, &ncol);
   if (st != kFoldOk) {
     if (lanei() == 0) res->status = st;
     return;

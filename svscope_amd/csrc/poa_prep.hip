@@ -16,9 +16,9 @@
 //    before it (the backward pass: the pushes pending for the chunk after
 //    it); finished chunks go to a per-job scratch area for the rarer
 //    references more than one chunk back;
-//  * the free list lives in one VGPR (lane i = entry i, <= 64 entries,
-//    host-checked), the row outputs of a chunk in VGPR lanes, stored once per
-//    chunk.
+//  * the free list lives in one VGPR (lane i = entry i) and, past 64
+//    entries, in LDS (up to kStripPrepMaxSlots, host-checked); the row
+//    outputs of a chunk in VGPR lanes, stored once per chunk.
 // No LDS, so the kernel can share CUs with the other group's DP kernel
 // (SVS_POA_PREP_STREAM=1).
 // Column 0 follows from the fewest-nodes distance sd alone: with e, c <= 0
@@ -66,7 +66,8 @@ struct Chunk {
 // in-edge slots; pool slots handed out from slot_base.
 __device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base, const uint32_t* __restrict__ gps,
                                const uint32_t* __restrict__ gpr, const uint32_t* __restrict__ ginfo,
-                               uint32_t* __restrict__ rec, uint32_t* __restrict__ pslot, int32_t* __restrict__ c0) {
+                               uint32_t* __restrict__ rec, uint32_t* __restrict__ pslot, int32_t* __restrict__ c0,
+                               uint32_t* fl_ext) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = uni(threadIdx.x >> 6);
   // this wave's scratch words, one per row (after the job's in-edge slots)
@@ -116,7 +117,7 @@ __device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base
   if (wave == 0) {
     // pool slots, record words w0 w1 w3, in-edge slots
     uint32_t next = slot_base, fsp = 0;
-    uint32_t fstack = 0;  // free list: lane i = entry i
+    uint32_t fstack = 0;  // free list: lane i = entry i; entries past 64 in LDS (fl_ext)
     uint32_t ebuf = 0, ebase = 0;  // in-edge slots of edges ebase + lane
     uint32_t pwin = 0;             // lane i: pool slot of row r0 - 64 + i (the chunk before)
     Chunk cur = load(0);
@@ -130,8 +131,12 @@ __device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base
         const uint32_t inf = lane_of(cur.info, i);
         uint32_t own = kNoSlot;
         if ((inf >> 9) & 1u) {
-          if (fsp != 0) own = lane_of(fstack, --fsp);
-          else own = next++;
+          if (fsp != 0) {
+            --fsp;
+            own = fsp < 64 ? lane_of(fstack, fsp) : uni(fl_ext[fsp - 64]);
+          } else {
+            own = next++;
+          }
         }
         uint32_t w1 = 0, w3 = 0;
         for (uint32_t x = a; x < b; ++x) {
@@ -148,7 +153,9 @@ __device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base
           ebuf = set_lane(ps, x - ebase, ebuf);
           if (x - a < kInlinePreds) w1 |= ps << (16 * (x - a));
           if (pe >> 31) {  // this row is the tail row's last pool reader: its slot is free again
-            fstack = set_lane(ps, fsp++, fstack);
+            if (fsp < 64) fstack = set_lane(ps, fsp, fstack);
+            else if (lane == 0) fl_ext[fsp - 64] = ps;
+            ++fsp;
             if (ps < 31u) w3 |= 1u << ps;
           }
         }
@@ -256,15 +263,17 @@ __device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base
 }
 
 __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __restrict__ jobs, PoaScore P) {
+  __shared__ uint32_t fl_ext[kStripPrepMaxSlots - 64];
   const PoaJob J = jobs[blockIdx.x];
   if (!(J.prep & 1u)) return;
   strip_prep_job(P, J.n_rows, J.prep >> 1, J.pstart, J.pred, J.info, const_cast<uint32_t*>(J.rec),
-                 const_cast<uint32_t*>(J.pslot), const_cast<int32_t*>(J.col0));
+                 const_cast<uint32_t*>(J.pslot), const_cast<int32_t*>(J.col0), fl_ext);
 }
 
 // The same for the device-resident graphs (poa_dgraph.hpp): the jobs whose
 // fold exported the next alignment's lite tables into their block.
 __global__ __launch_bounds__(192) void poa_dgraph_prep_kernel(const FoldJob* __restrict__ jobs, PoaScore P) {
+  __shared__ uint32_t fl_ext[kStripPrepMaxSlots - 64];
   const FoldJob J = jobs[blockIdx.x];
   if (!(J.flags & kFoldExport)) return;
   const FoldResult* res = J.result;
@@ -275,7 +284,7 @@ __global__ __launch_bounds__(192) void poa_dgraph_prep_kernel(const FoldJob* __r
   uint8_t* b = J.blk;
   strip_prep_job(P, V, 1u, reinterpret_cast<const uint32_t*>(b + L.pstart), reinterpret_cast<const uint32_t*>(b + L.pred),
                  reinterpret_cast<const uint32_t*>(b + L.info), reinterpret_cast<uint32_t*>(b + L.rec),
-                 reinterpret_cast<uint32_t*>(b + L.pslot), reinterpret_cast<int32_t*>(b + L.col0));
+                 reinterpret_cast<uint32_t*>(b + L.pslot), reinterpret_cast<int32_t*>(b + L.col0), fl_ext);
 }
 
 }  // namespace

@@ -137,7 +137,13 @@ struct PoaArena {
       SVS_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
       copy_stream = stream;
     } else {
-      SVS_HIP(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+      // the group's copies and (device-resident graphs) its fold kernels: at
+      // the highest stream priority, so that as the other group's DP
+      // workgroups finish, the fold's workgroups are dispatched first and the
+      // group's next launch is ready when the DP stream gets to it
+      int least = 0, greatest = 0;
+      SVS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      SVS_HIP(hipStreamCreateWithPriority(&copy_stream, hipStreamNonBlocking, greatest));
     }
     SVS_HIP(hipEventCreate(&ev0));
     SVS_HIP(hipEventCreate(&ev1));

@@ -21,13 +21,19 @@ struct EmConfig {
   double eps;
 };
 
+// Windows of up to kEmLdsReads reads keep gamma and the E-step partial sums
+// in LDS; larger ones (deep windows: WindowSelection_v8.py:600 keeps a window
+// by its span, not its depth) keep them in the workspace.
+constexpr int kEmLdsReads = 256;
+
 // theta per K | LT | gamma per K | pi per K | gsum | A | M | lik per K | XT
 // (feature-major reads, nf x round_up(n, 64) bytes) | XR (read-major, n x round_up(nf, 16) bytes)
+// [| gamma + E-step partials, 2 x n x 16 doubles, for n > kEmLdsReads]
 inline uint64_t em_workspace_doubles(int n, int nf, int kmax) {
   const uint64_t nk = static_cast<uint64_t>(kmax - 1);
   return nk * (nk + 1) / 2 * nf * 5 + nk * nf * 5 + nk * (nk + 1) / 2 * n + nk * (nk + 1) / 2 + 16 +
          2ull * n * 16 + nk * n + 8 + static_cast<uint64_t>(nf) * ((n + 63) / 64) * 8 +
-         static_cast<uint64_t>(n) * ((nf + 15) / 16) * 2 + 64;
+         static_cast<uint64_t>(n) * ((nf + 15) / 16) * 2 + 64 + (n > kEmLdsReads ? 2ull * n * 16 + 8 : 0);
 }
 
 hipError_t launch_similarity(const EmWindow* wins, int n, const uint8_t* X, const int64_t* s_off, double* S,

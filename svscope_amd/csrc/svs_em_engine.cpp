@@ -143,8 +143,8 @@ svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, co
                       const int32_t* labels, const svs_em_config& cfg) {
   if (cfg.max_c < 1 || cfg.max_c > 15) throw SvsError(SVS_E_UNSUPPORTED, "max_C must be in 1..15");
   for (int32_t w = 0; w < n; ++w)
-    if (wins[w].n_reads > 256)
-      throw SvsError(SVS_E_UNSUPPORTED, "window " + std::to_string(w) + " has more than 256 reads (EM kernel limit)");
+    if (wins[w].n_reads > (1 << 16))
+      throw SvsError(SVS_E_UNSUPPORTED, "window " + std::to_string(w) + " has more than 65536 reads");
   std::vector<EmWindow> W(n);
   uint64_t xbytes = 0, lab = 0, ws = 0, od = 0, oi = 0, par = 0;
   for (int32_t w = 0; w < n; ++w) {

@@ -620,7 +620,11 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
 // the fold jobs (the DP jobs' alignments first, in the same order, then the
 // tasks whose first read lands on an empty graph).
 struct DevLaunch {
-  std::vector<uint32_t> dp_ids, fold_ids;
+  // fold jobs: first the new tasks' first reads (chains, folded before the DP
+  // kernel: their second read is aligned in the same launch), then the DP
+  // jobs' alignments in DP-job order
+  std::vector<uint32_t> dp_ids, fold_ids, fold_seq;
+  size_t n_pre = 0;
   std::vector<PoaJob> jobs;
   std::vector<FoldJob> folds;
   std::vector<uint8_t> moved;                    // fold i's graph moved to a larger block
@@ -652,6 +656,14 @@ bool device_graphs(const svs_poa_config& c) {
 // against it after every fold (tests).
 bool verify_graph() {
   const char* e = std::getenv("SVS_POA_VERIFY_GRAPH");
+  return e && std::string(e) == "1";
+}
+bool debug_launches() {
+  static const bool on = std::getenv("SVS_POA_DEBUG") != nullptr;
+  return on;
+}
+bool sync_check() {
+  const char* e = std::getenv("SVS_POA_SYNC_CHECK");
   return e && std::string(e) == "1";
 }
 
@@ -771,9 +783,6 @@ struct PoaScheduler::Impl {
       }
     poff[i] = acc;
     uploads.emplace_back(at, &t);
-    t.n_paths = 0;
-    t.dg = DGraphRef{};
-    t.tables_ok = false;
   }
 
   void release_dev(PoaTask& t) {
@@ -797,28 +806,52 @@ struct PoaScheduler::Impl {
       refill(g);
       if (g.active.empty()) return;
       const auto th0 = Clock::now();
-      std::vector<uint32_t> dp, chain, keep, fin;
+      std::vector<uint32_t> dp, chain, chain_seq, keep, fin;
+      // tasks with nothing left to align complete first (every read empty; a
+      // finished graph completes in finish_dev), before any task's state is
+      // planned for the launch
       for (uint32_t id : g.active) {
         PoaTask& t = tasks[id];
         while (t.next < t.seqs.size() && t.seqs[t.next].empty()) ++t.next;
         if (t.next >= t.seqs.size()) {
-          // every read empty (a finished graph completes in finish_dev)
           t.consensus.clear();
           t.msa.clear();
           fin.push_back(id);
-          continue;
+        } else {
+          keep.push_back(id);
         }
-        keep.push_back(id);
-        if (t.dg.V == 0) chain.push_back(id);
-        else dp.push_back(id);
       }
       g.active = keep;
-      host_ms += ms_since(th0);
       if (!fin.empty()) {
         for (uint32_t id : fin) release_dev(tasks[id]);
         g.completed = fin;
+        host_ms += ms_since(th0);
         continue;
       }
+      for (uint32_t id : g.active) {
+        PoaTask& t = tasks[id];
+        if (t.dg.V == 0) {
+          // the first read becomes a chain before this launch's DP kernel; its
+          // tables are known in advance (rows in read order, each reading the
+          // row above: one pool slot), so the next read aligns in this launch
+          chain.push_back(id);
+          chain_seq.push_back(static_cast<uint32_t>(t.next));
+          const uint32_t len = static_cast<uint32_t>(t.seqs[t.next].size());
+          t.dg.V = len;
+          t.dg.E = len - 1;
+          t.dg.par = 1;
+          t.n_paths = 1;
+          t.n_slots_next = 1;
+          t.max_preds_next = len > 1 ? 1 : 0;
+          ++t.next;
+          while (t.next < t.seqs.size() && t.seqs[t.next].empty()) ++t.next;
+          t.tables_ok = t.next < t.seqs.size();
+          if (t.tables_ok) dp.push_back(id);
+        } else {
+          dp.push_back(id);
+        }
+      }
+      host_ms += ms_since(th0);
       // the launch's DP jobs within the group's device budget (longest first;
       // the rest wait for the next launch)
       order_by_cost(dp);
@@ -833,7 +866,7 @@ struct PoaScheduler::Impl {
       }
       dp.resize(fit);
       const auto tp0 = Clock::now();
-      pack_and_launch_dev(g, dp, chain);
+      pack_and_launch_dev(g, dp, chain, chain_seq);
       g_trace.host("pack", gid(g), tp0, dp.size() + chain.size());
       g.pending = true;
       return;
@@ -847,20 +880,37 @@ struct PoaScheduler::Impl {
     return V * ls * 2 + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
   }
 
-  void pack_and_launch_dev(Group& g, const std::vector<uint32_t>& dp, const std::vector<uint32_t>& chain) {
+  void pack_and_launch_dev(Group& g, const std::vector<uint32_t>& dp, const std::vector<uint32_t>& chain,
+                           const std::vector<uint32_t>& chain_seq) {
     auto th0 = Clock::now();
     PoaArena& A = *g.arena;
     DevLaunch& D = g.dl;
     D = DevLaunch{};
     D.dp_ids = dp;
-    D.fold_ids = dp;
-    D.fold_ids.insert(D.fold_ids.end(), chain.begin(), chain.end());
-    const size_t nj = dp.size(), nf = D.fold_ids.size();
+    D.n_pre = chain.size();
+    D.fold_ids = chain;
+    D.fold_ids.insert(D.fold_ids.end(), dp.begin(), dp.end());
+    D.fold_seq = chain_seq;
+    for (uint32_t id : dp) D.fold_seq.push_back(static_cast<uint32_t>(tasks[id].next));
+    const size_t nj = dp.size(), nf = D.fold_ids.size(), npre = D.n_pre;
     // reads of the tasks that start with this launch
     std::vector<char> up;
     std::vector<std::pair<size_t, PoaTask*>> uploads;
     for (uint32_t id : D.fold_ids)
       if (!tasks[id].d_static) activate_dev(tasks[id], up, uploads);
+    // a fresh block for each chain, sized for the chain and its next read's
+    // fold in this same launch
+    for (size_t i = 0; i < npre; ++i) {
+      PoaTask& t = tasks[D.fold_ids[i]];
+      const uint32_t len = static_cast<uint32_t>(t.seqs[D.fold_seq[i]].size());
+      const uint32_t nxt = t.next < t.seqs.size() ? static_cast<uint32_t>(t.seqs[t.next].size()) : 0u;
+      const uint32_t cv1 = std::max(3 * len, len + 2 * nxt) + 4096;
+      const uint32_t ce1 = std::max(4 * len, len + 3 * nxt) + 4096;
+      t.dg_bytes = dgraph_layout(cv1, ce1).bytes;
+      t.dg.blk = static_cast<uint8_t*>(darena->alloc(t.dg_bytes));
+      t.dg.cv = cv1;
+      t.dg.ce = ce1;
+    }
     // DP jobs: the tables the last fold exported, in the task's block
     D.jobs.assign(nj, PoaJob{});
     uint64_t n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
@@ -928,11 +978,39 @@ struct PoaScheduler::Impl {
     for (size_t i = 0; i < nf; ++i) {
       PoaTask& t = tasks[D.fold_ids[i]];
       FoldJob& F = D.folds[i];
-      const uint32_t len = static_cast<uint32_t>(t.seqs[t.next].size());
-      const bool chain_job = i >= nj;
-      if (!t.dg.blk || t.dg.V + len > t.dg.cv || t.dg.E + len + 1 > t.dg.ce) {
-        const uint32_t cv1 = std::max<uint32_t>(2 * t.dg.cv, t.dg.V + 2 * len + 4096);
-        const uint32_t ce1 = std::max<uint32_t>(2 * t.dg.ce, t.dg.E + 3 * len + 4096);
+      const uint32_t si = D.fold_seq[i];
+      const uint32_t len = static_cast<uint32_t>(t.seqs[si].size());
+      const bool chain_job = i < npre;
+      if (chain_job) {
+        F.blk = t.dg.blk;
+        F.cv = t.dg.cv;
+        F.ce = t.dg.ce;
+        F.V = 0;
+        F.E = 0;
+        F.par = 0;
+        F.n_paths = 0;
+        const bool last = si + 1 >= t.last_nonempty;
+        F.flags = kFoldChain | (last ? (kFoldFinal | (t.genmsa ? kFoldMsa : 0u)) : kFoldExport);
+        F.seq = t.d_static + t.seq_at[si];
+        F.len = len;
+        F.paths = t.d_paths;
+        F.path_off = t.d_path_off;
+        if (last) {
+          D.cons_off[i] = fin;
+          fin = round_up(fin + len, 64);
+          F.msa_stride = static_cast<uint32_t>(round_up(len, 64));
+          if (t.genmsa) {
+            D.msa_off[i] = fin;
+            fin += F.msa_stride;
+          }
+        }
+        continue;
+      }
+      if (t.dg.V + len > t.dg.cv || t.dg.E + len + 1 > t.dg.ce) {
+        // a window MSA of 64 reads x 3 kb ends near 2.2 L nodes and 2.9 L
+        // edges: the first block holds that, larger graphs double
+        const uint32_t cv1 = std::max<uint32_t>(2 * t.dg.cv, t.dg.V + 3 * len + 4096);
+        const uint32_t ce1 = std::max<uint32_t>(2 * t.dg.ce, t.dg.E + 4 * len + 4096);
         const size_t bytes = dgraph_layout(cv1, ce1).bytes;
         uint8_t* nb = static_cast<uint8_t*>(darena->alloc(bytes));
         if (t.dg.blk) {
@@ -952,9 +1030,9 @@ struct PoaScheduler::Impl {
       F.V = t.dg.V;
       F.E = t.dg.E;
       F.par = t.dg.par;
-      const bool last = t.next + 1 >= t.last_nonempty;
-      F.flags = (chain_job ? kFoldChain : 0u) | (last ? (kFoldFinal | (t.genmsa ? kFoldMsa : 0u)) : kFoldExport);
-      F.seq = t.d_static + t.seq_at[t.next];
+      const bool last = si + 1 >= t.last_nonempty;
+      F.flags = last ? (kFoldFinal | (t.genmsa ? kFoldMsa : 0u)) : kFoldExport;
+      F.seq = t.d_static + t.seq_at[si];
       F.len = len;
       F.n_paths = t.n_paths;
       F.paths = t.d_paths;
@@ -986,9 +1064,9 @@ struct PoaScheduler::Impl {
     for (size_t i = 0; i < nf; ++i) {
       FoldJob& F = D.folds[i];
       F.result = reinterpret_cast<FoldResult*>(dd + s_res) + i;
-      if (i < nj) {
-        F.aln = A.d_aln.as<int32_t>() + 2 * D.jobs[i].aln_off;
-        F.aln_status = A.d_alen.as<int32_t>() + i;
+      if (i >= npre) {
+        F.aln = A.d_aln.as<int32_t>() + 2 * D.jobs[i - npre].aln_off;
+        F.aln_status = A.d_alen.as<int32_t>() + (i - npre);
       }
       if (F.flags & kFoldFinal) {
         F.cons_out = A.d_fin.as<char>() + D.cons_off[i];
@@ -998,7 +1076,11 @@ struct PoaScheduler::Impl {
     char* hd = A.h_desc.as<char>();
     if (nj) std::memcpy(hd, D.jobs.data(), nj * sizeof(PoaJob));
     std::memcpy(hd + s_fold, D.folds.data(), nf * sizeof(FoldJob));
-    std::memset(hd + s_res, 0, nf * sizeof(FoldResult));
+    for (size_t i = 0; i < nf; ++i) {
+      FoldResult r{};
+      r.status = kFoldNotRun;  // only the update kernel makes it kFoldOk
+      std::memcpy(hd + s_res + i * sizeof(FoldResult), &r, sizeof(r));
+    }
     if (!up.empty()) std::memcpy(hd + s_up, up.data(), up.size());
     host_ms += ms_since(th0);
 
@@ -1014,6 +1096,35 @@ struct PoaScheduler::Impl {
                                  static_cast<uint32_t>(m[2]), reinterpret_cast<uint8_t*>(m[3]),
                                  static_cast<uint32_t>(m[4]), static_cast<uint32_t>(m[5]), static_cast<uint32_t>(m[6]),
                                  static_cast<uint32_t>(m[7]), static_cast<uint32_t>(m[8]), side));
+    uint32_t lds_words = 0;
+    for (const FoldJob& F : D.folds) {
+      const uint32_t W = (F.V + F.len + 31) / 32;
+      lds_words = std::max(lds_words, 2 * W);
+    }
+    lds_words += 1024;  // the DFS stack's LDS part (deeper stacks spill)
+    const FoldJob* dfold = reinterpret_cast<const FoldJob*>(dd + s_fold);
+    SVS_HIP(hipEventRecord(A.evp, side));
+    if (npre) {
+      // the new tasks' first reads, and their tables, before the DP kernel
+      SVS_HIP(launch_poa_fold(dfold, static_cast<int>(npre), lds_words, side));
+      SVS_HIP(launch_dgraph_prep(dfold, static_cast<int>(npre), score, side));
+    }
+    SVS_HIP(hipEventRecord(A.evp1, side));
+    if (npre && sync_check()) {
+      // SVS_POA_SYNC_CHECK=1 (debugging): the chains' results before any DP
+      // kernel reads their tables
+      std::vector<FoldResult> rr(npre);
+      SVS_HIP(hipMemcpyAsync(rr.data(), dd + s_res, npre * sizeof(FoldResult), hipMemcpyDeviceToHost, side));
+      SVS_HIP(hipStreamSynchronize(side));
+      for (size_t i = 0; i < npre; ++i) {
+        const FoldJob& F = D.folds[i];
+        if (rr[i].status != kFoldOk || rr[i].V != F.len || rr[i].E != F.len - 1 ||
+            ((F.flags & kFoldExport) && rr[i].n_slots != 1))
+          throw SvsError(SVS_E_INTERNAL, "sync check: chain fold " + std::to_string(i) + " status " +
+                                             std::to_string(rr[i].status) + " V " + std::to_string(rr[i].V) + "/" +
+                                             std::to_string(F.len) + " slots " + std::to_string(rr[i].n_slots));
+      }
+    }
     SVS_HIP(hipEventRecord(A.h2d, side));
     D.timed_dp = nj > 0;
     if (nj) {
@@ -1036,15 +1147,11 @@ struct PoaScheduler::Impl {
       SVS_HIP(hipStreamWaitEvent(side, A.ev1, 0));
     }
     // graph update, sort, export and table completion beside the other group's DP
-    uint32_t lds_words = 0;
-    for (const FoldJob& F : D.folds) {
-      const uint32_t W = (F.V + F.len + 31) / 32;
-      lds_words = std::max(lds_words, 2 * W);
-    }
-    lds_words += 2048;  // the DFS stack's LDS part
     SVS_HIP(hipEventRecord(A.evf0, side));
-    SVS_HIP(launch_poa_fold(reinterpret_cast<const FoldJob*>(dd + s_fold), static_cast<int>(nf), lds_words, side));
-    SVS_HIP(launch_dgraph_prep(reinterpret_cast<const FoldJob*>(dd + s_fold), static_cast<int>(nf), score, side));
+    if (nj) {
+      SVS_HIP(launch_poa_fold(dfold + npre, static_cast<int>(nj), lds_words, side));
+      SVS_HIP(launch_dgraph_prep(dfold + npre, static_cast<int>(nj), score, side));
+    }
     SVS_HIP(hipEventRecord(A.evf1, side));
     A.h_alen.ensure(nj * 12 + 64);
     if (nj) SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, A.d_alen.ptr, nj * 12, hipMemcpyDeviceToHost, side));
@@ -1055,6 +1162,14 @@ struct PoaScheduler::Impl {
       if (nj) SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, A.d_aln.ptr, n_aln * 8, hipMemcpyDeviceToHost, side));
     }
     SVS_HIP(hipEventRecord(A.done, side));
+    if (debug_launches()) {
+      uint32_t vmax = 0;
+      for (const FoldJob& F : D.folds) vmax = std::max(vmax, F.V + F.len);
+      std::fprintf(stderr, "[svs] dev launch g%d: %zu dp (wpj %d, slots %u, prune %d), %zu pre, %zu post folds, "
+                           "max V+len %u, lds %u words, %zu moves, fin %zu\n",
+                   gid(g), nj, wpj, max_slots, any_prune ? 1 : 0, npre, nf - npre, vmax, lds_words, moves.size(), fin);
+      std::fflush(stderr);
+    }
     st.launches += nj ? 1 : 0;
     st.alignments += nj;
     st.tb_bytes += n_tb * 2;
@@ -1062,6 +1177,7 @@ struct PoaScheduler::Impl {
     st.h2d_bytes += total;
     st.d2h_bytes += nj * 12 + nf * sizeof(FoldResult) + fin;
     st.fold_jobs += nf;
+    for (const FoldJob& F : D.folds) st.prep_jobs += (F.flags & kFoldExport) ? 1 : 0;
   }
 
   // Waits for the group's device launch and takes its results: DP statistics
@@ -1079,21 +1195,28 @@ struct PoaScheduler::Impl {
     SVS_HIP(hipEventSynchronize(A.done));
     st.gpu_wait_ms += ms_since(tw0);
     const size_t nj = D.dp_ids.size(), nf = D.fold_ids.size();
+    if (debug_launches()) {
+      std::fprintf(stderr, "[svs] dev done g%d: %zu dp, %zu folds, %.1f ms wait\n", gid(g), nj, nf, ms_since(tw0));
+      std::fflush(stderr);
+    }
     if (D.timed_dp) {
       float ms = 0.f;
       SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
       st.kernel_ms += ms;
     }
     {
-      float ms = 0.f;
+      float ms = 0.f, pms = 0.f;
       SVS_HIP(hipEventElapsedTime(&ms, A.evf0, A.evf1));
-      st.fold_ms += ms;
+      SVS_HIP(hipEventElapsedTime(&pms, A.evp, A.evp1));
+      st.fold_ms += ms + pms;
     }
     if (g_trace.f) {
       uint64_t cells = 0;
       for (const PoaJob& J : D.jobs) cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);
       g_trace.host("wait", gid(g), tw0, nf);
       if (D.timed_dp) g_trace.kernel(gid(g), A.ev0, A.ev1, nj, D.wpj, cells);
+      g_trace.kernel(10 + gid(g), A.evf0, A.evf1, nj, 0, 0);  // the fold chain after the DP kernel
+      if (D.n_pre) g_trace.kernel(20 + gid(g), A.evp, A.evp1, D.n_pre, 0, 0);  // the chains before it
     }
     const auto th0 = Clock::now();
     const int32_t* alen = A.h_alen.as<int32_t>();
@@ -1129,12 +1252,19 @@ struct PoaScheduler::Impl {
       if (r.status != kFoldOk)
         throw SvsError(SVS_E_INTERNAL, "device POA graph fold failed (status " + std::to_string(r.status) + ")");
       if (verify) verify_fold(g, i, r);
-      t.dg.V = r.V;
-      t.dg.E = r.E;
-      t.dg.par ^= 1u;
+      if (i < D.n_pre) {
+        // a chain: the counts the launch assumed for its second read
+        if (r.V != F.len || r.E != F.len - 1 ||
+            ((F.flags & kFoldExport) && (r.n_slots != 1 || r.max_preds != (F.len > 1 ? 1u : 0u))))
+          throw SvsError(SVS_E_INTERNAL, "device POA graph: first-read chain differs from its planned tables");
+      } else {
+        t.dg.V = r.V;
+        t.dg.E = r.E;
+        t.dg.par ^= 1u;
+        t.n_paths += 1;
+        t.next = D.fold_seq[i] + 1;
+      }
       t.dg.ncol = r.ncol;
-      t.n_paths += 1;
-      t.next += 1;
       if (F.flags & kFoldExport) {
         t.n_slots_next = r.n_slots;
         t.max_preds_next = r.max_preds;
@@ -1179,12 +1309,13 @@ struct PoaScheduler::Impl {
     DevLaunch& D = g.dl;
     PoaTask& t = tasks[D.fold_ids[i]];
     const FoldJob& F = D.folds[i];
-    const std::string& s = t.seqs[t.next];
+    const std::string& s = t.seqs[D.fold_seq[i]];
     if (F.flags & kFoldChain) {
       t.graph.add_alignment_nodes({}, s);
     } else {
-      const int32_t n = A.h_alen.as<int32_t>()[i];
-      const int32_t* p = A.h_aln.as<int32_t>() + 2 * D.jobs[i].aln_off;
+      const size_t k = i - D.n_pre;
+      const int32_t n = A.h_alen.as<int32_t>()[k];
+      const int32_t* p = A.h_aln.as<int32_t>() + 2 * D.jobs[k].aln_off;
       std::vector<int32_t> fwd(2 * static_cast<size_t>(n));
       for (int32_t x = 0; x < n; ++x) {
         fwd[2 * x] = p[2 * (n - 1 - x)];
@@ -1193,9 +1324,14 @@ struct PoaScheduler::Impl {
       t.graph.add_alignment_ranks(fwd, s);
     }
     const uint32_t V = t.graph.num_nodes(), E = t.graph.num_edges();
+    // a chain whose next read was aligned and folded in the same launch: the
+    // block already holds the later graph (checked with that fold)
+    if (i < D.n_pre)
+      for (size_t j = D.n_pre; j < D.fold_ids.size(); ++j)
+        if (D.fold_ids[j] == D.fold_ids[i]) return;
     auto fail = [&](const std::string& what) {
       throw SvsError(SVS_E_INTERNAL, "device graph differs from the host graph after fold (" + what + "), read " +
-                                         std::to_string(t.next) + ", V " + std::to_string(V));
+                                         std::to_string(D.fold_seq[i]) + ", V " + std::to_string(V));
     };
     if (r.V != V || r.E != E) fail("node/edge counts " + std::to_string(r.V) + "/" + std::to_string(r.E));
     const DGraphLayout L = dgraph_layout(F.cv, F.ce);

@@ -167,6 +167,7 @@ def test_pruning_stats_and_exactness(slack, retries):
     else:
         assert st["cells_computed"] < 0.6 * st["dp_cells"], st
     assert st["prep_jobs"] > 0, st  # the device completed the row tables
+    assert st["fold_jobs"] > 0, st  # and folded the alignments into its graphs
 
 
 def test_wide_slot_jobs_share_pruned_launches():
@@ -182,7 +183,8 @@ def test_wide_slot_jobs_share_pruned_launches():
     small = [synth.make_window(w, 8, 900)[0] for w in range(10, 14)]
     small += helpers.random_cases(77, 20, max_seqs=10, max_len=260, edits=20)
     cases = [c for pair in zip(small[:2], wide) for c in pair] + small[2:]
-    env = {"SVS_POA_TEST_WIDE_SLOTS": "1500", "SVS_POA_VERIFY_PREP": "1"}  # device planner from slot 40 too
+    # (host graphs: the slot-numbering hook lives in their planner)
+    env = {"SVS_POA_TEST_WIDE_SLOTS": "1500", "SVS_POA_VERIFY_PREP": "1", "SVS_POA_HOST_GRAPH": "1"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
