@@ -482,6 +482,7 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
   // every examination pops or pushes: a bound on them stops a corrupt graph
   uint64_t steps = 0;
   const uint64_t max_steps = 64ull * (V + S.spill_cap) + 4096;
+  auto done_of = [&](uint32_t v) -> uint32_t { return (S.done[v >> 5] >> (v & 31u)) & 1u; };
   while (root < V && !S.err) {
     const uint32_t fw = uni(~S.done[root >> 5]) >> (root & 31u);
     if (fw == 0) {
@@ -491,53 +492,70 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
     root += static_cast<uint32_t>(__builtin_ctz(fw));
     if (root >= V) break;
     push(root);
-    while (S.sp + S.spilled > 0 && !S.err) {
+    uint32_t cur = root;
+    while (!S.err) {
       if (++steps > max_steps) {
         S.err = true;
         break;
       }
-      if (S.sp == 0) refill();
-      const uint32_t cur = uni(S.st[S.sp - 1]);
-      if (bit_of(S.done, cur)) {
-        --S.sp;
-        continue;
-      }
       // the node record: CSR start, in-degree | aligned count, aligned list,
-      // first three tails (one scalar load of 32 B)
+      // first three tails (one scalar load of 32 B); then every flag the
+      // examination needs in one batch of LDS reads
       const gu32* nr = nrec + 8 * cur;
       const uint32_t off = nr[0], w1 = nr[1];
       const uint32_t deg = w1 & 0xFFFFFFu, alc = w1 >> 24;
       const uint32_t m0 = nr[2], m1 = nr[3], m2 = nr[4], t0 = nr[5], t1 = nr[6], t2 = nr[7];
-      bool valid = true;
-      for (uint32_t x = 0; x < deg; ++x) {
-        const uint32_t t = x == 0 ? t0 : (x == 1 ? t1 : (x == 2 ? t2 : in_nbr[off + x]));
-        if (!bit_of(S.done, t)) {
-          push(t);
-          valid = false;
-        }
-      }
-      const bool ig = bit_of(S.ign, cur);
-      if (!ig) {
-        for (uint32_t k = 0; k < alc; ++k) {
-          const uint32_t m = k == 0 ? m0 : (k == 1 ? m1 : m2);
-          if (!bit_of(S.done, m)) {
-            push(m);
-            set_bit(S.ign, m);
+      const uint32_t dc = uni(done_of(cur)), ig = uni(bit_of(S.ign, cur) ? 1u : 0u);
+      // (unused slots read as done; they are never looked at)
+      const uint32_t d0 = uni(deg > 0 ? done_of(t0) : 1u), d1 = uni(deg > 1 ? done_of(t1) : 1u),
+                     d2 = uni(deg > 2 ? done_of(t2) : 1u);
+      const uint32_t e0 = uni(alc > 0 ? done_of(m0) : 1u), e1 = uni(alc > 1 ? done_of(m1) : 1u),
+                     e2 = uni(alc > 2 ? done_of(m2) : 1u);
+      bool pop = dc != 0;
+      if (!pop) {
+        bool valid = true;
+        for (uint32_t x = 0; x < deg; ++x) {
+          uint32_t t, dt;
+          if (x < 3) {
+            t = x == 0 ? t0 : (x == 1 ? t1 : t2);
+            dt = x == 0 ? d0 : (x == 1 ? d1 : d2);
+          } else {
+            t = in_nbr[off + x];
+            dt = uni(done_of(t));
+          }
+          if (!dt) {
+            push(t);
             valid = false;
           }
         }
-      }
-      if (valid) {
-        set_bit(S.done, cur);
         if (!ig) {
-          emit(cur);
-          for (uint32_t k = 0; k < alc; ++k) emit(k == 0 ? m0 : (k == 1 ? m1 : m2));
-          ++ncol;
+          for (uint32_t k = 0; k < alc; ++k) {
+            const uint32_t m = k == 0 ? m0 : (k == 1 ? m1 : m2);
+            const uint32_t dm = k == 0 ? e0 : (k == 1 ? e1 : e2);
+            if (!dm) {
+              push(m);
+              set_bit(S.ign, m);
+              valid = false;
+            }
+          }
         }
-        // the entry popped is cur's (pushes above only happen when !valid)
+        if (valid) {
+          set_bit(S.done, cur);
+          if (!ig) {
+            emit(cur);
+            for (uint32_t k = 0; k < alc; ++k) emit(k == 0 ? m0 : (k == 1 ? m1 : m2));
+            ++ncol;
+          }
+          pop = true;  // the entry popped is cur's (pushes only happen when !valid)
+        }
+      }
+      if (pop) {
         if (S.sp == 0) refill();
         --S.sp;
+        if (S.sp + S.spilled == 0) break;
+        if (S.sp == 0) refill();
       }
+      cur = uni(S.st[S.sp - 1]);
     }
     ++root;
   }
