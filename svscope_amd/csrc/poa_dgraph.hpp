@@ -105,6 +105,10 @@ constexpr int32_t kFoldNotRun = -100;     // the host's initial value: no fold k
 struct FoldResult {
   int32_t status;
   uint32_t V, E, n_slots, max_preds, ncol, pad0, pad1;
+  // phase times in 10 ns ticks (s_memrealtime): update kernel, sort, export,
+  // consensus + MSA rows (SVS_POA_FOLD_TIMES prints their totals)
+  uint32_t t_upd, t_sort, t_exp, t_fin;
+  uint32_t n_exam, n_roots;  // DFS examinations and DFS starts of the sort
 };
 
 // One fold job: fold the job's alignment (or, with kFoldChain, the whole

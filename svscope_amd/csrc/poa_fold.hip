@@ -190,6 +190,11 @@ __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, cons
 
 }  // namespace
 
+// The fold kernels run one wave per job beside the DP kernel's waves on the
+// same SIMDs and sit on the chain DP -> fold -> next DP of their group: they
+// issue ahead of the DP waves (s_setprio), which only wait on them.
+#define SVS_FOLD_PRIO() __builtin_amdgcn_s_setprio(3)
+
 // ---------------------------------------------------------------- update
 // spoa Graph::AddAlignment (poa_graph.cpp add_alignment_nodes): nodes of the
 // prefix chain, then the suffix chain, then the middle's new nodes in path
@@ -199,6 +204,8 @@ __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, cons
 // anchor; every member appends the newcomer).  Then one edge per consecutive
 // path pair, existing ones gaining weight.
 __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __restrict__ jobs) {
+  SVS_FOLD_PRIO();
+  const uint64_t T0 = __builtin_amdgcn_s_memrealtime();
   const FoldJob J = jobs[blockIdx.x];
   const uint32_t lane = lanei();
   GLB FoldResult* res = glb(J.result);
@@ -294,13 +301,13 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
       mis_m &= mis_m - 1;
       const uint32_t nj = lane_val(nn, j), lt = lane_val(letter, j);
       __builtin_amdgcn_s_waitcnt(0);  // this wave's earlier group updates have landed
-      const uint32_t cnt = ldc(g.al + 4 * nj);
+      const uint32_t cnt = uni(ldc(g.al + 4 * nj));
       if (cnt > 3) return fail(kFoldErrAligned);
       uint32_t mem[3] = {0, 0, 0};
       uint32_t found = kNone;
       for (uint32_t k = 0; k < cnt; ++k) {
-        mem[k] = ldc(g.al + 4 * nj + 1 + k);
-        if (found == kNone && ldc_u8(g.base, mem[k]) == lt) found = mem[k];
+        mem[k] = uni(ldc(g.al + 4 * nj + 1 + k));
+        if (found == kNone && uni(ldc_u8(g.base, mem[k])) == lt) found = mem[k];
       }
       uint32_t cj = found;
       if (found == kNone) {
@@ -321,7 +328,7 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
         // every member, then the anchor, appends the newcomer
         for (uint32_t k = 0; k <= cnt; ++k) {
           const uint32_t a = k < cnt ? mem[k] : nj;
-          const uint32_t ca = ldc(g.al + 4 * a);
+          const uint32_t ca = uni(ldc(g.al + 4 * a));
           if (ca >= 3) return fail(kFoldErrAligned);
           if (lane == 0) {
             g.al[4 * a + 1 + ca] = cj;
@@ -391,6 +398,7 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
     res->status = kFoldOk;
     res->V = V1;
     res->E = E1;
+    res->t_upd = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime() - T0);
   }
 }
 
@@ -416,6 +424,7 @@ struct SortState {
   uint32_t sp;       // entries in the LDS part
   uint32_t spill_cap;  // entries the spill area holds
   bool err;            // the stack outgrew its spill area
+  uint32_t n_exam, n_roots;  // statistics
 };
 
 __device__ __forceinline__ bool bit_of(const uint32_t* plane, uint32_t v) { return (plane[v >> 5] >> (v & 31u)) & 1u; }
@@ -446,16 +455,22 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
         S.err = true;
         return;
       }
-      for (uint32_t k = lane; k < half; k += 64) S.spill[S.spilled + k] = S.st[k];
-      for (uint32_t k = lane; k < half; k += 64) {
-        const uint32_t x = S.st[k + half];
+      // (loops with uniform trip counts and predicated lanes: a loop whose
+      // lanes leave at different trips makes the whole DFS loop divergent)
+      for (uint32_t k0 = 0; k0 < half; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        if (k < half) S.spill[S.spilled + k] = S.st[k];
+      }
+      for (uint32_t k0 = 0; k0 < half; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const uint32_t x = k < half ? S.st[k + half] : 0u;
         __builtin_amdgcn_wave_barrier();
-        S.st[k] = x;
+        if (k < half) S.st[k] = x;
       }
       S.spilled += half;
       S.sp -= half;
     }
-    if (lane == 0) S.st[S.sp] = v;
+    S.st[S.sp] = v;  // (every lane the same word: no divergent branch)
     ++S.sp;
   };
   auto refill = [&]() {
@@ -463,26 +478,43 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
     const uint32_t half = S.cap / 2;
     const uint32_t k0 = S.spilled > half ? S.spilled - half : 0u, m = S.spilled - k0;
     __builtin_amdgcn_s_waitcnt(0);
-    for (uint32_t k = lane; k < m; k += 64) S.st[k] = ldc(S.spill + k0 + k);
+    for (uint32_t j0 = 0; j0 < m; j0 += 64) {
+      const uint32_t k = j0 + lane;
+      if (k < m) S.st[k] = ldc(S.spill + k0 + k);
+    }
     S.spilled = k0;
     S.sp = m;
   };
-  auto set_bit = [&](uint32_t* plane, uint32_t v) {
-    if (lane == 0) plane[v >> 5] |= 1u << (v & 31u);
-  };
+  // every lane stores the same words (a lane-0 branch would make the DFS loop
+  // divergent: values in vector registers, control through exec masks)
+  auto set_bit = [&](uint32_t* plane, uint32_t v) { plane[v >> 5] |= 1u << (v & 31u); };
   auto emit = [&](uint32_t node) {
-    if (lane == 0) {
-      r2n[cnt] = node;
-      n2r[node] = cnt;
-      col[node] = ncol;
-    }
+    r2n[cnt] = node;
+    n2r[node] = cnt;
+    col[node] = ncol;
     ++cnt;
   };
   uint32_t root = 0;
   // every examination pops or pushes: a bound on them stops a corrupt graph
-  uint64_t steps = 0;
-  const uint64_t max_steps = 64ull * (V + S.spill_cap) + 4096;
+  uint32_t steps = 0;
+  const uint32_t max_steps = 64u * (V + S.spill_cap) + 4096u;
   auto done_of = [&](uint32_t v) -> uint32_t { return (S.done[v >> 5] >> (v & 31u)) & 1u; };
+  // Node records come from two 64-node windows held in registers (lane l:
+  // node base + l), loaded whole with one coalesced load: R follows the root
+  // scan (ids ascending), D the nodes the DFS pushes (mostly the new nodes of
+  // the latest read, whose ids are close together).  An examination then
+  // reads its record with lane reads instead of a dependent load.
+  uint32_t bR = 0x80000000u, bD = 0x80000000u;  // empty: no id (< 2^31) is within 64 of them
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0, r5 = 0, r6 = 0, r7 = 0;
+  uint32_t d0w = 0, d1w = 0, d2w = 0, d3w = 0, d4w = 0, d5w = 0, d6w = 0, d7w = 0;
+  auto load_win = [&](uint32_t b, uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3, uint32_t& w4,
+                      uint32_t& w5, uint32_t& w6, uint32_t& w7) {
+    const uint32_t v = min(b + lane, V - 1u);
+    const u32x4 x = *reinterpret_cast<const GLB u32x4*>(nrec + 8 * v);
+    const u32x4 y = *reinterpret_cast<const GLB u32x4*>(nrec + 8 * v + 4);
+    w0 = x.x; w1 = x.y; w2 = x.z; w3 = x.w;
+    w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
+  };
   while (root < V && !S.err) {
     const uint32_t fw = uni(~S.done[root >> 5]) >> (root & 31u);
     if (fw == 0) {
@@ -492,6 +524,7 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
     root += static_cast<uint32_t>(__builtin_ctz(fw));
     if (root >= V) break;
     push(root);
+    ++S.n_roots;
     uint32_t cur = root;
     while (!S.err) {
       if (++steps > max_steps) {
@@ -499,18 +532,39 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
         break;
       }
       // the node record: CSR start, in-degree | aligned count, aligned list,
-      // first three tails (one scalar load of 32 B); then every flag the
+      // first three tails (from a register window); then every flag the
       // examination needs in one batch of LDS reads
-      const gu32* nr = nrec + 8 * cur;
-      const uint32_t off = nr[0], w1 = nr[1];
+      bool inR = cur - bR < 64u, inD = cur - bD < 64u;
+      if (!inR && !inD) {
+        if (cur == root) {
+          bR = cur;
+          load_win(bR, r0, r1, r2, r3, r4, r5, r6, r7);
+          inR = true;
+        } else {
+          bD = cur > 32u ? cur - 32u : 0u;
+          load_win(bD, d0w, d1w, d2w, d3w, d4w, d5w, d6w, d7w);
+        }
+      }
+      uint32_t off, w1, m0, m1, m2, t0, t1, t2;
+      if (inR) {
+        const uint32_t l = cur - bR;
+        off = lane_val(r0, l); w1 = lane_val(r1, l); m0 = lane_val(r2, l); m1 = lane_val(r3, l);
+        m2 = lane_val(r4, l); t0 = lane_val(r5, l); t1 = lane_val(r6, l); t2 = lane_val(r7, l);
+      } else {
+        const uint32_t l = cur - bD;
+        off = lane_val(d0w, l); w1 = lane_val(d1w, l); m0 = lane_val(d2w, l); m1 = lane_val(d3w, l);
+        m2 = lane_val(d4w, l); t0 = lane_val(d5w, l); t1 = lane_val(d6w, l); t2 = lane_val(d7w, l);
+      }
       const uint32_t deg = w1 & 0xFFFFFFu, alc = w1 >> 24;
-      const uint32_t m0 = nr[2], m1 = nr[3], m2 = nr[4], t0 = nr[5], t1 = nr[6], t2 = nr[7];
       const uint32_t dc = uni(done_of(cur)), ig = uni(bit_of(S.ign, cur) ? 1u : 0u);
-      // (unused slots read as done; they are never looked at)
-      const uint32_t d0 = uni(deg > 0 ? done_of(t0) : 1u), d1 = uni(deg > 1 ? done_of(t1) : 1u),
-                     d2 = uni(deg > 2 ? done_of(t2) : 1u);
-      const uint32_t e0 = uni(alc > 0 ? done_of(m0) : 1u), e1 = uni(alc > 1 ? done_of(m1) : 1u),
-                     e2 = uni(alc > 2 ? done_of(m2) : 1u);
+      // (unused slots read cur's word and count as done; they are never looked
+      // at: all eight reads issue together, one wait)
+      const uint32_t d0 = uni(done_of(deg > 0 ? t0 : cur) | (deg > 0 ? 0u : 1u));
+      const uint32_t d1 = uni(done_of(deg > 1 ? t1 : cur) | (deg > 1 ? 0u : 1u));
+      const uint32_t d2 = uni(done_of(deg > 2 ? t2 : cur) | (deg > 2 ? 0u : 1u));
+      const uint32_t e0 = uni(done_of(alc > 0 ? m0 : cur) | (alc > 0 ? 0u : 1u));
+      const uint32_t e1 = uni(done_of(alc > 1 ? m1 : cur) | (alc > 1 ? 0u : 1u));
+      const uint32_t e2 = uni(done_of(alc > 2 ? m2 : cur) | (alc > 2 ? 0u : 1u));
       bool pop = dc != 0;
       if (!pop) {
         bool valid = true;
@@ -560,6 +614,7 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
     ++root;
   }
   *ncol_out = ncol;
+  S.n_exam = static_cast<uint32_t>(steps);
   return (cnt == V && !S.err) ? kFoldOk : kFoldErrStack;
 }
 
@@ -719,6 +774,96 @@ __device__ uint32_t consensus_rev(uint32_t V, const gu8* __restrict__ base, cons
   return n;
 }
 
+// consensus_rev with the scores and predecessors in LDS (sc: V int32, pn: V
+// uint16, 0xFFFF = none; V < 65535) and each 64-row chunk's nodes and first
+// four in-edges (tail, weight) loaded into lanes with coalesced loads before
+// the chunk's rows are scored one by one, so a row costs LDS reads instead of
+// a chain of dependent global loads.  Same comparisons, same order.
+__device__ uint32_t consensus_rev_lds(uint32_t V, const gu8* __restrict__ base, const gu32* __restrict__ in_off,
+                                      const gu32* __restrict__ in_nbr, const gu32* __restrict__ in_eid,
+                                      const gu32* __restrict__ out_off, const gu32* __restrict__ out_nbr,
+                                      const gu32* __restrict__ ew, const gu32* __restrict__ r2n,
+                                      const gu32* __restrict__ n2r, int32_t* sc, uint16_t* pn, gch* __restrict__ out) {
+  const uint32_t lane = lanei();
+  constexpr uint16_t kNoPred = 0xFFFFu;
+  for (uint32_t v = lane; v < V; v += 64) {
+    sc[v] = -1;
+    pn[v] = kNoPred;
+  }
+  int32_t best = -1, best_sc = 0;
+  // rows rbeg .. V-1 in rank order; rescan: in-edges from an unscored (-1) tail are skipped
+  auto pass = [&](uint32_t rbeg, bool rescan) {
+    best = -1;
+    best_sc = 0;
+    for (uint32_t c0 = rbeg; c0 < V; c0 += 64) {
+      const uint32_t r = c0 + lane;
+      uint32_t node = 0, a = 0, deg = 0, ta = 0, tb = 0, tc = 0, td = 0, wa = 0, wb = 0, wc = 0, wd = 0;
+      if (r < V) {
+        node = r2n[r];
+        a = in_off[node];
+        deg = in_off[node + 1] - a;
+        if (deg > 0) { ta = in_nbr[a]; wa = ew[in_eid[a]]; }
+        if (deg > 1) { tb = in_nbr[a + 1]; wb = ew[in_eid[a + 1]]; }
+        if (deg > 2) { tc = in_nbr[a + 2]; wc = ew[in_eid[a + 2]]; }
+        if (deg > 3) { td = in_nbr[a + 3]; wd = ew[in_eid[a + 3]]; }
+      }
+      const uint32_t nh = min(64u, V - c0);
+      for (uint32_t i = 0; i < nh; ++i) {
+        const uint32_t nd = lane_val(node, i), dg = lane_val(deg, i);
+        int32_t s = -1, p = -1, sp = 0;
+        auto edge = [&](uint32_t t, uint32_t wu) {
+          const int32_t st = static_cast<int32_t>(uni(static_cast<uint32_t>(sc[t])));
+          if (rescan && st == -1) return;
+          const int32_t w = static_cast<int32_t>(wu);
+          if (s < w || (s == w && sp <= st)) {
+            s = w;
+            p = static_cast<int32_t>(t);
+            sp = st;
+          }
+        };
+        if (dg > 0) edge(lane_val(ta, i), lane_val(wa, i));
+        if (dg > 1) edge(lane_val(tb, i), lane_val(wb, i));
+        if (dg > 2) edge(lane_val(tc, i), lane_val(wc, i));
+        if (dg > 3) edge(lane_val(td, i), lane_val(wd, i));
+        if (dg > 4) {
+          const uint32_t ai = lane_val(a, i);
+          for (uint32_t x = 4; x < dg; ++x) edge(uni(in_nbr[ai + x]), uni(ew[in_eid[ai + x]]));
+        }
+        if (p != -1) s += sp;
+        if (lane == 0) {
+          sc[nd] = s;
+          pn[nd] = p == -1 ? kNoPred : static_cast<uint16_t>(p);
+        }
+        if (best == -1 || best_sc < s) {
+          best = static_cast<int32_t>(nd);
+          best_sc = s;
+        }
+      }
+    }
+  };
+  pass(0, false);
+  if (best < 0) return 0;
+  // branch completion while the best node has successors
+  while (out_off[best + 1] != out_off[best]) {
+    const uint32_t start = static_cast<uint32_t>(best), rank = n2r[start];
+    for (uint32_t e = out_off[start]; e < out_off[start + 1]; ++e) {
+      const uint32_t hd = out_nbr[e];
+      for (uint32_t f = in_off[hd]; f < in_off[hd + 1]; ++f)
+        if (in_nbr[f] != start && lane == 0) sc[in_nbr[f]] = -1;
+    }
+    pass(rank + 1, true);
+  }
+  // the path back from best, node ids first into sc (scores are done), then
+  // its letters gathered by all lanes
+  uint32_t n = 0;
+  for (uint32_t x = static_cast<uint32_t>(best); x != kNoPred && n < V; x = uni(pn[x])) {
+    if (lane == 0) sc[n] = static_cast<int32_t>(x);
+    ++n;
+  }
+  for (uint32_t k = lane; k < n; k += 64) out[k] = static_cast<char>(base[sc[k]]);
+  return n;
+}
+
 // MSA rows: every sequence's path nodes at their columns, '-' elsewhere.
 __device__ void msa_rows(uint32_t n_paths, const gu32* __restrict__ paths, const gu32* __restrict__ path_off,
                          const gu32* __restrict__ colv, const gu8* __restrict__ base, uint32_t ncol,
@@ -740,7 +885,9 @@ __device__ void msa_rows(uint32_t n_paths, const gu32* __restrict__ paths, const
 }
 
 __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __restrict__ jobs, uint32_t lds_words) {
+  SVS_FOLD_PRIO();
   extern __shared__ uint32_t lds[];
+  const uint64_t T0 = __builtin_amdgcn_s_memrealtime();
   const FoldJob J = jobs[blockIdx.x];
   GLB FoldResult* res = glb(J.result);
   if (uni(static_cast<uint32_t>(res->status)) != static_cast<uint32_t>(kFoldOk)) return;
@@ -758,33 +905,76 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
   S.sp = 0;
   S.spill_cap = J.ce + 2 * J.cv + 64;
   S.err = false;
+  S.n_exam = 0;
+  S.n_roots = 0;
   uint32_t ncol = 0;
   if (S.cap < 64) {
     if (lanei() == 0) res->status = kFoldErrStack;
     return;
   }
-  const int32_t st = dfs_sort(V, g.nrec, g.in_nbr, g.r2n, g.n2r, g.col, S, &ncol);
+  int32_t st = kFoldOk;
+  if (J.flags & kFoldChain) {
+    // a fresh chain (node i's only in-edge from i - 1): the DFS order is the
+    // identity, one column per node
+    for (uint32_t v = lanei(); v < V; v += 64) {
+      g.r2n[v] = v;
+      g.n2r[v] = v;
+      g.col[v] = v;
+    }
+    ncol = V;
+  } else {
+    st = dfs_sort(V, g.nrec, g.in_nbr, g.r2n, g.n2r, g.col, S, &ncol);
+  }
   if (st != kFoldOk) {
     if (lanei() == 0) res->status = st;
     return;
   }
   wave_sync_mem();
+  const uint64_t T1 = __builtin_amdgcn_s_memrealtime();
   uint32_t n_slots = 0, max_preds = 0;
   if (J.flags & kFoldExport)
     export_lite(V, g.base, g.in_off, g.in_nbr, g.out_off, g.r2n, g.n2r, g.last, g.pstart, g.pred, g.info, &n_slots,
                 &max_preds);
-  if (J.flags & kFoldFinal) {
-    const uint32_t nc = consensus_rev(V, g.base, g.in_off, g.in_nbr, g.in_eid, g.out_off, g.out_nbr, g.ew, g.r2n,
-                                      g.n2r, reinterpret_cast<gi32*>(g.last), reinterpret_cast<gi32*>(g.pstart),
-                                      glb(J.cons_out));
-    if (J.flags & kFoldMsa)
-      msa_rows(J.n_paths + 1, glb(J.paths), glb(J.path_off), g.col, g.base, ncol, glb(J.msa_out), J.msa_stride);
-    if (lanei() == 0) res->pad0 = nc;
-  }
+  const uint64_t T2 = __builtin_amdgcn_s_memrealtime();
   if (lanei() == 0) {
     res->n_slots = n_slots;
     res->max_preds = max_preds;
     res->ncol = ncol;
+    res->t_sort = static_cast<uint32_t>(T1 - T0);
+    res->t_exp = static_cast<uint32_t>(T2 - T1);
+    res->n_exam = S.n_exam;
+    res->n_roots = S.n_roots;
+  }
+}
+
+// The last read's fold (kFoldFinal): consensus and MSA rows, after the sort.
+// lds_words: the LDS the launch gives each job (6 B per node for the scores
+// and predecessors; larger graphs score in global memory).
+__global__ __launch_bounds__(64) void poa_fold_final_kernel(const FoldJob* __restrict__ jobs, uint32_t lds_words) {
+  SVS_FOLD_PRIO();
+  extern __shared__ uint32_t lds[];
+  const uint64_t T0 = __builtin_amdgcn_s_memrealtime();
+  const FoldJob J = jobs[blockIdx.x];
+  if (!(J.flags & kFoldFinal)) return;
+  GLB FoldResult* res = glb(J.result);
+  if (uni(static_cast<uint32_t>(res->status)) != static_cast<uint32_t>(kFoldOk)) return;
+  const uint32_t V = uni(res->V), ncol = uni(res->ncol);
+  const GPtr g = gptr(J.blk, J.cv, J.ce, 1u - J.par);
+  uint32_t nc;
+  if (V < 65535u && 6ull * V + 8 <= 4ull * lds_words) {
+    int32_t* sc = reinterpret_cast<int32_t*>(lds);
+    uint16_t* pn = reinterpret_cast<uint16_t*>(lds + V);
+    nc = consensus_rev_lds(V, g.base, g.in_off, g.in_nbr, g.in_eid, g.out_off, g.out_nbr, g.ew, g.r2n, g.n2r, sc, pn,
+                           glb(J.cons_out));
+  } else {
+    nc = consensus_rev(V, g.base, g.in_off, g.in_nbr, g.in_eid, g.out_off, g.out_nbr, g.ew, g.r2n, g.n2r,
+                       reinterpret_cast<gi32*>(g.last), reinterpret_cast<gi32*>(g.pstart), glb(J.cons_out));
+  }
+  if (J.flags & kFoldMsa)
+    msa_rows(J.n_paths + 1, glb(J.paths), glb(J.path_off), g.col, g.base, ncol, glb(J.msa_out), J.msa_stride);
+  if (lanei() == 0) {
+    res->pad0 = nc;
+    res->t_fin = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime() - T0);
   }
 }
 
@@ -824,10 +1014,14 @@ __global__ __launch_bounds__(256) void poa_dgraph_move_kernel(const uint8_t* __r
   cp(A.pslot, B.pslot, 4ull * E);
 }
 
-hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, hipStream_t stream) {
+hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, uint32_t final_lds_words,
+                           hipStream_t stream) {
   if (n_jobs <= 0) return hipSuccess;
   hipLaunchKernelGGL(poa_fold_update_kernel, dim3(n_jobs), dim3(64), 0, stream, jobs);
   hipLaunchKernelGGL(poa_fold_sort_kernel, dim3(n_jobs), dim3(64), lds_words * 4, stream, jobs, lds_words);
+  if (final_lds_words)
+    hipLaunchKernelGGL(poa_fold_final_kernel, dim3(n_jobs), dim3(64), final_lds_words * 4, stream, jobs,
+                       final_lds_words);
   return hipGetLastError();
 }
 

@@ -40,6 +40,13 @@ namespace svs {
 
 namespace {
 
+// Global-memory (address space 1) views of the job's tables: loads through
+// them are global_load (vmcnt only) instead of flat loads, which also count in
+// lgkmcnt and so made every LDS-pool wait of a row wait for the carries
+// prefetched for a later row as well.
+#define GLB __attribute__((address_space(1)))
+template <class T> __device__ __forceinline__ const GLB T* glb(const T* p) { return (const GLB T*)(p); }
+
 // One pool slot: 65 int32 Hx = H at columns j0-1 .. j0+63 (so a successor
 // reads H[j] at Hx[l+1] and its diagonal H[j-1] at Hx[l], with no lane shift),
 // then 64 uint16 D = dF | dO << 8 with dF = min(H - F, tF), dO = min(H - O, tO)
@@ -133,7 +140,7 @@ struct RowIn {
   int32_t b0, b1, b2, b3;
 };
 
-__device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, const uint32_t* __restrict__ spill) {
+__device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, const GLB uint32_t* __restrict__ spill) {
   if (k >= kInlinePreds) return spill[k];
   return (d.w1 >> (16 * k)) & 0xFFFFu;
 }
@@ -210,12 +217,12 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * kStride;
   else pool = gpool + J.pool_off + static_cast<uint64_t>(wave) * ((nslot * kSlotInts + 63) / 64 * 64);
   uint16_t* __restrict__ tbj = tb + J.tb_off;
-  const uint32_t* __restrict__ rec = J.rec;
-  const uint32_t* __restrict__ rps = J.pstart;
-  const uint32_t* __restrict__ prow = J.pred;
-  const uint32_t* __restrict__ pslot = J.pslot;
-  const int32_t* __restrict__ rc0 = J.col0;
-  const uint8_t* __restrict__ seq = J.seq;
+  const GLB uint32_t* __restrict__ rec = glb(J.rec);
+  const GLB uint32_t* __restrict__ rps = glb(J.pstart);
+  const GLB uint32_t* __restrict__ prow = glb(J.pred);
+  const GLB uint32_t* __restrict__ pslot = glb(J.pslot);
+  const GLB int32_t* __restrict__ rc0 = glb(J.col0);
+  const GLB uint8_t* __restrict__ seq = glb(J.seq);
   int32_t* __restrict__ bnd = bnd_all + J.bnd_off;
   // The same carry buffer, read-only: loads through it are uniform and never
   // clobbered by this kernel's stores (those go through bnd), so they become
@@ -223,7 +230,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   // launch, by whole 128-B lines (strip blocks padded to 8 rows), and read only
   // after its producer has finished the line (progress is published at
   // multiples of 8 rows after a release) and drained its stores.
-  const int32_t* __restrict__ bndr = bnd_rd + J.bnd_off;
+  const GLB int32_t* __restrict__ bndr = glb(bnd_rd) + J.bnd_off;
 
   int32_t best = SVS_NEG_INF;  // meaningful on the lane owning column L
   int32_t best_row = 0;
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const int32_t j = j0 + lane;
     const uint8_t rc = seq[j - 1];  // seq[-1] is a zero pad byte (column 0)
     uint16_t* __restrict__ tbl = tbj + j;  // this lane's column of the traceback codes
-    const int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
+    const GLB int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
     int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
     const int32_t pw = (wave + WPJ - 1) % WPJ;          // producer of strip s-1
     const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
@@ -319,7 +326,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     auto fetch = [&](RowIn& d, uint32_t r) {
       const uint32_t rr = r < V ? r : V - 1;
       // 32-bit byte offsets off the job's bases (a job has < 2^28 rows)
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(rec) + (rr << 4));
+      const GLB uint32_t* w = rec + (rr << 2);
       d.w0 = w[0];
       d.w1 = w[1];
       if constexpr (PRUNE) {
@@ -340,7 +347,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
             avail = strip_wait_ge(&prog[pw], need, &s_err);
           }
         }
-        const int4 v = *reinterpret_cast<const int4*>(reinterpret_cast<const char*>(bin) + (rr << 4));
+        const svs_i32x4 v = *reinterpret_cast<const GLB svs_i32x4*>(bin + (rr << 2));
         d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
       }
     };
@@ -383,7 +390,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
           const uint32_t wp = __builtin_amdgcn_readfirstlane(d.w1);
           live = slot_alive(wp & 0xFFFFu) || (np >= 2 && slot_alive(wp >> 16));
           if (!live && np > kInlinePreds) {
-            const uint32_t* __restrict__ spill = pslot + rps[r];
+            const GLB uint32_t* __restrict__ spill = pslot + rps[r];
             for (uint32_t k = kInlinePreds; k < np && !live; ++k)
               live = slot_alive(__builtin_amdgcn_readfirstlane(spill[k]));
           }
@@ -526,7 +533,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         code |= lbit ? 0x100u : 0u;
         code |= ((va || (!vb && vc)) ? 0x200u : 0u) | (ch0 ? 0u : (1u << 10));
       } else {
-        const uint32_t* __restrict__ spill = pslot + rps[r];
+        const GLB uint32_t* __restrict__ spill = pslot + rps[r];
         F = SVS_VNEG;
         O = SVS_VNEG;
         int32_t Hd = SVS_VNEG;

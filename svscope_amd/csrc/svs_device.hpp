@@ -81,7 +81,10 @@ hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore&
                                  hipStream_t stream);
 // Device-resident graphs (poa_fold.hip, poa_prep.hip; poa_dgraph.hpp).
 struct FoldJob;
-hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, hipStream_t stream);
+// update + sort (+ the final kernel when final_lds_words > 0: some job of the
+// launch has kFoldFinal)
+hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, uint32_t final_lds_words,
+                           hipStream_t stream);
 hipError_t launch_dgraph_prep(const FoldJob* jobs, int n_jobs, const PoaScore& score, hipStream_t stream);
 hipError_t launch_dgraph_move(const uint8_t* src, uint32_t cv0, uint32_t ce0, uint8_t* dst, uint32_t cv1, uint32_t ce1,
                               uint32_t V, uint32_t E, uint32_t par, hipStream_t stream);

@@ -658,6 +658,47 @@ bool verify_graph() {
   const char* e = std::getenv("SVS_POA_VERIFY_GRAPH");
   return e && std::string(e) == "1";
 }
+// SVS_POA_FOLD_TIMES: totals of the fold kernels' phase times (FoldResult
+// t_*), printed at exit
+struct FoldTimes {
+  bool on = [] {
+    const char* e = std::getenv("SVS_POA_FOLD_TIMES");
+    return e && std::atoi(e) != 0;
+  }();
+  double upd = 0, sort = 0, exp = 0, fin = 0, max_sort = 0, max_fin = 0;
+  uint64_t n = 0, n_exp = 0, n_fin = 0, verts = 0, exams = 0, roots = 0;
+  void add(const FoldResult& r, uint32_t flags) {
+    if (!on) return;
+    ++n;
+    verts += r.V;
+    exams += r.n_exam;
+    roots += r.n_roots;
+    upd += r.t_upd * 1e-5;
+    sort += r.t_sort * 1e-5;
+    max_sort = std::max(max_sort, r.t_sort * 1e-5);
+    if (flags & kFoldExport) {
+      ++n_exp;
+      exp += r.t_exp * 1e-5;
+    }
+    if (flags & kFoldFinal) {
+      ++n_fin;
+      fin += r.t_fin * 1e-5;
+      max_fin = std::max(max_fin, r.t_fin * 1e-5);
+    }
+  }
+  ~FoldTimes() {
+    if (!on || !n) return;
+    std::fprintf(stderr,
+                 "[svs] fold times (ms per job): %llu folds, mean V %.0f; update %.3f, sort %.3f (max %.2f); "
+                 "%llu exports %.3f; %llu finals %.3f (max %.2f); per fold %.0f DFS examinations, %.0f roots\n",
+                 static_cast<unsigned long long>(n), double(verts) / n, upd / n, sort / n, max_sort,
+                 static_cast<unsigned long long>(n_exp), n_exp ? exp / n_exp : 0.0,
+                 static_cast<unsigned long long>(n_fin), n_fin ? fin / n_fin : 0.0, max_fin, double(exams) / n,
+                 double(roots) / n);
+  }
+};
+FoldTimes g_fold_times;
+
 bool debug_launches() {
   static const bool on = std::getenv("SVS_POA_DEBUG") != nullptr;
   return on;
@@ -1102,11 +1143,21 @@ struct PoaScheduler::Impl {
       lds_words = std::max(lds_words, 2 * W);
     }
     lds_words += 1024;  // the DFS stack's LDS part (deeper stacks spill)
+    // the final kernel's LDS per job (6 B per node, up to 64 KiB; larger
+    // graphs score in global memory), 0 when a fold range has no final fold
+    auto final_lds = [&](size_t i0, size_t i1) -> uint32_t {
+      uint32_t w = 0;
+      for (size_t i = i0; i < i1; ++i) {
+        const FoldJob& F = D.folds[i];
+        if (F.flags & kFoldFinal) w = std::max(w, (6 * (F.V + F.len) + 8 + 3) / 4);
+      }
+      return std::min(w, 16384u);
+    };
     const FoldJob* dfold = reinterpret_cast<const FoldJob*>(dd + s_fold);
     SVS_HIP(hipEventRecord(A.evp, side));
     if (npre) {
       // the new tasks' first reads, and their tables, before the DP kernel
-      SVS_HIP(launch_poa_fold(dfold, static_cast<int>(npre), lds_words, side));
+      SVS_HIP(launch_poa_fold(dfold, static_cast<int>(npre), lds_words, final_lds(0, npre), side));
       SVS_HIP(launch_dgraph_prep(dfold, static_cast<int>(npre), score, side));
     }
     SVS_HIP(hipEventRecord(A.evp1, side));
@@ -1149,7 +1200,7 @@ struct PoaScheduler::Impl {
     // graph update, sort, export and table completion beside the other group's DP
     SVS_HIP(hipEventRecord(A.evf0, side));
     if (nj) {
-      SVS_HIP(launch_poa_fold(dfold + npre, static_cast<int>(nj), lds_words, side));
+      SVS_HIP(launch_poa_fold(dfold + npre, static_cast<int>(nj), lds_words, final_lds(npre, npre + nj), side));
       SVS_HIP(launch_dgraph_prep(dfold + npre, static_cast<int>(nj), score, side));
     }
     SVS_HIP(hipEventRecord(A.evf1, side));
@@ -1251,6 +1302,7 @@ struct PoaScheduler::Impl {
       if (r.status == kFoldSkipped) continue;  // a pruning retry: graph and tables unchanged
       if (r.status != kFoldOk)
         throw SvsError(SVS_E_INTERNAL, "device POA graph fold failed (status " + std::to_string(r.status) + ")");
+      g_fold_times.add(r, F.flags);
       if (verify) verify_fold(g, i, r);
       if (i < D.n_pre) {
         // a chain: the counts the launch assumed for its second read
