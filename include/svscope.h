@@ -65,6 +65,8 @@ typedef struct svs_poa_stats {
   double fold_ms;           /* device-resident graphs: graph update + sort + export + table
                                completion (poa_fold.hip, poa_prep.hip) per launch, HIP events */
   uint64_t fold_jobs;       /* alignments (and first reads) folded into device-resident graphs */
+  uint64_t wide_launches;   /* DP launches with 32-bit traceback codes (a graph node with more
+                               than 31 in-edges) */
 } svs_poa_stats;
 
 /* One context per host thread; owns a HIP stream and device arenas. */

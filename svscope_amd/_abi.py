@@ -42,7 +42,7 @@ class PoaStats(ctypes.Structure):
                 ("wall_ms", ctypes.c_double), ("gpu_wait_ms", ctypes.c_double),
                 ("cells_computed", ctypes.c_uint64), ("prune_retries", ctypes.c_uint64),
                 ("prep_ms", ctypes.c_double), ("prep_jobs", ctypes.c_uint64),
-                ("fold_ms", ctypes.c_double), ("fold_jobs", ctypes.c_uint64)]
+                ("fold_ms", ctypes.c_double), ("fold_jobs", ctypes.c_uint64), ("wide_launches", ctypes.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

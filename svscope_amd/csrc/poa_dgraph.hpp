@@ -109,6 +109,7 @@ struct FoldResult {
   // consensus + MSA rows (SVS_POA_FOLD_TIMES prints their totals)
   uint32_t t_upd, t_sort, t_exp, t_fin;
   uint32_t n_exam, n_roots;  // DFS examinations and DFS starts of the sort
+  uint32_t prof[4];          // SVS_FOLD_PROF builds: DFS phase clocks / 1024
 };
 
 // One fold job: fold the job's alignment (or, with kFoldChain, the whole

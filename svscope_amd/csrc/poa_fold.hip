@@ -425,7 +425,13 @@ struct SortState {
   uint32_t spill_cap;  // entries the spill area holds
   bool err;            // the stack outgrew its spill area
   uint32_t n_exam, n_roots;  // statistics
+  uint64_t prof[4];          // SVS_FOLD_PROF: fast roots, DFS runs, window loads, rest (clocks)
 };
+#ifdef SVS_FOLD_PROF
+#define SVS_PF_CLK() __builtin_readcyclecounter()
+#else
+#define SVS_PF_CLK() 0ull
+#endif
 
 __device__ __forceinline__ bool bit_of(const uint32_t* plane, uint32_t v) { return (plane[v >> 5] >> (v & 31u)) & 1u; }
 
@@ -515,16 +521,53 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
     w0 = x.x; w1 = x.y; w2 = x.z; w3 = x.w;
     w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
   };
+  // Every node with an id below the current root is done (each root's DFS
+  // finishes all it pushed), so flags are only read for larger ids and a root
+  // whose tails and aligned nodes all have smaller ids is emitted at once,
+  // with no stack and no flag access (its own done bit is then never read).
+  // The root scan keeps its done word in a register while no DFS writes.
+  uint32_t dwi = kNone, dwv = 0;
   while (root < V && !S.err) {
-    const uint32_t fw = uni(~S.done[root >> 5]) >> (root & 31u);
+    if ((root >> 5) != dwi) {
+      dwi = root >> 5;
+      dwv = uni(S.done[dwi]);
+    }
+    const uint32_t fw = ~dwv >> (root & 31u);
     if (fw == 0) {
       root = (root | 31u) + 1u;
       continue;
     }
     root += static_cast<uint32_t>(__builtin_ctz(fw));
     if (root >= V) break;
-    push(root);
     ++S.n_roots;
+    const uint64_t pf0 = SVS_PF_CLK();
+    {
+      if (root - bR >= 64u) {
+        bR = root;
+        load_win(bR, r0, r1, r2, r3, r4, r5, r6, r7);
+      }
+      const uint32_t l = root - bR;
+      const uint32_t w1 = lane_val(r1, l), deg = w1 & 0xFFFFFFu, alc = w1 >> 24;
+      if (deg <= 3u) {
+        const uint32_t m0 = lane_val(r2, l), m1 = lane_val(r3, l), m2 = lane_val(r4, l);
+        const uint32_t t0 = lane_val(r5, l), t1 = lane_val(r6, l), t2 = lane_val(r7, l);
+        const bool fast = (deg < 1u || t0 < root) && (deg < 2u || t1 < root) && (deg < 3u || t2 < root) &&
+                          (alc < 1u || m0 < root) && (alc < 2u || m1 < root) && (alc < 3u || m2 < root);
+        if (fast) {
+          ++steps;
+          emit(root);
+          if (alc > 0u) emit(m0);
+          if (alc > 1u) emit(m1);
+          if (alc > 2u) emit(m2);
+          ++ncol;
+          ++root;
+          S.prof[0] += SVS_PF_CLK() - pf0;
+          continue;
+        }
+      }
+    }
+    dwi = kNone;  // the DFS below sets done bits
+    push(root);
     uint32_t cur = root;
     while (!S.err) {
       if (++steps > max_steps) {
@@ -544,6 +587,7 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
           bD = cur > 32u ? cur - 32u : 0u;
           load_win(bD, d0w, d1w, d2w, d3w, d4w, d5w, d6w, d7w);
         }
+        S.prof[2] += 1;
       }
       uint32_t off, w1, m0, m1, m2, t0, t1, t2;
       if (inR) {
@@ -558,13 +602,13 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
       const uint32_t deg = w1 & 0xFFFFFFu, alc = w1 >> 24;
       const uint32_t dc = uni(done_of(cur)), ig = uni(bit_of(S.ign, cur) ? 1u : 0u);
       // (unused slots read cur's word and count as done; they are never looked
-      // at: all eight reads issue together, one wait)
-      const uint32_t d0 = uni(done_of(deg > 0 ? t0 : cur) | (deg > 0 ? 0u : 1u));
-      const uint32_t d1 = uni(done_of(deg > 1 ? t1 : cur) | (deg > 1 ? 0u : 1u));
-      const uint32_t d2 = uni(done_of(deg > 2 ? t2 : cur) | (deg > 2 ? 0u : 1u));
-      const uint32_t e0 = uni(done_of(alc > 0 ? m0 : cur) | (alc > 0 ? 0u : 1u));
-      const uint32_t e1 = uni(done_of(alc > 1 ? m1 : cur) | (alc > 1 ? 0u : 1u));
-      const uint32_t e2 = uni(done_of(alc > 2 ? m2 : cur) | (alc > 2 ? 0u : 1u));
+      // at: all eight reads issue together, one wait; ids below the root are
+      // done)
+      auto dn = [&](bool used, uint32_t v) -> uint32_t {
+        return uni(done_of(used ? v : cur) | (used && v >= root ? 0u : 1u));
+      };
+      const uint32_t d0 = dn(deg > 0, t0), d1 = dn(deg > 1, t1), d2 = dn(deg > 2, t2);
+      const uint32_t e0 = dn(alc > 0, m0), e1 = dn(alc > 1, m1), e2 = dn(alc > 2, m2);
       bool pop = dc != 0;
       if (!pop) {
         bool valid = true;
@@ -574,8 +618,8 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
             t = x == 0 ? t0 : (x == 1 ? t1 : t2);
             dt = x == 0 ? d0 : (x == 1 ? d1 : d2);
           } else {
-            t = in_nbr[off + x];
-            dt = uni(done_of(t));
+            t = uni(in_nbr[off + x]);
+            dt = t < root ? 1u : uni(done_of(t));
           }
           if (!dt) {
             push(t);
@@ -611,6 +655,7 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
       }
       cur = uni(S.st[S.sp - 1]);
     }
+    S.prof[1] += SVS_PF_CLK() - pf0;
     ++root;
   }
   *ncol_out = ncol;
@@ -647,7 +692,7 @@ __device__ void export_lite(uint32_t V, const gu8* __restrict__ base, const gu32
     if (r < V) {
       pstart[r] = o;
       const bool sink = out_off[node + 1] == out_off[node];
-      info[r] = static_cast<uint32_t>(base[node]) | (sink ? 0x100u : 0u) | (d << 10);
+      info[r] = static_cast<uint32_t>(base[node]) | (sink ? 0x100u : 0u) | (min(d, 63u) << 10);  // 63: >= 63
       for (uint32_t k = 0; k < d; ++k) {
         const uint32_t pr = n2r[in_nbr[a + k]];
         pred[o + k] = pr + 1;
@@ -907,6 +952,7 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
   S.err = false;
   S.n_exam = 0;
   S.n_roots = 0;
+  S.prof[0] = S.prof[1] = S.prof[2] = S.prof[3] = 0;
   uint32_t ncol = 0;
   if (S.cap < 64) {
     if (lanei() == 0) res->status = kFoldErrStack;
@@ -944,6 +990,7 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
     res->t_exp = static_cast<uint32_t>(T2 - T1);
     res->n_exam = S.n_exam;
     res->n_roots = S.n_roots;
+    for (int k = 0; k < 4; ++k) res->prof[k] = static_cast<uint32_t>(S.prof[k] >> (k == 2 ? 0 : 10));
   }
 }
 
@@ -1022,6 +1069,21 @@ hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, 
   if (final_lds_words)
     hipLaunchKernelGGL(poa_fold_final_kernel, dim3(n_jobs), dim3(64), final_lds_words * 4, stream, jobs,
                        final_lds_words);
+  return hipGetLastError();
+}
+
+// The new tasks' read blocks from the launch's staging into their own blocks:
+// one workgroup per copy, 16-byte words.
+__global__ __launch_bounds__(256) void scatter_copy_kernel(const CopyDesc* __restrict__ d) {
+  const CopyDesc c = d[blockIdx.x];
+  const u32x4* __restrict__ s = reinterpret_cast<const u32x4*>(c.src);
+  u32x4* __restrict__ t = reinterpret_cast<u32x4*>(c.dst);
+  for (uint64_t k = threadIdx.x; k < c.bytes / 16; k += blockDim.x) t[k] = s[k];
+}
+
+hipError_t launch_scatter_copy(const CopyDesc* d, int n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_copy_kernel, dim3(n), dim3(256), 0, stream, d);
   return hipGetLastError();
 }
 

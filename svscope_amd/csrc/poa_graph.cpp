@@ -331,7 +331,7 @@ void PoaGraph::export_strip_rows(RowTables* t, const int32_t* gaps, const StripD
     const uint32_t a = pstart[r], b = pstart[r + 1];
     uint32_t* w = rec + static_cast<size_t>(r) * kRecWords;
     w[0] = static_cast<uint8_t>(base_[node]) | (out_[node].empty() ? 0x100u : 0u) | (store ? 0x200u : 0u) |
-           ((b - a) << 10) | (own << 16);
+           (std::min<uint32_t>(b - a, 63u) << 10) | (own << 16);  // in-degree 63: >= 63 (pstart has it)
     uint32_t w1 = 0, w3 = 0;  // a source's in-edge comes from the virtual row 0 (slot 0)
     for (uint32_t x = a; x < b; ++x) {
       const uint32_t pr = pred_row[x] - 1;
@@ -398,7 +398,8 @@ void PoaGraph::export_strip_lite(RowTables* t, const StripLiteDst* dst) const {
       pred_row[k++] = pr + 1;
       if (pr + 1 != r && last[pr] < r + 1) last[pr] = r + 1;
     }
-    info[r] = static_cast<uint8_t>(base_[node]) | (out_[node].empty() ? 0x100u : 0u) | (in.size() << 10);
+    info[r] = static_cast<uint8_t>(base_[node]) | (out_[node].empty() ? 0x100u : 0u) |
+              (std::min<uint32_t>(static_cast<uint32_t>(in.size()), 63u) << 10);
   }
   pstart[V] = k;
   t->max_preds = max_preds;

@@ -280,7 +280,7 @@ __global__ __launch_bounds__(192) void poa_dgraph_prep_kernel(const FoldJob* __r
   const FoldResult* res = J.result;
   if (uni(static_cast<uint32_t>(res->status)) != static_cast<uint32_t>(kFoldOk)) return;
   const uint32_t V = uni(res->V);
-  if (V == 0 || V > kStripPrepMaxRows || uni(res->n_slots) > kStripPrepMaxSlots || uni(res->max_preds) > 31u) return;
+  if (V == 0 || V > kStripPrepMaxRows || uni(res->n_slots) > kStripPrepMaxSlots || uni(res->max_preds) > kMaxInEdges) return;
   const DGraphLayout L = dgraph_layout(J.cv, J.ce);
   uint8_t* b = J.blk;
   strip_prep_job(P, V, 1u, reinterpret_cast<const uint32_t*>(b + L.pstart), reinterpret_cast<const uint32_t*>(b + L.pred),

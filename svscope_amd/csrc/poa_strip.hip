@@ -179,7 +179,7 @@ __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, 
 // ...; strip s reads the carries wave (w-1) mod WPJ left for strip s-1, which
 // it publishes every 8 rows through an LDS progress counter (workgroup-scope
 // release / acquire), so the waves form a row-skewed pipeline over strips.
-template <bool LDSP, int WPJ, bool PRUNE>
+template <bool LDSP, int WPJ, bool PRUNE, class CodeT>
 // The pruning variant is held to 80 VGPRs (6 waves per SIMD; a few spills to
 // scratch in cold paths): measured faster than its natural 86 (5 waves),
 // profiles/r01_v36.  SVS_PRUNE_OCC overrides it in development builds.
@@ -189,9 +189,10 @@ template <bool LDSP, int WPJ, bool PRUNE>
 #define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? SVS_PRUNE_OCC : 1)))
 __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore Parg,
-    uint16_t* __restrict__ tb, int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
+    CodeT* __restrict__ tb, int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
     int32_t* __restrict__ gpool, int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
   extern __shared__ int32_t lds[];
+  using TF = TbFmt<CodeT>;
   const PoaScore P = Parg;
   __shared__ int32_t prog[WPJ];  // per wave: strip * (V + 1) + rows done, carries published
   __shared__ int32_t s_err;
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   int32_t* __restrict__ pool;  // this wave's pool: nslot x {H, F, O} x 64, then nslot boundary H
   if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * kStride;
   else pool = gpool + J.pool_off + static_cast<uint64_t>(wave) * ((nslot * kSlotInts + 63) / 64 * 64);
-  uint16_t* __restrict__ tbj = tb + J.tb_off;
+  CodeT* __restrict__ tbj = tb + J.tb_off;
   const GLB uint32_t* __restrict__ rec = glb(J.rec);
   const GLB uint32_t* __restrict__ rps = glb(J.pstart);
   const GLB uint32_t* __restrict__ prow = glb(J.pred);
@@ -265,7 +266,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const int32_t j0 = s << 6;
     const int32_t j = j0 + lane;
     const uint8_t rc = seq[j - 1];  // seq[-1] is a zero pad byte (column 0)
-    uint16_t* __restrict__ tbl = tbj + j;  // this lane's column of the traceback codes
+    CodeT* __restrict__ tbl = tbj + j;  // this lane's column of the traceback codes
     const GLB int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
     int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
     const int32_t pw = (wave + WPJ - 1) % WPJ;          // producer of strip s-1
@@ -358,7 +359,9 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       const uint32_t nb = w0 & 0xFFu;
       const bool sink = (w0 >> 8) & 1u;
       const bool store = (w0 >> 9) & 1u;
-      const uint32_t np = (w0 >> 10) & 31u;
+      // in-degree: 6 bits of w0 (63: at least 63); launches with wide codes
+      // count it from pstart
+      const uint32_t np = sizeof(CodeT) == 4 ? rps[r + 1] - rps[r] : (w0 >> 10) & 63u;
       const uint32_t own = w0 >> 16;
       // slots >= 31 have no liveness bit (only jobs without a bound of their
       // own, kPruneAll, have them): always alive
@@ -496,9 +499,9 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const uint32_t upc = (ua || (!ub && uc)) ? 5u : 1u;
         const uint32_t lfc = (la || (!lb && lc)) ? 6u : 2u;
         code = dg ? 0u : (up ? upc : (lf ? lfc : 3u));
-        code |= lbit ? 0x100u : 0u;
-        if (np != 0) code |= (va || (!vb && vc)) ? 0x200u : 0u;
-        else code |= 31u << 10;
+        code |= lbit ? 1u << TF::kLBit : 0u;
+        if (np != 0) code |= (va || (!vb && vc)) ? 1u << TF::kStop : 0u;
+        else code |= TF::kMask << TF::kUc;
         }
       } else if (!FIRST && np == 2) {
         // Two in-edges (the common merge row), both kept in registers between
@@ -530,8 +533,8 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const uint32_t upc = ((ua || (!ub && uc)) ? 5u : 1u) | (up0 ? 0u : 8u);
         const uint32_t lfc = (la || (!lb && lc)) ? 6u : 2u;
         code = H == D0 ? 0u : (H == D1 ? 8u : (up0 || up1 ? upc : (lf ? lfc : 3u)));
-        code |= lbit ? 0x100u : 0u;
-        code |= ((va || (!vb && vc)) ? 0x200u : 0u) | (ch0 ? 0u : (1u << 10));
+        code |= lbit ? 1u << TF::kLBit : 0u;
+        code |= ((va || (!vb && vc)) ? 1u << TF::kStop : 0u) | (ch0 ? 0u : (1u << TF::kUc));
       } else {
         const GLB uint32_t* __restrict__ spill = pslot + rps[r];
         F = SVS_VNEG;
@@ -548,17 +551,17 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         if (c0) { F = F0; O = O0; }
         const int32_t Hpre = c0 ? H0 : imax(Hd, imax(F, O));
         gaps(Hpre, inner);
-        uint32_t diag_k = 31, up_k = 31, up_ext = 0, uc_k = 31, uc_stop = 0;
+        uint32_t diag_k = TF::kMask, up_k = TF::kMask, up_ext = 0, uc_k = TF::kMask, uc_stop = 0;
         for (uint32_t k = 0; k < np; ++k) {
           int32_t hp, fp, op, hpm;
           pred_vals(__builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hp, fp, op, hpm);
           if (FIRST) hpm = c0 ? 0 : hpm;
-          if (inner && diag_k == 31 && H == hpm + mc) diag_k = k;
-          if (up_k == 31) {
+          if (inner && diag_k == TF::kMask && H == hpm + mc) diag_k = k;
+          if (up_k == TF::kMask) {
             const bool a = H == fp + P.e, b = H == hp + P.g, c = H == op + P.c, dd = H == hp + P.q;
             if (a || b || c || dd) { up_k = k; up_ext = (a || (!b && c)) ? 1u : 0u; }
           }
-          if (uc_k == 31) {
+          if (uc_k == TF::kMask) {
             const bool a = F == hp + P.g, b = F == fp + P.e, c = O == hp + P.q, dd = O == op + P.c;
             if (a || b || c || dd) { uc_k = k; uc_stop = (a || (!b && c)) ? 1u : 0u; }
           }
@@ -566,11 +569,11 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const bool la = inner && H == prevEe, lb = inner && H == prevH + P.g;
         const bool lc = inner && H == prevQc, ld = inner && H == prevH + P.q;
         const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
-        code = assemble_code(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k, uc_stop);
+        code = assemble_code<TF>(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k, uc_stop);
       }
       // 32-bit row offset off this lane's column: the host keeps n_rows x ls
       // below 2^31 per job
-      tbl[r * LS] = static_cast<uint16_t>(code);
+      tbl[r * LS] = static_cast<CodeT>(code);
       bool any_alive = true;
       if (prune) {
         const int32_t ub = ub_of(w2w3.x, rrem, mrr);
@@ -631,7 +634,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         } else {
           if (in) cand = __builtin_nontemporal_load(bin + 4ull * rr + 3) > SVS_VNEG / 2;
         }
-        if ((alive & 1u) && in) cand = cand || ((rec[static_cast<uint64_t>(rr) * kRecWords] >> 10) & 31u) == 0;
+        if ((alive & 1u) && in) cand = cand || ((rec[static_cast<uint64_t>(rr) * kRecWords] >> 10) & 63u) == 0;
         const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
         const uint32_t n = m ? static_cast<uint32_t>(__builtin_ctzll(m)) : lim;
         if (write_bnd && static_cast<uint32_t>(lane) < n)
@@ -806,7 +809,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       out[2 * n + 1] = b;
     }
   };
-  const int32_t nout = poa_traceback(P, V, L, best_row, tbc, pred_of, emit);
+  const int32_t nout = poa_traceback<TF>(P, V, L, best_row, tbc, pred_of, emit);
   if (lane == 0) aln_len[job_id] = nout;
 }
 
@@ -815,10 +818,18 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   const int w = a.waves_per_job;
   const bool lds_pool = a.lds_slots > 0;
   const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * kStripSlotBytes : 0;
-#define SVS_STRIP3(LP, W, PR)                                                                                     \
-  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, a.n_jobs,  \
-                     a.score, a.tb, a.bnd, a.bnd,                                                                    \
-                     a.pool, a.aln, a.aln_len, a.lds_slots)
+#define SVS_STRIP4(LP, W, PR, CT)                                                                              \
+  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR, CT>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs,     \
+                     a.n_jobs, a.score, static_cast<CT*>(a.tb), a.bnd, a.bnd, a.pool, a.aln, a.aln_len,            \
+                     a.lds_slots)
+#define SVS_STRIP3(LP, W, PR)              \
+  do {                                     \
+    if (a.wide) {                          \
+      SVS_STRIP4(LP, W, PR, uint32_t);     \
+    } else {                               \
+      SVS_STRIP4(LP, W, PR, uint16_t);     \
+    }                                      \
+  } while (0)
 #define SVS_STRIP(LP, W)              \
   do {                                \
     if (a.prune) {                    \
@@ -848,6 +859,7 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   }
 #undef SVS_STRIP
 #undef SVS_STRIP3
+#undef SVS_STRIP4
   return hipGetLastError();
 }
 

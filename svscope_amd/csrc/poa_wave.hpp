@@ -115,22 +115,34 @@ __device__ __forceinline__ void strip_gaps(const PoaScore& P, int lane, int32_t 
   cr.cH = imax(hl, imax(cr.cE, cr.cQ));
 }
 
-// Traceback code of one DP cell (uint16; the strip kernel writes one per
-// evaluated cell, the backtrack below reads nothing else):
+// Traceback code of one DP cell (the strip kernel writes one per evaluated
+// cell, the backtrack below reads nothing else).  Narrow (uint16, graphs
+// whose nodes have at most 31 in-edges):
 //   bits 0-1  main move: 0 diagonal, 1 up, 2 left, 3 none
 //   bit  2    extend flag of the main move (extend_up / extend_left)
 //   bits 3-7  in-edge index of the main move (diag/up)
 //   bit  8    left-gap run opened here:  H[j-1]+g==E[j] || H[j-1]+q==Q[j]
 //   bit  9    up-gap run stop flag
 //   bits 10-14 in-edge index continuing an up-gap run (31 = none)
-// Assembly from the per-in-edge tests (branch-free selects).
+// Wide (uint32, up to 4094 in-edges: large windows): in-edge indices of 12
+// bits at 3-14 and 17-28 (4095 = none), the flags at bits 15 and 16.
+template <class CodeT> struct TbFmt;
+template <> struct TbFmt<uint16_t> {
+  static constexpr uint32_t kMask = 31, kLBit = 8, kStop = 9, kUc = 10, kMaxPreds = 31;
+};
+template <> struct TbFmt<uint32_t> {
+  static constexpr uint32_t kMask = 4095, kLBit = 15, kStop = 16, kUc = 17, kMaxPreds = 4094;
+};
+
+// Assembly from the per-in-edge tests (branch-free selects); kMask = none.
+template <class F>
 __device__ __forceinline__ uint32_t assemble_code(uint32_t diag_k, uint32_t up_k, uint32_t up_ext, bool left_ok,
                                                   bool left_ext, bool lbit, uint32_t uc_k, uint32_t uc_stop) {
   const uint32_t left = left_ok ? (2u | (left_ext ? 4u : 0u)) : 3u;
   const uint32_t up = 1u | (up_ext << 2) | (up_k << 3);
-  uint32_t code = up_k != 31 ? up : left;
-  code = diag_k != 31 ? (diag_k << 3) : code;
-  return code | ((lbit ? 1u : 0u) << 8) | (uc_stop << 9) | (uc_k << 10);
+  uint32_t code = up_k != F::kMask ? up : left;
+  code = diag_k != F::kMask ? (diag_k << 3) : code;
+  return code | ((lbit ? 1u : 0u) << F::kLBit) | (uc_stop << F::kStop) | (uc_k << F::kUc);
 }
 
 // Lane-0 traceback (spoa SisdAlignmentEngine backtrack order, kNW convex)
@@ -140,7 +152,7 @@ __device__ __forceinline__ uint32_t assemble_code(uint32_t diag_k, uint32_t up_k
 // pair n.  Returns the pair count, or -1 for an inconsistent path.  Control
 // flow depends only on its arguments and on tbc / pred_of results, so a whole
 // wave may run it in lockstep (the strip kernel's tile-cached codes).
-template <class Tbc, class PredOf, class Emit>
+template <class F, class Tbc, class PredOf, class Emit>
 __device__ int32_t poa_traceback(const PoaScore& P, uint32_t V, int32_t L, int32_t best_row, Tbc tbc,
                                  PredOf pred_of, Emit emit) {
   const int64_t cap = static_cast<int64_t>(V) + L + 1;
@@ -159,7 +171,7 @@ __device__ int32_t poa_traceback(const PoaScore& P, uint32_t V, int32_t L, int32
       pj = jj - 1;
     } else {
       const uint32_t code = tbc(i, jj);
-      const uint32_t t = code & 3u, k = (code >> 3) & 31u;
+      const uint32_t t = code & 3u, k = (code >> 3) & F::kMask;
       if (t == 0) { pi = pred_of(i, k); pj = jj - 1; }
       else if (t == 1) { pi = pred_of(i, k); eu = (code >> 2) & 1u; }
       else if (t == 2) { pj = jj - 1; el = (code >> 2) & 1u; }
@@ -180,7 +192,7 @@ __device__ int32_t poa_traceback(const PoaScore& P, uint32_t V, int32_t L, int32
         if (i == 0) {
           stop = row0_h(P, jj) + P.g == row0_e(P, jj + 1) || row0_h(P, jj) + P.q == row0_q(P, jj + 1);
         } else {
-          stop = (tbc(i, jj + 1) >> 8) & 1u;
+          stop = (tbc(i, jj + 1) >> F::kLBit) & 1u;
         }
         if (stop) break;
       }
@@ -188,9 +200,9 @@ __device__ int32_t poa_traceback(const PoaScore& P, uint32_t V, int32_t L, int32
       while (true) {
         if (n >= cap || i <= 0) { ok = false; break; }
         const uint32_t code = tbc(i, jj);
-        const uint32_t k = (code >> 10) & 31u;
-        const bool stop = (code >> 9) & 1u;
-        const int32_t nxt = (k == 31u) ? 0 : pred_of(i, k);
+        const uint32_t k = (code >> F::kUc) & F::kMask;
+        const bool stop = (code >> F::kStop) & 1u;
+        const int32_t nxt = (k == F::kMask) ? 0 : pred_of(i, k);
         emit(n, i - 1, -1);
         ++n;
         i = nxt;

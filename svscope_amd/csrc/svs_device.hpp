@@ -47,7 +47,7 @@ struct PoaLaunch {
   const PoaJob* jobs;
   int n_jobs;
   PoaScore score;
-  uint16_t* tb;
+  void* tb;              // traceback codes: uint16 (wide: uint32) per cell
   int32_t* bnd;          // strip-boundary carries
   int32_t* pool;         // global row pools
   int32_t* aln;
@@ -56,7 +56,21 @@ struct PoaLaunch {
   int waves_per_job;     // strip-pipeline waves per job: 1, 2, 4, 8 (16 with the pool in LDS)
   uint32_t lds_slots;    // pool slots per wave held in LDS (max n_slots of the launch)
   bool prune;            // some job has a pruning bound: the pruning kernel variant
+  bool wide;             // some row has more than 31 in-edges: 32-bit codes (TbFmt, poa_wave.hpp)
 };
+
+// One block copy of launch_scatter_copy (bytes a multiple of 64, both ends
+// 64-byte aligned).
+struct CopyDesc {
+  const char* src;
+  uint8_t* dst;
+  uint64_t bytes;
+};
+hipError_t launch_scatter_copy(const CopyDesc* d, int n, hipStream_t stream);
+
+// In-edges per graph node the traceback codes can name: 31 with 16-bit codes,
+// 4094 with 32-bit ones (launches with such a node; TbFmt, poa_wave.hpp).
+constexpr uint32_t kMaxInEdgesNarrow = 31, kMaxInEdges = 4094;
 
 // Row stride of a strip job: len + 1 rounded up to whole 64-column strips.
 inline uint32_t strip_ls(uint32_t len) { return (len + 1 + 63) / 64 * 64; }

@@ -63,6 +63,7 @@ struct Launch {
   PoaArena* arena = nullptr;
   int wpj = 0;
   int gid = 0;
+  int code_bytes = 2;    // traceback code width of the launch (4: a node with > 31 in-edges)
   size_t prep_jobs = 0;  // jobs whose tables the device completed (poa_prep.hip)
   int32_t gaps[4] = {0, 0, 0, 0};  // g, e, q, c of the launch (SVS_POA_VERIFY_PREP)
 };
@@ -211,7 +212,7 @@ bool export_direct(PoaTask& t, const int32_t* gaps, PoaArena& A) {
     const StripLiteDst dst{reinterpret_cast<uint32_t*>(base + b.pstart), reinterpret_cast<uint32_t*>(base + b.pred_row),
                            reinterpret_cast<uint32_t*>(base + b.info)};
     t.graph.export_strip_lite(&t.rows, &dst);
-    if (t.rows.n_slots <= kStripPrepMaxSlots && t.rows.max_preds <= 31) {
+    if (t.rows.n_slots <= kStripPrepMaxSlots && t.rows.max_preds <= kMaxInEdges) {
       write_read(base + b.seq, s, ls);
       t.rows_at = 2;
       t.blk_off = off;
@@ -236,13 +237,22 @@ bool export_direct(PoaTask& t, const int32_t* gaps, PoaArena& A) {
   return true;
 }
 
-uint64_t job_bytes(const RowTables& tt, uint64_t L, const KernelEnv& ke) {
+// SVS_POA_FORCE_WIDE=1 (tests): every DP launch with 32-bit traceback codes
+// (read per launch: tests set it between calls)
+bool force_wide() {
+  const char* e = std::getenv("SVS_POA_FORCE_WIDE");
+  return e && std::atoi(e) != 0;
+}
+
+// code_bytes: the launch's traceback code width (4 when some job of it has a
+// node with more than 31 in-edges)
+uint64_t job_bytes(const RowTables& tt, uint64_t L, const KernelEnv& ke, uint64_t code_bytes) {
   const uint64_t ls = strip_ls(static_cast<uint32_t>(L)), V = tt.n_rows;
   // traceback codes + two strip-boundary carry buffers (+ a global pool when
   // the graph needs more slots than the LDS pool holds)
   const uint64_t pool = (tt.n_slots > kStripMaxLdsSlots || ke.global_pool)
                             ? 8ull * round_up(static_cast<uint64_t>(tt.n_slots) * 97, 64) * 4 : 0;
-  return V * ls * 2 + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
+  return V * ls * code_bytes + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
 }
 
 void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks);
@@ -325,8 +335,11 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     max_preds = std::max(max_preds, tt.max_preds);
     st.dp_cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);
   }
-  if (max_preds > 31)
-    throw SvsError(SVS_E_UNSUPPORTED, "a graph node has more than 31 in-edges (traceback code limit)");
+  if (max_preds > kMaxInEdges)
+    throw SvsError(SVS_E_UNSUPPORTED, "a graph node has more than 4094 in-edges (traceback code limit)");
+  const bool wide = max_preds > kMaxInEdgesNarrow || force_wide();
+  la.code_bytes = wide ? 4 : 2;
+  st.wide_launches += wide ? 1 : 0;
   // the pruning variant prunes every job of its launch: the others get no bound
   if (any_prune)
     for (PoaJob& J : la.jobs)
@@ -413,7 +426,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   A.d_in.ensure(dev_end);
   // the traceback codes dominate a launch's footprint: sized to the group's
   // budget at the first launch, so it never regrows (and syncs) mid-run
-  A.d_tb.ensure(n_tb * 2 + 4096, ctx->device_budget / 2);
+  A.d_tb.ensure(n_tb * la.code_bytes + 4096, ctx->device_budget / 2);
   A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096);
   A.d_aln.ensure(n_aln * 8);
   A.d_alen.ensure(nj * 12);
@@ -459,13 +472,14 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
   pl.n_jobs = static_cast<int>(nj);
   pl.score = score;
-  pl.tb = A.d_tb.as<uint16_t>();
+  pl.tb = A.d_tb.as<char>();
   pl.bnd = A.d_pool.as<int32_t>();
   pl.pool = A.d_pool.as<int32_t>() + n_bnd;
   pl.aln = A.d_aln.as<int32_t>();
   pl.aln_len = A.d_alen.as<int32_t>();
   pl.lds_slots = lds_pool ? max_slots : 0;
   pl.prune = any_prune;
+  pl.wide = la.code_bytes == 4;
   pl.waves_per_job = wpj;
   la.wpj = wpj;
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
@@ -666,13 +680,14 @@ struct FoldTimes {
     return e && std::atoi(e) != 0;
   }();
   double upd = 0, sort = 0, exp = 0, fin = 0, max_sort = 0, max_fin = 0;
-  uint64_t n = 0, n_exp = 0, n_fin = 0, verts = 0, exams = 0, roots = 0;
+  uint64_t n = 0, n_exp = 0, n_fin = 0, verts = 0, exams = 0, roots = 0, prof[4] = {0, 0, 0, 0};
   void add(const FoldResult& r, uint32_t flags) {
     if (!on) return;
     ++n;
     verts += r.V;
     exams += r.n_exam;
     roots += r.n_roots;
+    for (int k = 0; k < 4; ++k) prof[k] += r.prof[k];
     upd += r.t_upd * 1e-5;
     sort += r.t_sort * 1e-5;
     max_sort = std::max(max_sort, r.t_sort * 1e-5);
@@ -695,6 +710,9 @@ struct FoldTimes {
                  static_cast<unsigned long long>(n_exp), n_exp ? exp / n_exp : 0.0,
                  static_cast<unsigned long long>(n_fin), n_fin ? fin / n_fin : 0.0, max_fin, double(exams) / n,
                  double(roots) / n);
+    if (prof[0] || prof[1])
+      std::fprintf(stderr, "[svs] DFS profile per fold: fast roots %.0f kclk, DFS runs %.0f kclk, %.1f window loads\n",
+                   double(prof[0]) * 1.024 / n, double(prof[1]) * 1.024 / n, double(prof[2]) / n);
   }
 };
 FoldTimes g_fold_times;
@@ -784,9 +802,11 @@ struct PoaScheduler::Impl {
   // ------------------------------------------------ device-resident graphs
   // A task's reads (each as the DP kernel reads it: a zero pad byte, the read,
   // zeros up to ls + 64), the path offsets of its non-empty reads and room for
-  // their node paths: one block, uploaded once (from the launch's pinned
-  // staging, `up`), read by every DP and fold of the task.
-  void activate_dev(PoaTask& t, std::vector<char>& up, std::vector<std::pair<size_t, PoaTask*>>& uploads) {
+  // their node paths: one block, uploaded once (through the launch's pinned
+  // staging), read by every DP and fold of the task.  plan_static lays the
+  // block out and allocates it; returns the bytes of its host image (reads +
+  // path offsets; the paths are written by the folds).
+  size_t plan_static(PoaTask& t) {
     const size_t n = t.seqs.size();
     t.seq_at.assign(n, 0);
     size_t o = 64;
@@ -808,22 +828,22 @@ struct PoaScheduler::Impl {
     t.d_static = static_cast<uint8_t*>(darena->alloc(t.static_bytes));
     t.d_path_off = reinterpret_cast<uint32_t*>(t.d_static + po);
     t.d_paths = reinterpret_cast<uint32_t*>(t.d_static + pa);
-    // host image of the reads + path offsets (the paths are written by the folds)
-    const size_t at = up.size();
-    up.resize(at + pa);
-    char* h = up.data() + at;
-    std::memset(h, 0, pa);
-    for (size_t k = 0; k < n; ++k)
+    return pa;
+  }
+  // The host image of plan_static's block (`bytes` of it) at h.
+  static void write_static(const PoaTask& t, char* h, size_t bytes) {
+    const size_t po = static_cast<size_t>(reinterpret_cast<const uint8_t*>(t.d_path_off) - t.d_static);
+    std::memset(h, 0, bytes);
+    for (size_t k = 0; k < t.seqs.size(); ++k)
       if (!t.seqs[k].empty()) std::memcpy(h + t.seq_at[k], t.seqs[k].data(), t.seqs[k].size());
     uint32_t* poff = reinterpret_cast<uint32_t*>(h + po);
     uint32_t acc = 0, i = 0;
-    for (size_t k = 0; k < n; ++k)
-      if (!t.seqs[k].empty()) {
+    for (const std::string& q : t.seqs)
+      if (!q.empty()) {
         poff[i++] = acc;
-        acc += static_cast<uint32_t>(t.seqs[k].size());
+        acc += static_cast<uint32_t>(q.size());
       }
     poff[i] = acc;
-    uploads.emplace_back(at, &t);
   }
 
   void release_dev(PoaTask& t) {
@@ -897,11 +917,13 @@ struct PoaScheduler::Impl {
       // the rest wait for the next launch)
       order_by_cost(dp);
       const KernelEnv ke;
-      uint64_t total = 0;
+      uint64_t total = 0, code_bytes = force_wide() ? 4 : 2;
+      for (uint32_t id : dp)
+        if (tasks[id].max_preds_next > kMaxInEdgesNarrow) code_bytes = 4;
       size_t fit = 0;
       for (; fit < dp.size(); ++fit) {
         const PoaTask& t = tasks[dp[fit]];
-        const uint64_t b = job_bytes_dev(t, ke);
+        const uint64_t b = job_bytes_dev(t, ke, code_bytes);
         if (fit > 0 && total + b > budget) break;
         total += b;
       }
@@ -914,11 +936,11 @@ struct PoaScheduler::Impl {
     }
   }
 
-  uint64_t job_bytes_dev(const PoaTask& t, const KernelEnv& ke) const {
+  uint64_t job_bytes_dev(const PoaTask& t, const KernelEnv& ke, uint64_t code_bytes) const {
     const uint64_t L = t.seqs[t.next].size(), ls = strip_ls(static_cast<uint32_t>(L)), V = t.dg.V;
     const uint64_t pool = (t.n_slots_next > kStripMaxLdsSlots || ke.global_pool)
                               ? 8ull * round_up(static_cast<uint64_t>(t.n_slots_next) * 97, 64) * 4 : 0;
-    return V * ls * 2 + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
+    return V * ls * code_bytes + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
   }
 
   void pack_and_launch_dev(Group& g, const std::vector<uint32_t>& dp, const std::vector<uint32_t>& chain,
@@ -934,11 +956,18 @@ struct PoaScheduler::Impl {
     D.fold_seq = chain_seq;
     for (uint32_t id : dp) D.fold_seq.push_back(static_cast<uint32_t>(tasks[id].next));
     const size_t nj = dp.size(), nf = D.fold_ids.size(), npre = D.n_pre;
-    // reads of the tasks that start with this launch
-    std::vector<char> up;
-    std::vector<std::pair<size_t, PoaTask*>> uploads;
+    // reads of the tasks that start with this launch: blocks planned here,
+    // images written straight into the pinned staging below
+    std::vector<std::pair<size_t, PoaTask*>> uploads;  // staging offset (from s_up), task
+    std::vector<size_t> up_bytes;
+    size_t up_total = 0;
     for (uint32_t id : D.fold_ids)
-      if (!tasks[id].d_static) activate_dev(tasks[id], up, uploads);
+      if (!tasks[id].d_static) {
+        const size_t b = plan_static(tasks[id]);
+        uploads.emplace_back(up_total, &tasks[id]);
+        up_bytes.push_back(b);
+        up_total += round_up(b, 64);
+      }
     // a fresh block for each chain, sized for the chain and its next read's
     // fold in this same launch
     for (size_t i = 0; i < npre; ++i) {
@@ -956,12 +985,13 @@ struct PoaScheduler::Impl {
     D.jobs.assign(nj, PoaJob{});
     uint64_t n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
     uint32_t max_slots = 1, min_strips = 0xFFFFFFFFu;
-    bool any_prune = false;
+    bool any_prune = false, wide = force_wide();
     for (uint32_t id : dp) {
       const PoaTask& t = tasks[id];
       if (!t.tables_ok) throw SvsError(SVS_E_INTERNAL, "device graph: no row tables for the next read");
-      if (t.max_preds_next > 31)
-        throw SvsError(SVS_E_UNSUPPORTED, "a graph node has more than 31 in-edges (traceback code limit)");
+      if (t.max_preds_next > kMaxInEdges)
+        throw SvsError(SVS_E_UNSUPPORTED, "a graph node has more than 4094 in-edges (traceback code limit)");
+      wide = wide || t.max_preds_next > kMaxInEdgesNarrow;
       max_slots = std::max(max_slots, t.n_slots_next);
       min_strips = std::min(min_strips, strip_ls(static_cast<uint32_t>(t.seqs[t.next].size())) / 64);
     }
@@ -1005,7 +1035,8 @@ struct PoaScheduler::Impl {
         if (J.lb == kNoPrune) J.lb = kPruneAll;
     D.n_aln = n_aln;
     D.wpj = wpj;
-    A.d_tb.ensure(n_tb * 2 + 4096, ctx->device_budget / 2);
+    st.wide_launches += wide ? 1 : 0;
+    A.d_tb.ensure(n_tb * (wide ? 4 : 2) + 4096, ctx->device_budget / 2);
     A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096);
     A.d_aln.ensure(n_aln * 8 + 64);
     A.d_alen.ensure(nj * 12 + 64);
@@ -1091,10 +1122,12 @@ struct PoaScheduler::Impl {
     }
     D.fin_bytes = fin;
     // descriptors: DP jobs, fold jobs, fold results; then the new tasks' reads
+    // and the scatter list that copies them into their blocks
     const size_t s_fold = round_up(nj * sizeof(PoaJob), 256);
     const size_t s_res = round_up(s_fold + nf * sizeof(FoldJob), 256);
     const size_t s_up = round_up(s_res + nf * sizeof(FoldResult), 256);
-    const size_t total = s_up + up.size();
+    const size_t s_cp = round_up(s_up + up_total, 256);
+    const size_t total = s_cp + uploads.size() * sizeof(CopyDesc);
     D.s_fold = s_fold;
     D.s_res = s_res;
     A.h_desc.ensure(total);
@@ -1122,16 +1155,19 @@ struct PoaScheduler::Impl {
       r.status = kFoldNotRun;  // only the update kernel makes it kFoldOk
       std::memcpy(hd + s_res + i * sizeof(FoldResult), &r, sizeof(r));
     }
-    if (!up.empty()) std::memcpy(hd + s_up, up.data(), up.size());
+    CopyDesc* cps = reinterpret_cast<CopyDesc*>(hd + s_cp);
+    for (size_t u = 0; u < uploads.size(); ++u)
+      cps[u] = CopyDesc{dd + s_up + uploads[u].first, uploads[u].second->d_static, round_up(up_bytes[u], 64)};
+    if (!uploads.empty())
+      ctx->pool->parallel_for(uploads.size(), [&](size_t u) {
+        write_static(*uploads[u].second, hd + s_up + uploads[u].first, round_up(up_bytes[u], 64));
+      });
     host_ms += ms_since(th0);
 
     hipStream_t side = A.copy_stream;
     SVS_HIP(hipMemcpyAsync(dd, hd, total, hipMemcpyHostToDevice, side));
-    for (const auto& u : uploads) {
-      PoaTask& t = *u.second;
-      const size_t bytes = static_cast<size_t>(reinterpret_cast<uint8_t*>(t.d_paths) - t.d_static);
-      SVS_HIP(hipMemcpyAsync(t.d_static, dd + s_up + u.first, bytes, hipMemcpyDeviceToDevice, side));
-    }
+    if (!uploads.empty())
+      SVS_HIP(launch_scatter_copy(reinterpret_cast<const CopyDesc*>(dd + s_cp), static_cast<int>(uploads.size()), side));
     for (const auto& m : moves)
       SVS_HIP(launch_dgraph_move(reinterpret_cast<const uint8_t*>(m[0]), static_cast<uint32_t>(m[1]),
                                  static_cast<uint32_t>(m[2]), reinterpret_cast<uint8_t*>(m[3]),
@@ -1183,13 +1219,14 @@ struct PoaScheduler::Impl {
       pl.jobs = reinterpret_cast<const PoaJob*>(dd);
       pl.n_jobs = static_cast<int>(nj);
       pl.score = score;
-      pl.tb = A.d_tb.as<uint16_t>();
+      pl.tb = A.d_tb.as<char>();
       pl.bnd = A.d_pool.as<int32_t>();
       pl.pool = A.d_pool.as<int32_t>() + n_bnd;
       pl.aln = A.d_aln.as<int32_t>();
       pl.aln_len = A.d_alen.as<int32_t>();
       pl.lds_slots = lds_pool ? max_slots : 0;
       pl.prune = any_prune;
+      pl.wide = wide;
       pl.waves_per_job = wpj;
       SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
       SVS_HIP(hipEventRecord(A.ev0, A.stream));
@@ -1405,7 +1442,7 @@ struct PoaScheduler::Impl {
       if (h.n_slots != r.n_slots) fail("slot count " + std::to_string(r.n_slots) + " vs " + std::to_string(h.n_slots));
       if (h.max_preds != r.max_preds) fail("max in-degree");
       // the completed tables against the host's full export
-      if (r.V <= kStripPrepMaxRows && r.n_slots <= kStripPrepMaxSlots && r.max_preds <= 31) {
+      if (r.V <= kStripPrepMaxRows && r.n_slots <= kStripPrepMaxSlots && r.max_preds <= kMaxInEdges) {
         RowTables full;
         const int32_t gaps[4] = {score.g, score.e, score.q, score.c};
         t.graph.export_strip_rows(&full, gaps);
@@ -1463,9 +1500,12 @@ struct PoaScheduler::Impl {
         g_trace.host("done", gid(g), td0, fin.size());
         if (ids.empty()) continue;  // refill and try again
       }
-      uint64_t total = 0;
+      uint64_t total = 0, code_bytes = force_wide() ? 4 : 2;
       const KernelEnv ke;
-      for (uint32_t id : ids) total += job_bytes(tasks[id].rows, tasks[id].seqs[tasks[id].next].size(), ke);
+      for (uint32_t id : ids)
+        if (tasks[id].rows.max_preds > kMaxInEdgesNarrow) code_bytes = 4;
+      for (uint32_t id : ids)
+        total += job_bytes(tasks[id].rows, tasks[id].seqs[tasks[id].next].size(), ke, code_bytes);
       if (total <= budget) {
         order_by_cost(ids);
         g.la.ids = std::move(ids);
@@ -1483,7 +1523,8 @@ struct PoaScheduler::Impl {
         size_t last = first;
         uint64_t bytes = 0;
         while (last < ids.size()) {
-          const uint64_t b = job_bytes(tasks[ids[last]].rows, tasks[ids[last]].seqs[tasks[ids[last]].next].size(), ke);
+          const uint64_t b =
+              job_bytes(tasks[ids[last]].rows, tasks[ids[last]].seqs[tasks[ids[last]].next].size(), ke, code_bytes);
           if (last > first && bytes + b > budget) break;
           bytes += b;
           ++last;

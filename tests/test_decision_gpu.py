@@ -226,3 +226,33 @@ def test_bench_windows_match_oracle_digests():
     bad = [k for k, (a, b) in enumerate(zip(digests, gold["digests"])) if a != b]
     assert not bad, f"{len(bad)} windows differ from the oracle, first {bad[:8]}"
     assert hashlib.sha256("\n".join(digests).encode()).hexdigest() == gold["all"]
+
+
+def test_big_windows_mixed_into_config3_batch_match_oracle():
+    """windows past the 64-read configs, a 600-read one
+    (300 tumor + 300 normal, 1.2 kb) and a 320-read one (2 kb), mixed into a
+    batch of config-3 windows (64 reads x 3 kb), through the whole GPU
+    pipeline (MSA POA, features, EM beyond 256 reads, consensus POA): every
+    record equals the CPU oracle's (big_window_digests.json,
+    gen_big_window_goldens.py; the config-3 windows against
+    bench_config3_digests.json)."""
+    import hashlib
+    from svscope_amd import synth
+    from svscope_amd.decision_maker import DecisionSession
+    from svscope_amd.local_graph import _window, record_line
+    gdir = os.path.join(os.path.dirname(__file__), "golden")
+    bench = json.load(open(os.path.join(gdir, "bench_config3_digests.json")))
+    big = json.load(open(os.path.join(gdir, "big_window_digests.json")))["windows"]
+    rows, want = [], []
+    for w in range(6):
+        rows.append(synth.make_window(w, 64, 3000))
+        want.append(bench["digests"][w])
+        if w in (1, 3):
+            b = big[0] if w == 1 else big[1]
+            rows.append(synth.make_window(b["window"], b["reads"], b["ref_len"]))
+            want.append(b["sha256"])
+    with DecisionSession() as s:
+        got = s.wait(s.submit([_window(r) for r in rows]))
+    digests = [hashlib.sha256(record_line(r).encode()).hexdigest() for r in got]
+    bad = [k for k, (a, b) in enumerate(zip(digests, want)) if a != b]
+    assert not bad, f"windows {bad} differ from the oracle"

@@ -218,3 +218,34 @@ def test_device_graphs_verified_against_host_replay():
         os.environ.pop("SVS_POA_VERIFY_GRAPH", None)
     for seqs, g in zip(cases, got):
         assert g == oracle_poa(seqs, 1), seqs
+
+
+
+@pytest.mark.parametrize("mode", ["device", "host"])
+def test_wide_traceback_codes_match_oracle(mode):
+    """32-bit traceback codes (TbFmt<uint32_t>: graphs with a node of more than
+    31 in-edges) on every launch (SVS_POA_FORCE_WIDE):
+    the wide kernel variants, their in-degree from pstart and the 12-bit
+    in-edge fields of the traceback, on the random edge cases and synthetic
+    windows, device graphs (checked fold by fold against a host replay) and
+    host graphs, give the oracle's consensus and MSA."""
+    import os
+    from svscope_amd import synth
+    from svscope_amd.poa import poa_batch
+    cases = helpers.random_cases(31, 120) + helpers.random_cases(32, 12, max_seqs=12, max_len=300, edits=25)
+    cases += [synth.make_window(w, 16, 1500)[0] for w in range(2)]
+    env = {"SVS_POA_FORCE_WIDE": "1"}
+    env.update({"SVS_POA_VERIFY_GRAPH": "1"} if mode == "device" else {"SVS_POA_HOST_GRAPH": "1"})
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        got, st = poa_batch(cases, return_stats=True)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    for seqs, g in zip(cases, got):
+        assert g == oracle_poa(seqs, 1), seqs
+    assert st["wide_launches"] == st["launches"] > 0, st
