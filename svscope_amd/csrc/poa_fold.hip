@@ -427,10 +427,22 @@ struct SortState {
   uint32_t n_exam, n_roots;  // statistics
   uint64_t prof[4];          // SVS_FOLD_PROF: fast roots, DFS runs, window loads, rest (clocks)
 };
-#ifdef SVS_FOLD_PROF
+// Profile builds (tools/build_variant.py): SVS_FOLD_PROF: fast-root and DFS-run
+// clocks, window loads; SVS_FOLD_PROF_EXAM: the DFS examination's phases
+// (record, flag reads, pushes/emits, pop) in prof[0..3].
+#if defined(SVS_FOLD_PROF) || defined(SVS_FOLD_PROF_EXAM)
 #define SVS_PF_CLK() __builtin_readcyclecounter()
 #else
 #define SVS_PF_CLK() 0ull
+#endif
+#ifdef SVS_FOLD_PROF_EXAM
+#define SVS_PF_COUNT(k) ((void)0)
+#define SVS_PF_ADD(k, t) ((void)0)
+#define SVS_PF_EXAM(k, t) (S.prof[k] += SVS_PF_CLK() - (t))
+#else
+#define SVS_PF_COUNT(k) (S.prof[k] += 1)
+#define SVS_PF_ADD(k, t) (S.prof[k] += SVS_PF_CLK() - (t))
+#define SVS_PF_EXAM(k, t) ((void)0)
 #endif
 
 __device__ __forceinline__ bool bit_of(const uint32_t* plane, uint32_t v) { return (plane[v >> 5] >> (v & 31u)) & 1u; }
@@ -440,9 +452,12 @@ __device__ __forceinline__ bool bit_of(const uint32_t* plane, uint32_t v) { retu
 // The sort, export and finalize helpers take the arrays as restrict
 // parameters so the compiler can read the read-only ones through the scalar
 // cache.
-__device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu32* __restrict__ in_nbr,
-                            gu32* __restrict__ r2n, gu32* __restrict__ n2r, gu32* __restrict__ col, SortState& S,
-                            uint32_t* ncol_out) {
+// V0: the node count before this fold (nodes >= V0 are the fold's new ones);
+// r2n_old: the previous sort's rank order of nodes < V0 (a copy: r2n is
+// overwritten as nodes are emitted).
+__device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nrec, const gu32* __restrict__ in_nbr,
+                            gu32* __restrict__ r2n, gu32* __restrict__ n2r, const gu32* __restrict__ r2n_old,
+                            gu32* __restrict__ col, SortState& S, uint32_t* ncol_out) {
   const uint32_t lane = lanei();
   const uint32_t W = (V + 31u) >> 5;
   for (uint32_t w = lane; w < W; w += 64) {
@@ -453,6 +468,7 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
   // Uniform control throughout.  LDS operations of one wave complete in
   // order, so a bit set or a push is seen by the next read without a wait;
   // only the spill area (global memory) needs its stores drained.
+  uint32_t top = 0;  // the entry last pushed
   auto push = [&](uint32_t v) {
     if (S.sp == S.cap) {
       // spill the lower half of the LDS part
@@ -478,6 +494,7 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
     }
     S.st[S.sp] = v;  // (every lane the same word: no divergent branch)
     ++S.sp;
+    top = v;
   };
   auto refill = [&]() {
     // the LDS part is empty: bring back up to half of it from the spill area
@@ -491,35 +508,83 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
     S.spilled = k0;
     S.sp = m;
   };
-  // every lane stores the same words (a lane-0 branch would make the DFS loop
-  // divergent: values in vector registers, control through exec masks)
-  auto set_bit = [&](uint32_t* plane, uint32_t v) { plane[v >> 5] |= 1u << (v & 31u); };
+  // A flag set is an LDS atomic OR by every lane (no returned value to wait
+  // for; a lane-0 branch would make the DFS loop divergent: values in vector
+  // registers, control through exec masks).
+  auto set_bit = [&](uint32_t* plane, uint32_t v) {
+    __hip_atomic_fetch_or(plane + (v >> 5), 1u << (v & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  // Emitted nodes collect in two registers (lane k: the k-th buffered node and
+  // its column) and go out 64 at a time, one store per table per 64 nodes
+  // (nothing reads an emitted node's entries during the sort).
+  uint32_t eb_node = 0, eb_col = 0, eb_n = 0;
   auto emit = [&](uint32_t node) {
-    r2n[cnt] = node;
-    n2r[node] = cnt;
-    col[node] = ncol;
+    const bool mine = lane == eb_n;  // (selects: lane eb_n takes the entry)
+    eb_node = mine ? node : eb_node;
+    eb_col = mine ? ncol : eb_col;
     ++cnt;
+    if (++eb_n == 64u) {
+      const uint32_t rk = cnt - 64u + lane;
+      r2n[rk] = eb_node;
+      n2r[eb_node] = rk;
+      col[eb_node] = eb_col;
+      eb_n = 0;
+    }
   };
   uint32_t root = 0;
   // every examination pops or pushes: a bound on them stops a corrupt graph
   uint32_t steps = 0;
   const uint32_t max_steps = 64u * (V + S.spill_cap) + 4096u;
   auto done_of = [&](uint32_t v) -> uint32_t { return (S.done[v >> 5] >> (v & 31u)) & 1u; };
-  // Node records come from two 64-node windows held in registers (lane l:
-  // node base + l), loaded whole with one coalesced load: R follows the root
-  // scan (ids ascending), D the nodes the DFS pushes (mostly the new nodes of
-  // the latest read, whose ids are close together).  An examination then
-  // reads its record with lane reads instead of a dependent load.
-  uint32_t bR = 0x80000000u, bD = 0x80000000u;  // empty: no id (< 2^31) is within 64 of them
-  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0, r5 = 0, r6 = 0, r7 = 0;
+  // Node records come from two 64-node windows held in registers (lane l one
+  // node's record): O holds 64 consecutive old nodes in the previous sort's
+  // rank order, which the DFS follows closely (a node and the deep nodes it
+  // reaches sit together there), found by comparing ids across the lanes; N
+  // holds 64 consecutive new nodes by id (the fold's read adds them in path
+  // order).  A miss loads a whole window with coalesced loads; a hit costs
+  // lane reads only.
+  uint32_t oid = kNone;  // lane: node id of the O window entry (kNone: empty)
+  uint32_t bN = 0x80000000u;  // N window base (empty: no id < 2^31 is within 64 of it)
+  uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o4 = 0, o5 = 0, o6 = 0, o7 = 0;
   uint32_t d0w = 0, d1w = 0, d2w = 0, d3w = 0, d4w = 0, d5w = 0, d6w = 0, d7w = 0;
-  auto load_win = [&](uint32_t b, uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3, uint32_t& w4,
+  auto load_rec = [&](uint32_t v, bool ok, uint32_t& w0, uint32_t& w1, uint32_t& w2, uint32_t& w3, uint32_t& w4,
                       uint32_t& w5, uint32_t& w6, uint32_t& w7) {
-    const uint32_t v = min(b + lane, V - 1u);
-    const u32x4 x = *reinterpret_cast<const GLB u32x4*>(nrec + 8 * v);
-    const u32x4 y = *reinterpret_cast<const GLB u32x4*>(nrec + 8 * v + 4);
+    const uint32_t u = ok ? v : 0u;
+    const u32x4 x = *reinterpret_cast<const GLB u32x4*>(nrec + 8 * u);
+    const u32x4 y = *reinterpret_cast<const GLB u32x4*>(nrec + 8 * u + 4);
     w0 = x.x; w1 = x.y; w2 = x.z; w3 = x.w;
     w4 = y.x; w5 = y.y; w6 = y.z; w7 = y.w;
+  };
+  // record of node v: off, in-degree | aligned count << 24, aligned list, first three tails
+  auto record = [&](uint32_t v, uint32_t& off, uint32_t& w1, uint32_t& m0, uint32_t& m1, uint32_t& m2, uint32_t& t0,
+                    uint32_t& t1, uint32_t& t2) {
+    if (v >= V0) {
+      if (v - bN >= 64u) {
+        bN = v >= V0 + 32u ? v - 32u : V0;
+        const uint32_t u = bN + lane;
+        load_rec(u, u < V, d0w, d1w, d2w, d3w, d4w, d5w, d6w, d7w);
+        SVS_PF_COUNT(2);
+      }
+      const uint32_t l = v - bN;
+      off = lane_val(d0w, l); w1 = lane_val(d1w, l); m0 = lane_val(d2w, l); m1 = lane_val(d3w, l);
+      m2 = lane_val(d4w, l); t0 = lane_val(d5w, l); t1 = lane_val(d6w, l); t2 = lane_val(d7w, l);
+      return;
+    }
+    uint64_t hit = ballot(oid == v);
+    if (!hit) {
+      // the old rank of v (n2r still holds it: v is not emitted yet), a few
+      // ranks of look-behind
+      const uint32_t rk = uni(n2r[v]);
+      const uint32_t b = rk > 8u ? rk - 8u : 0u;
+      const uint32_t k = b + lane;
+      oid = k < V0 ? r2n_old[k] : kNone;
+      load_rec(oid, oid != kNone, o0, o1, o2, o3, o4, o5, o6, o7);
+      SVS_PF_COUNT(3);
+      hit = ballot(oid == v);
+    }
+    const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(hit));
+    off = lane_val(o0, l); w1 = lane_val(o1, l); m0 = lane_val(o2, l); m1 = lane_val(o3, l);
+    m2 = lane_val(o4, l); t0 = lane_val(o5, l); t1 = lane_val(o6, l); t2 = lane_val(o7, l);
   };
   // Every node with an id below the current root is done (each root's DFS
   // finishes all it pushed), so flags are only read for larger ids and a root
@@ -542,15 +607,10 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
     ++S.n_roots;
     const uint64_t pf0 = SVS_PF_CLK();
     {
-      if (root - bR >= 64u) {
-        bR = root;
-        load_win(bR, r0, r1, r2, r3, r4, r5, r6, r7);
-      }
-      const uint32_t l = root - bR;
-      const uint32_t w1 = lane_val(r1, l), deg = w1 & 0xFFFFFFu, alc = w1 >> 24;
+      uint32_t off, w1, m0, m1, m2, t0, t1, t2;
+      record(root, off, w1, m0, m1, m2, t0, t1, t2);
+      const uint32_t deg = w1 & 0xFFFFFFu, alc = w1 >> 24;
       if (deg <= 3u) {
-        const uint32_t m0 = lane_val(r2, l), m1 = lane_val(r3, l), m2 = lane_val(r4, l);
-        const uint32_t t0 = lane_val(r5, l), t1 = lane_val(r6, l), t2 = lane_val(r7, l);
         const bool fast = (deg < 1u || t0 < root) && (deg < 2u || t1 < root) && (deg < 3u || t2 < root) &&
                           (alc < 1u || m0 < root) && (alc < 2u || m1 < root) && (alc < 3u || m2 < root);
         if (fast) {
@@ -561,7 +621,7 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
           if (alc > 2u) emit(m2);
           ++ncol;
           ++root;
-          S.prof[0] += SVS_PF_CLK() - pf0;
+          SVS_PF_ADD(0, pf0);
           continue;
         }
       }
@@ -574,31 +634,13 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
         S.err = true;
         break;
       }
-      // the node record: CSR start, in-degree | aligned count, aligned list,
-      // first three tails (from a register window); then every flag the
-      // examination needs in one batch of LDS reads
-      bool inR = cur - bR < 64u, inD = cur - bD < 64u;
-      if (!inR && !inD) {
-        if (cur == root) {
-          bR = cur;
-          load_win(bR, r0, r1, r2, r3, r4, r5, r6, r7);
-          inR = true;
-        } else {
-          bD = cur > 32u ? cur - 32u : 0u;
-          load_win(bD, d0w, d1w, d2w, d3w, d4w, d5w, d6w, d7w);
-        }
-        S.prof[2] += 1;
-      }
+      // the node record (register windows); then every flag the examination
+      // needs in one batch of LDS reads
       uint32_t off, w1, m0, m1, m2, t0, t1, t2;
-      if (inR) {
-        const uint32_t l = cur - bR;
-        off = lane_val(r0, l); w1 = lane_val(r1, l); m0 = lane_val(r2, l); m1 = lane_val(r3, l);
-        m2 = lane_val(r4, l); t0 = lane_val(r5, l); t1 = lane_val(r6, l); t2 = lane_val(r7, l);
-      } else {
-        const uint32_t l = cur - bD;
-        off = lane_val(d0w, l); w1 = lane_val(d1w, l); m0 = lane_val(d2w, l); m1 = lane_val(d3w, l);
-        m2 = lane_val(d4w, l); t0 = lane_val(d5w, l); t1 = lane_val(d6w, l); t2 = lane_val(d7w, l);
-      }
+      const uint64_t px0 = SVS_PF_CLK();
+      record(cur, off, w1, m0, m1, m2, t0, t1, t2);
+      SVS_PF_EXAM(0, px0);
+      const uint64_t px1 = SVS_PF_CLK();
       const uint32_t deg = w1 & 0xFFFFFFu, alc = w1 >> 24;
       const uint32_t dc = uni(done_of(cur)), ig = uni(bit_of(S.ign, cur) ? 1u : 0u);
       // (unused slots read cur's word and count as done; they are never looked
@@ -610,6 +652,8 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
       const uint32_t d0 = dn(deg > 0, t0), d1 = dn(deg > 1, t1), d2 = dn(deg > 2, t2);
       const uint32_t e0 = dn(alc > 0, m0), e1 = dn(alc > 1, m1), e2 = dn(alc > 2, m2);
       bool pop = dc != 0;
+      SVS_PF_EXAM(1, px1);
+      const uint64_t px2 = SVS_PF_CLK();
       if (!pop) {
         bool valid = true;
         for (uint32_t x = 0; x < deg; ++x) {
@@ -647,16 +691,31 @@ __device__ int32_t dfs_sort(uint32_t V, const gu32* __restrict__ nrec, const gu3
           pop = true;  // the entry popped is cur's (pushes only happen when !valid)
         }
       }
+      SVS_PF_EXAM(2, px2);
+      const uint64_t px3 = SVS_PF_CLK();
       if (pop) {
         if (S.sp == 0) refill();
         --S.sp;
-        if (S.sp + S.spilled == 0) break;
+        if (S.sp + S.spilled == 0) {
+          SVS_PF_EXAM(3, px3);
+          break;
+        }
         if (S.sp == 0) refill();
+        cur = uni(S.st[S.sp - 1]);
+      } else {
+        cur = top;  // something was pushed: the last push is on top
       }
-      cur = uni(S.st[S.sp - 1]);
+      SVS_PF_EXAM(3, px3);
     }
-    S.prof[1] += SVS_PF_CLK() - pf0;
+    SVS_PF_ADD(1, pf0);
     ++root;
+  }
+  // the buffered emissions
+  if (lane < eb_n) {
+    const uint32_t rk = cnt - eb_n + lane;
+    r2n[rk] = eb_node;
+    n2r[eb_node] = rk;
+    col[eb_node] = eb_col;
   }
   *ncol_out = ncol;
   S.n_exam = static_cast<uint32_t>(steps);
@@ -969,7 +1028,12 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
     }
     ncol = V;
   } else {
-    st = dfs_sort(V, g.nrec, g.in_nbr, g.r2n, g.n2r, g.col, S, &ncol);
+    // the previous rank order, kept for the DFS's record windows (export
+    // reuses `last` after the sort)
+    const uint32_t V0 = min(J.V, V);
+    for (uint32_t r = lanei(); r < V0; r += 64) g.last[r] = g.r2n[r];
+    wave_sync_mem();
+    st = dfs_sort(V, V0, g.nrec, g.in_nbr, g.r2n, g.n2r, g.last, g.col, S, &ncol);
   }
   if (st != kFoldOk) {
     if (lanei() == 0) res->status = st;
@@ -990,7 +1054,10 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
     res->t_exp = static_cast<uint32_t>(T2 - T1);
     res->n_exam = S.n_exam;
     res->n_roots = S.n_roots;
-    for (int k = 0; k < 4; ++k) res->prof[k] = static_cast<uint32_t>(S.prof[k] >> (k == 2 ? 0 : 10));
+    for (int k = 0; k < 4; ++k) res->prof[k] = static_cast<uint32_t>(S.prof[k] >> (k < 2 ? 10 : 0));
+#ifdef SVS_FOLD_PROF_EXAM
+    for (int k = 0; k < 4; ++k) res->prof[k] = static_cast<uint32_t>(S.prof[k] >> 10);
+#endif
   }
 }
 

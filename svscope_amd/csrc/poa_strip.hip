@@ -180,11 +180,15 @@ __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, 
 // it publishes every 8 rows through an LDS progress counter (workgroup-scope
 // release / acquire), so the waves form a row-skewed pipeline over strips.
 template <bool LDSP, int WPJ, bool PRUNE, class CodeT>
-// The pruning variant is held to 80 VGPRs (6 waves per SIMD; a few spills to
-// scratch in cold paths): measured faster than its natural 86 (5 waves),
-// profiles/r01_v36.  SVS_PRUNE_OCC overrides it in development builds.
+// The pruning variant is held to 72 VGPRs (a few spills to scratch in cold
+// paths): its workgroups still fill a CU 6 waves per SIMD deep (LDS-bound),
+// and the 80 registers per SIMD left over take the one-wave fold kernels
+// that run beside it (poa_fold.hip) without displacing a DP workgroup:
+// 232 vs 225 windows/s at 80 VGPRs (profiles/r03_v28); 80 beat the natural 86
+// in round 1 (profiles/r01_v36).  SVS_PRUNE_OCC overrides it in development
+// builds.
 #ifndef SVS_PRUNE_OCC
-#define SVS_PRUNE_OCC 6
+#define SVS_PRUNE_OCC 7
 #endif
 #define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? SVS_PRUNE_OCC : 1)))
 __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(

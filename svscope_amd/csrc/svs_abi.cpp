@@ -115,6 +115,10 @@ void svs_release(svs_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->em_stream) (void)hipStreamSynchronize(ctx->em_stream);
   ctx->poa_arenas.clear();
+  if (ctx->poa_dp_stream) {
+    (void)hipStreamSynchronize(ctx->poa_dp_stream);
+    (void)hipStreamDestroy(ctx->poa_dp_stream);
+  }
   ctx->dgraph_arena.reset();
   for (svs::DeviceBuf* b : {&ctx->d_em_in, &ctx->d_em_ws, &ctx->d_em_out, &ctx->d_rng, &ctx->d_ms_pairs,
                             &ctx->d_ms_seq, &ctx->d_ms_nib, &ctx->d_ms_carry, &ctx->d_ms_stack, &ctx->d_ms_out})

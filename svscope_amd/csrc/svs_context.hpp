@@ -192,6 +192,10 @@ struct svs_context {
   std::vector<std::unique_ptr<svs::PoaArena>> poa_arenas;
   // blocks of the device-resident POA graphs (svs_devarena.hpp)
   std::unique_ptr<svs::DevArena> dgraph_arena;
+  // SVS_POA_FOLD_CUS=n: the POA kernels split the CUs, n for the groups' fold
+  // kernels (their copy streams), the rest for the DP kernel (this stream)
+  int poa_fold_cus = 0;
+  hipStream_t poa_dp_stream = nullptr;
   // EM arenas
   svs::DeviceBuf d_em_in, d_em_ws, d_em_out, d_rng;
   svs::PinnedBuf h_em_in, h_em_out;

@@ -711,8 +711,10 @@ struct FoldTimes {
                  static_cast<unsigned long long>(n_fin), n_fin ? fin / n_fin : 0.0, max_fin, double(exams) / n,
                  double(roots) / n);
     if (prof[0] || prof[1])
-      std::fprintf(stderr, "[svs] DFS profile per fold: fast roots %.0f kclk, DFS runs %.0f kclk, %.1f window loads\n",
-                   double(prof[0]) * 1.024 / n, double(prof[1]) * 1.024 / n, double(prof[2]) / n);
+      std::fprintf(stderr,
+                   "[svs] DFS profile per fold: fast roots %.0f kclk, DFS runs %.0f kclk, %.1f new-node and %.1f "
+                   "old-node window loads\n",
+                   double(prof[0]) * 1.024 / n, double(prof[1]) * 1.024 / n, double(prof[2]) / n, double(prof[3]) / n);
   }
 };
 FoldTimes g_fold_times;
@@ -771,6 +773,40 @@ struct PoaScheduler::Impl {
     while (ctx->poa_arenas.size() < 2)
       ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, shared ? ctx->stream : nullptr));
     for (int g = 0; g < 2; ++g) groups[g].arena = ctx->poa_arenas[g].get();
+    if (shared) split_cus();
+  }
+
+  // SVS_POA_FOLD_CUS=n (device-resident graphs, shared DP stream): n CUs,
+  // spread evenly over the device, run the fold kernels (the groups' copy
+  // streams) and the DP kernel gets the others, so that fold waves never take
+  // the register file or LDS a DP workgroup needs on its CU.
+  void split_cus() {
+    const char* e = std::getenv("SVS_POA_FOLD_CUS");
+    const int want = e ? std::atoi(e) : 0;
+    if (!dev || want <= 0 || want == ctx->poa_fold_cus) return;
+    hipDeviceProp_t prop;
+    SVS_HIP(hipGetDeviceProperties(&prop, ctx->device));
+    const int n_cu = prop.multiProcessorCount;
+    if (want >= n_cu) return;
+    const int words = (n_cu + 31) / 32, step = n_cu / want;
+    std::vector<uint32_t> fold(words, 0), dp(words, 0);
+    for (int i = 0; i < n_cu; ++i) {
+      const bool f = (i % step) == step - 1 && i / step < want;
+      (f ? fold : dp)[i / 32] |= 1u << (i % 32);
+    }
+    for (auto& a : ctx->poa_arenas) SVS_HIP(hipStreamSynchronize(a->copy_stream));
+    if (ctx->poa_dp_stream) {
+      SVS_HIP(hipStreamSynchronize(ctx->poa_dp_stream));
+      SVS_HIP(hipStreamDestroy(ctx->poa_dp_stream));
+    }
+    SVS_HIP(hipExtStreamCreateWithCUMask(&ctx->poa_dp_stream, static_cast<uint32_t>(n_cu), dp.data()));
+    for (auto& a : ctx->poa_arenas) {
+      SVS_HIP(hipStreamSynchronize(a->stream));
+      SVS_HIP(hipStreamDestroy(a->copy_stream));
+      SVS_HIP(hipExtStreamCreateWithCUMask(&a->copy_stream, static_cast<uint32_t>(n_cu), fold.data()));
+      a->stream = ctx->poa_dp_stream;
+    }
+    ctx->poa_fold_cus = want;
   }
 
   // Moves queued tasks into the group, up to `cap` active tasks; when the
