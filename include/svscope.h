@@ -193,6 +193,8 @@ typedef struct svs_decision_result svs_decision_result;
 #define SVS_DEC_EM 1          /* EM ran, no somatic + germline pair: default record */
 #define SVS_DEC_EMOUTPUT 2    /* record with clusters, flag + "|EMOutput" */
 #define SVS_DEC_INDEX_ERROR 3 /* a label row has no read id: the reference raises IndexError */
+#define SVS_DEC_FAILED 4      /* the window went past an engine limit (svs_decision_result_window_error says
+                                 which); the other windows of the batch are unaffected */
 
 int svs_decision_batch(svs_context* ctx, int32_t n_windows, const svs_decision_window* wins,
                        const int64_t* seq_byte_start, const char* seq_bytes, const char* text,
@@ -223,6 +225,8 @@ int svs_decision_session_close(svs_decision_session* s);
 
 int svs_decision_result_window(const svs_decision_result* r, int32_t window, int32_t* status, int32_t* K,
                                int32_t* n_som, int32_t* n_germ);
+/* the reason of an SVS_DEC_FAILED window (empty string otherwise); owned by r */
+int svs_decision_result_window_error(const svs_decision_result* r, int32_t window, const char** msg);
 /* cluster c of a window: somatic clusters first (c < n_som), then germline;
  * ids = ReadIDs indices of the cluster's reads, cons = its consensus ("-" when
  * every read of the cluster is empty). */

@@ -71,7 +71,7 @@ class DecisionStats(ctypes.Structure):
         return d
 
 
-DEC_NO_EM, DEC_EM, DEC_EMOUTPUT, DEC_INDEX_ERROR = 0, 1, 2, 3
+DEC_NO_EM, DEC_EM, DEC_EMOUTPUT, DEC_INDEX_ERROR, DEC_FAILED = 0, 1, 2, 3, 4
 
 
 class MisscoreStats(ctypes.Structure):
@@ -160,6 +160,8 @@ def _declare_em(lib):
     lib.svs_decision_session_close.restype = ctypes.c_int
     lib.svs_decision_result_window.argtypes = [P, I32, PI32, PI32, PI32, PI32]
     lib.svs_decision_result_window.restype = ctypes.c_int
+    lib.svs_decision_result_window_error.argtypes = [P, I32, ctypes.POINTER(ctypes.c_char_p)]
+    lib.svs_decision_result_window_error.restype = ctypes.c_int
     lib.svs_decision_result_cluster.argtypes = [P, I32, I32, ctypes.POINTER(PI32), PI32,
                                                 ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64)]
     lib.svs_decision_result_cluster.restype = ctypes.c_int

@@ -187,7 +187,7 @@ __device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base
       for (uint32_t i = 0; i < cur.n; ++i) {
         const uint32_t r = cur.r0 + i;
         const uint32_t a = pstart_of(cur, i), b = pstart_of(cur, i + 1);
-        uint32_t sd = a == b ? 0u : 0xFFFFu;  // a source: 0
+        uint32_t sd = a == b ? 0u : 0x3FFFFFFFu;  // a source: 0
         for (uint32_t x = a; x < b; ++x) {
           const uint32_t pr = (edge(cur, x) & 0x7FFFFFFFu) - 1;
           const uint32_t sdp =

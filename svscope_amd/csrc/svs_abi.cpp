@@ -372,6 +372,13 @@ int svs_decision_result_window(const svs_decision_result* r, int32_t window, int
   return SVS_OK;
 }
 
+int svs_decision_result_window_error(const svs_decision_result* r, int32_t window, const char** msg) {
+  if (!r || window < 0 || window >= static_cast<int32_t>(r->w.size()) || !msg)
+    return fail(SVS_E_INVALID, "svs_decision_result_window_error: invalid argument");
+  *msg = r->w[window].error.c_str();
+  return SVS_OK;
+}
+
 int svs_decision_result_cluster(const svs_decision_result* r, int32_t window, int32_t cluster,
                                 const int32_t** ids, int32_t* n_ids, const char** cons, int64_t* cons_len) {
   if (!r || window < 0 || window >= static_cast<int32_t>(r->w.size()) || !ids || !n_ids || !cons || !cons_len)

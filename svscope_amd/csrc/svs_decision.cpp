@@ -336,6 +336,19 @@ class Pipeline {
       const TaskRef ref = refs[t.tag];
       free_refs.push_back(t.tag);
       Batch& b = *ref.b;
+      if (!t.error.empty()) {
+        // past an engine limit: this window fails alone
+        auto& out = b.res->w[ref.w];
+        if (out.status != SVS_DEC_FAILED) out.error = t.error;
+        out.status = SVS_DEC_FAILED;
+        if (ref.cluster < 0) {
+          --msa_outstanding;
+          window_complete(b);
+        } else if (--b.cons_left[ref.w] == 0) {
+          window_complete(b);
+        }
+        continue;
+      }
       if (ref.cluster < 0) {
         msa_ids.emplace_back(id, WinRef{&b, ref.w});
         b.msa_rate[ref.w] = t.rate;

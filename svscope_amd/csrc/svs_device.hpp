@@ -86,9 +86,11 @@ constexpr uint64_t kStripLdsBytes = 160 * 1024 - 256;
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream);
 // Device half of the strip row export (poa_prep.hip) for the jobs with
 // PoaJob::prep bit 0.
-// rows of a prep job: its fewest-nodes-from-a-source distances (column 0) are
-// kept below 0xFFFF, exact for any graph of fewer rows
-constexpr uint32_t kStripPrepMaxRows = 65535;
+// rows of a prep job (its path lengths for the pruning bound are kept in 16
+// bits, clamped: exact for reads shorter than 65535 bases, the engine prunes
+// no longer read)
+constexpr uint32_t kStripPrepMaxRows = 1u << 24;
+constexpr uint32_t kPruneMaxReadLen = 65534;
 constexpr uint32_t kStripPrepMaxSlots = 1024;  // pool slots of a prep job (free list: a VGPR, then LDS)
 size_t strip_prep_scratch_words(uint32_t n_rows);  // after the job's in-edge slots (rounded to 4)
 hipError_t launch_poa_strip_prep(const PoaJob* jobs, int n_jobs, const PoaScore& score, uint32_t max_rows,

@@ -27,6 +27,7 @@ struct svs_decision_result {
   struct Win {
     int32_t status = 0, K = 0;
     std::vector<svs::ClusterPlan> som, germ;
+    std::string error;  // SVS_DEC_FAILED: which limit
   };
   std::vector<Win> w;
   svs_decision_stats st{};
@@ -73,6 +74,9 @@ struct PoaTask {
 
   std::string consensus;
   std::vector<std::string> msa;
+  // set when the task went past an engine limit (a per-task failure: the task
+  // completes with no consensus / MSA, the others go on)
+  std::string error;
 };
 
 // Continuous-batching POA driver.  Every launch aligns the next sequence of

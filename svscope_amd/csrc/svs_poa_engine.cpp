@@ -326,7 +326,8 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     J.pool_off = n_pool;
     J.aln_off = n_aln;
     J.lb = prune_bound(tasks[la.ids[k]], score, J.n_rows, J.len, penv);
-    if (J.n_slots > 31) J.lb = kNoPrune;  // the kernel tracks slot liveness in 31 bits
+    // the kernel tracks slot liveness in 31 bits; path lengths are 16-bit
+    if (J.n_slots > 31 || J.len > kPruneMaxReadLen) J.lb = kNoPrune;
     any_prune = any_prune || J.lb != kNoPrune;
     n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
     n_bnd += round_up(round_up(J.n_rows, 8) * (J.ls / 64) * 4, 64);
@@ -882,6 +883,24 @@ struct PoaScheduler::Impl {
     poff[i] = acc;
   }
 
+  // A task past an engine limit completes alone, with no consensus or MSA and
+  // the reason in t.error (the decision layer fails its window only).
+  void fail_task(Group& g, uint32_t id, std::string why) {
+    PoaTask& t = tasks[id];
+    t.error = std::move(why);
+    t.consensus.clear();
+    t.msa.clear();
+    release_dev(t);
+    g.completed.push_back(id);
+  }
+  // the row limit of the device table planner (SVS_POA_TEST_MAX_ROWS lowers it
+  // in tests, to fail one window of a batch on purpose)
+  static uint32_t planner_max_rows() {
+    const char* e = std::getenv("SVS_POA_TEST_MAX_ROWS");
+    const long v = e ? std::atol(e) : 0;
+    return v > 0 && static_cast<uint64_t>(v) < kStripPrepMaxRows ? static_cast<uint32_t>(v) : kStripPrepMaxRows;
+  }
+
   void release_dev(PoaTask& t) {
     if (t.d_static) darena->free(t.d_static, t.static_bytes);
     if (t.dg.blk) darena->free(t.dg.blk, t.dg_bytes);
@@ -922,6 +941,31 @@ struct PoaScheduler::Impl {
       if (!fin.empty()) {
         for (uint32_t id : fin) release_dev(tasks[id]);
         g.completed = fin;
+        host_ms += ms_since(th0);
+        continue;
+      }
+      // the next alignment of every task within the DP kernel's limits (a
+      // task starting now aligns its second read against its first)
+      keep.clear();
+      for (uint32_t id : g.active) {
+        const PoaTask& t = tasks[id];
+        uint64_t rows = t.dg.V, len = t.next < t.seqs.size() ? t.seqs[t.next].size() : 0;
+        if (t.dg.V == 0) {
+          rows = len;
+          size_t k = t.next + 1;
+          while (k < t.seqs.size() && t.seqs[k].empty()) ++k;
+          len = k < t.seqs.size() ? t.seqs[k].size() : 0;
+        }
+        const char* why = nullptr;
+        if (t.dg.V > 0 && t.max_preds_next > kMaxInEdges)
+          why = "a graph node has more than 4094 in-edges (traceback code limit)";
+        else if (len > 0 && rows * strip_ls(static_cast<uint32_t>(len)) > 0x7FFFFFFFull)
+          why = "an alignment's traceback matrix exceeds 2^31 cells";
+        if (why) fail_task(g, id, why);
+        else keep.push_back(id);
+      }
+      if (keep.size() != g.active.size()) {
+        g.active = keep;
         host_ms += ms_since(th0);
         continue;
       }
@@ -1058,7 +1102,7 @@ struct PoaScheduler::Impl {
       J.pool_off = n_pool;
       J.aln_off = n_aln;
       J.lb = prune_bound(t, score, J.n_rows, J.len, penv);
-      if (J.n_slots > 31) J.lb = kNoPrune;
+      if (J.n_slots > 31 || J.len > kPruneMaxReadLen) J.lb = kNoPrune;
       any_prune = any_prune || J.lb != kNoPrune;
       n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
       n_bnd += round_up(round_up(J.n_rows, 8) * (J.ls / 64) * 4, 64);
@@ -1373,6 +1417,7 @@ struct PoaScheduler::Impl {
       const FoldResult& r = res[i];
       const FoldJob& F = D.folds[i];
       if (r.status == kFoldSkipped) continue;  // a pruning retry: graph and tables unchanged
+      if (!t.error.empty()) continue;          // the task failed at an earlier fold of this launch
       if (r.status != kFoldOk)
         throw SvsError(SVS_E_INTERNAL, "device POA graph fold failed (status " + std::to_string(r.status) + ")");
       g_fold_times.add(r, F.flags);
@@ -1393,9 +1438,14 @@ struct PoaScheduler::Impl {
       if (F.flags & kFoldExport) {
         t.n_slots_next = r.n_slots;
         t.max_preds_next = r.max_preds;
-        // the device planner's limits (poa_prep.hip); beyond them the tables are incomplete
-        if (r.V > kStripPrepMaxRows || r.n_slots > kStripPrepMaxSlots)
-          throw SvsError(SVS_E_UNSUPPORTED, "device POA graph beyond the row-table planner's limits");
+        // the device planner's limits (poa_prep.hip); beyond them the tables
+        // are incomplete: this task fails alone
+        if (r.V > planner_max_rows() || r.n_slots > kStripPrepMaxSlots || r.max_preds > kMaxInEdges) {
+          fail_task(g, D.fold_ids[i],
+                    "a POA graph beyond the device row-table planner's limits (" + std::to_string(r.V) + " rows, " +
+                        std::to_string(r.n_slots) + " pool slots, " + std::to_string(r.max_preds) + " in-edges)");
+          continue;
+        }
         t.tables_ok = true;
       }
       if (F.flags & kFoldFinal) {
@@ -1700,15 +1750,21 @@ void run_poa_tasks(svs_context* ctx, std::vector<PoaTask>& tasks, const svs_poa_
       t.genmsa = cfg.genmsa != 0;
       sched.add(std::move(t));
     }
+    std::string first_error;
     sched.run(
         [&](const std::vector<uint32_t>& ids) {
           for (uint32_t id : ids) {
             PoaTask& t = sched.task(id);
+            if (!t.error.empty() && first_error.empty())
+              first_error = "POA job " + std::to_string(id) + ": " + t.error;
             tasks[id].consensus = std::move(t.consensus);
             tasks[id].msa = std::move(t.msa);
           }
         },
         [](bool) { return false; });
+    // the batch API has no per-job status: a job past a limit fails the call
+    // (after every other job has run)
+    if (!first_error.empty()) throw SvsError(SVS_E_UNSUPPORTED, first_error);
   }
   st.wall_ms += ms_since(t_wall0);
 }

@@ -83,9 +83,26 @@ def _gate(windows):
     return records, gated
 
 
+class WindowFailed(_abi.SvsError):
+    """Some windows of a batch went past an engine limit (status
+    SVS_DEC_FAILED): ``failed`` maps their batch indices to the reason,
+    ``records`` holds every other window's finished record (None for the failed
+    ones).  The reference has no such limits; the engine fails those windows
+    alone and the caller decides what to write."""
+
+    def __init__(self, failed, records):
+        self.failed = dict(failed)
+        self.records = records
+        first = next(iter(self.failed.items()))
+        super().__init__(f"{len(self.failed)} window(s) past an engine limit, window {first[0]}: {first[1]}")
+
+
 def _format(lib, res, windows, gated, records):
-    """Fills the records of the gated windows from a decision result (:178-190)."""
+    """Fills the records of the gated windows from a decision result (:178-190).
+    Raises WindowFailed, after filling every other record, when windows went
+    past an engine limit."""
     status, K, ns, ng = (ctypes.c_int32() for _ in range(4))
+    failed = {}
     iptr = ctypes.POINTER(ctypes.c_int32)()
     nid = ctypes.c_int32()
     cptr = ctypes.c_void_p()
@@ -95,6 +112,12 @@ def _format(lib, res, windows, gated, records):
                                                   ctypes.byref(ns), ctypes.byref(ng)))
         if status.value == _abi.DEC_INDEX_ERROR:
             raise IndexError(f"window {w}: an EM label row has no read id (the reference raises here)")
+        if status.value == _abi.DEC_FAILED:
+            msg = ctypes.c_char_p()
+            _abi.check(lib.svs_decision_result_window_error(res, k, ctypes.byref(msg)))
+            failed[w] = (msg.value or b"").decode()
+            records[w] = None
+            continue
         if status.value != _abi.DEC_EMOUTPUT:
             continue
         ids = windows[w][2]
@@ -112,6 +135,8 @@ def _format(lib, res, windows, gated, records):
         r[7] = ";".join(ids_out[ns.value:])
         r[8] = ng.value
         r[9] = r[9] + "|EMOutput"
+    if failed:
+        raise WindowFailed(failed, records)
     return records
 
 

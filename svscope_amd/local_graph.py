@@ -83,25 +83,46 @@ def _window(r):
 def iter_batches(rows, batch_size=512, context=None, depth=4):
     """Yields the records of each batch of ``rows``, in order, streamed through
     one DecisionSession with up to ``depth`` batches in flight (the engine's
-    scheduler never drains between batches)."""
+    scheduler never drains between batches).  A window past an engine limit
+    (decision_maker.WindowFailed) yields None in its place; the others run on,
+    and once every batch is done a WindowFailed names all such windows (row
+    indices into ``rows``)."""
     from collections import deque
-    from .decision_maker import DecisionSession
+    from .decision_maker import DecisionSession, WindowFailed
     if not rows:
         return
+    failed = {}
+
+    def take(session, ticket, base):
+        try:
+            return session.wait(ticket)
+        except WindowFailed as e:
+            failed.update({base + w: why for w, why in e.failed.items()})
+            return e.records
+
     with DecisionSession(context) as session:
         tickets = deque()
         for k in range(0, len(rows), batch_size):
-            tickets.append(session.submit([_window(r) for r in rows[k:k + batch_size]]))
+            tickets.append((session.submit([_window(r) for r in rows[k:k + batch_size]]), k))
             if len(tickets) >= depth:
-                yield session.wait(tickets.popleft())
+                yield take(session, *tickets.popleft())
         while tickets:
-            yield session.wait(tickets.popleft())
+            yield take(session, *tickets.popleft())
+    if failed:
+        raise WindowFailed(failed, None)
 
 
 def run_windows(rows, batch_size=512, context=None):
+    """Records of ``rows`` in order; a WindowFailed carries them (None for the
+    failed windows) in ``records``."""
+    from .decision_maker import WindowFailed
     out = []
-    for recs in iter_batches(rows, batch_size, context):
-        out.extend(recs)
+    try:
+        for recs in iter_batches(rows, batch_size, context):
+            out.extend(recs)
+    except WindowFailed as e:
+        e.records = out
+        raise
     return out
 
 
@@ -113,7 +134,7 @@ def write_journal(path, mode, rows, batch_size):
     lines = []
     with open(path, mode) as fh:
         for recs in iter_batches(rows, batch_size):
-            chunk = [record_line(x) for x in recs]
+            chunk = [record_line(x) for x in recs if x is not None]
             fh.write("".join(line + "\n" for line in chunk))
             fh.flush()
             lines.extend(chunk)
