@@ -193,7 +193,10 @@ __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, cons
 // The fold kernels run one wave per job beside the DP kernel's waves on the
 // same SIMDs and sit on the chain DP -> fold -> next DP of their group: they
 // issue ahead of the DP waves (s_setprio), which only wait on them.
-#define SVS_FOLD_PRIO() __builtin_amdgcn_s_setprio(3)
+#ifndef SVS_FOLD_PRIO_LEVEL
+#define SVS_FOLD_PRIO_LEVEL 3
+#endif
+#define SVS_FOLD_PRIO() __builtin_amdgcn_s_setprio(SVS_FOLD_PRIO_LEVEL)
 
 // ---------------------------------------------------------------- update
 // spoa Graph::AddAlignment (poa_graph.cpp add_alignment_nodes): nodes of the

@@ -273,7 +273,10 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
 // The same for the device-resident graphs (poa_dgraph.hpp): the jobs whose
 // fold exported the next alignment's lite tables into their block.
 __global__ __launch_bounds__(192) void poa_dgraph_prep_kernel(const FoldJob* __restrict__ jobs, PoaScore P) {
-  __builtin_amdgcn_s_setprio(3);  // beside the DP kernel, on its group's critical chain (poa_fold.hip)
+#ifndef SVS_FOLD_PRIO_LEVEL
+#define SVS_FOLD_PRIO_LEVEL 3
+#endif
+  __builtin_amdgcn_s_setprio(SVS_FOLD_PRIO_LEVEL);  // beside the DP kernel, on its group's critical chain (poa_fold.hip)
   __shared__ uint32_t fl_ext[kStripPrepMaxSlots - 64];
   const FoldJob J = jobs[blockIdx.x];
   if (!(J.flags & kFoldExport)) return;
