@@ -197,6 +197,13 @@ __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, cons
 #define SVS_FOLD_PRIO_LEVEL 3
 #endif
 #define SVS_FOLD_PRIO() __builtin_amdgcn_s_setprio(SVS_FOLD_PRIO_LEVEL)
+// The sort (the longest fold kernel) may instead start at the DP waves'
+// priority and raise its own once it has run SVS_FOLD_RAISE_TICKS x 10 ns
+// (0: raised from the start), so that early finishers never take issue slots
+// ahead of the DP waves while late ones still meet their group's next launch.
+#ifndef SVS_FOLD_RAISE_TICKS
+#define SVS_FOLD_RAISE_TICKS 0
+#endif
 
 // ---------------------------------------------------------------- update
 // spoa Graph::AddAlignment (poa_graph.cpp add_alignment_nodes): nodes of the
@@ -429,6 +436,8 @@ struct SortState {
   bool err;            // the stack outgrew its spill area
   uint32_t n_exam, n_roots;  // statistics
   uint64_t prof[4];          // SVS_FOLD_PROF: fast roots, DFS runs, window loads, rest (clocks)
+  uint64_t raise_at;         // s_memrealtime at which the wave raises its priority (SVS_FOLD_RAISE_TICKS)
+  bool raised;
 };
 // Profile builds (tools/build_variant.py): SVS_FOLD_PROF: fast-root and DFS-run
 // clocks, window loads; SVS_FOLD_PROF_EXAM: the DFS examination's phases
@@ -633,6 +642,11 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
     push(root);
     uint32_t cur = root;
     while (!S.err) {
+      if (SVS_FOLD_RAISE_TICKS > 0 && (steps & 255u) == 0 && !S.raised &&
+          __builtin_amdgcn_s_memrealtime() >= S.raise_at) {
+        __builtin_amdgcn_s_setprio(SVS_FOLD_PRIO_LEVEL);
+        S.raised = true;
+      }
       if (++steps > max_steps) {
         S.err = true;
         break;
@@ -640,10 +654,10 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
       // the node record (register windows); then every flag the examination
       // needs in one batch of LDS reads
       uint32_t off, w1, m0, m1, m2, t0, t1, t2;
-      const uint64_t px0 = SVS_PF_CLK();
+      [[maybe_unused]] const uint64_t px0 = SVS_PF_CLK();
       record(cur, off, w1, m0, m1, m2, t0, t1, t2);
       SVS_PF_EXAM(0, px0);
-      const uint64_t px1 = SVS_PF_CLK();
+      [[maybe_unused]] const uint64_t px1 = SVS_PF_CLK();
       const uint32_t deg = w1 & 0xFFFFFFu, alc = w1 >> 24;
       const uint32_t dc = uni(done_of(cur)), ig = uni(bit_of(S.ign, cur) ? 1u : 0u);
       // (unused slots read cur's word and count as done; they are never looked
@@ -656,7 +670,7 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
       const uint32_t e0 = dn(alc > 0, m0), e1 = dn(alc > 1, m1), e2 = dn(alc > 2, m2);
       bool pop = dc != 0;
       SVS_PF_EXAM(1, px1);
-      const uint64_t px2 = SVS_PF_CLK();
+      [[maybe_unused]] const uint64_t px2 = SVS_PF_CLK();
       if (!pop) {
         bool valid = true;
         for (uint32_t x = 0; x < deg; ++x) {
@@ -695,7 +709,7 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
         }
       }
       SVS_PF_EXAM(2, px2);
-      const uint64_t px3 = SVS_PF_CLK();
+      [[maybe_unused]] const uint64_t px3 = SVS_PF_CLK();
       if (pop) {
         if (S.sp == 0) refill();
         --S.sp;
@@ -992,7 +1006,7 @@ __device__ void msa_rows(uint32_t n_paths, const gu32* __restrict__ paths, const
 }
 
 __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __restrict__ jobs, uint32_t lds_words) {
-  SVS_FOLD_PRIO();
+  if (SVS_FOLD_RAISE_TICKS == 0) SVS_FOLD_PRIO();
   extern __shared__ uint32_t lds[];
   const uint64_t T0 = __builtin_amdgcn_s_memrealtime();
   const FoldJob J = jobs[blockIdx.x];
@@ -1015,6 +1029,8 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
   S.n_exam = 0;
   S.n_roots = 0;
   S.prof[0] = S.prof[1] = S.prof[2] = S.prof[3] = 0;
+  S.raise_at = T0 + SVS_FOLD_RAISE_TICKS;
+  S.raised = SVS_FOLD_RAISE_TICKS == 0;
   uint32_t ncol = 0;
   if (S.cap < 64) {
     if (lanei() == 0) res->status = kFoldErrStack;
@@ -1044,6 +1060,7 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
   }
   wave_sync_mem();
   const uint64_t T1 = __builtin_amdgcn_s_memrealtime();
+  if (!S.raised) SVS_FOLD_PRIO();  // the export: the last step before the prep kernel
   uint32_t n_slots = 0, max_preds = 0;
   if (J.flags & kFoldExport)
     export_lite(V, g.base, g.in_off, g.in_nbr, g.out_off, g.r2n, g.n2r, g.last, g.pstart, g.pred, g.info, &n_slots,
