@@ -164,6 +164,12 @@ int32_t prune_bound(const PoaTask& t, const PoaScore& P, uint32_t n_rows, uint32
   return static_cast<int32_t>(lb);
 }
 
+// LDS words a final fold job may take (64 KiB): above it, or for graphs whose
+// scores do not fit, the consensus scores in global memory (poa_fold.hip).
+#ifndef SVS_FINAL_LDS_CAP
+#define SVS_FINAL_LDS_CAP 16384
+#endif
+
 // Kernel selection flags read from the environment once per call site
 // (not once per job: getenv scans the whole environment).
 struct KernelEnv {
@@ -1267,7 +1273,7 @@ struct PoaScheduler::Impl {
         const FoldJob& F = D.folds[i];
         if (F.flags & kFoldFinal) w = std::max(w, (6 * (F.V + F.len) + 8 + 3) / 4);
       }
-      return std::min(w, 16384u);
+      return std::min(w, static_cast<uint32_t>(SVS_FINAL_LDS_CAP));
     };
     const FoldJob* dfold = reinterpret_cast<const FoldJob*>(dd + s_fold);
     SVS_HIP(hipEventRecord(A.evp, side));
