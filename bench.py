@@ -357,6 +357,7 @@ def main():
                                           "unit": "TFLOP/s", "frac": round(em_tflops / FP64_MATRIX_PEAK_TFLOPS, 5)},
                           "em_wall_s": round(st["em_wall_ms"] / 1e3, 3),
                           "em_launches": st["em_launches"], "em_windows": st["em_windows"],
+                          "em_reruns_in_order": st["em_reruns"],
                           "consensus_tasks": st["consensus_tasks"],
                           "features_s": round(st["features_ms"] / 1e3, 3),
                           "labelling_s": round(st["labelling_ms"] / 1e3, 3),

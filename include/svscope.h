@@ -184,6 +184,9 @@ typedef struct svs_decision_stats {
   /* SURVEY.md §8(d) dense-equivalent EM FLOPs of the windows sent to EM:
    * per window sum over K of 41 x 2 N (5 nf) K (21 E-steps + 20 M-steps) */
   double em_flops;
+  /* windows the K-parallel EM could not place its RNG draws for and reran with
+   * K in order (em_kernels.hip em_select_kernel) */
+  int64_t em_reruns;
 } svs_decision_stats;
 
 typedef struct svs_decision_result svs_decision_result;

@@ -63,7 +63,7 @@ class DecisionStats(ctypes.Structure):
     _fields_ = [("poa", PoaStats), ("wall_ms", ctypes.c_double), ("features_ms", ctypes.c_double),
                 ("labelling_ms", ctypes.c_double), ("em_wall_ms", ctypes.c_double), ("em_kernel_ms", ctypes.c_double),
                 ("msa_tasks", ctypes.c_int64), ("consensus_tasks", ctypes.c_int64), ("em_windows", ctypes.c_int64),
-                ("em_launches", ctypes.c_int64), ("em_flops", ctypes.c_double)]
+                ("em_launches", ctypes.c_int64), ("em_flops", ctypes.c_double), ("em_reruns", ctypes.c_int64)]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_ if name != "poa"}

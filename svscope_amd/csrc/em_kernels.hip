@@ -138,7 +138,7 @@ struct EmShared {
   uint64_t rng_off;
 };
 
-constexpr int kMaxK = 15;      // K = 1..max_C, max_C <= 15 (host check)
+// K = 1..max_C with max_C <= 15 (host check in svs_em_engine.cpp): gamma, A and M rows are 16 wide
 
 // gamma staged for the M-step, E-step partial sums (4/chunks feature slices x
 // N reads x K): LDS for windows of up to kEmLdsReads reads, workspace beyond.
@@ -357,6 +357,132 @@ __device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xr,
   __syncthreads();
 }
 
+// One window's workspace for one K (em_ws_layout): every K has its own
+// theta, LT, gamma, pi, gsum, A, M, lik and deep-window scratch, so the K
+// values of a window can also run in parallel workgroups (em_k_kernel).
+struct EmK {
+  double *th, *lt, *g, *pi, *gsum, *A, *M, *lik, *big;
+};
+__device__ __forceinline__ EmK em_k_ptrs(const EmWindow& W, double* ws, int K) {
+  const EmWsLayout L = em_ws_layout(W.n_reads, W.n_feat, W.kmax);
+  double* b = ws + W.ws_off;
+  const int64_t kk = static_cast<int64_t>(K) * (K - 1) / 2;  // sum_{k<K} k
+  const int64_t N = W.n_reads, nf = W.n_feat;
+  EmK e;
+  e.th = b + L.theta + kk * nf * 5;
+  e.lt = b + L.lt + kk * nf * 5;
+  e.g = b + L.gamma + kk * N;
+  e.pi = b + L.pi + kk;
+  e.gsum = b + L.gsum + 16 * (K - 1);
+  e.A = b + L.A + 16 * N * (K - 1);
+  e.M = b + L.M + 16 * N * (K - 1);
+  e.lik = b + L.lik + N * (K - 1);
+  e.big = L.big ? b + L.big + 32 * N * (K - 1) : nullptr;
+  return e;
+}
+
+// feature-major copy of the reads: XT[f][i] (row stride N rounded up to 64),
+// pad symbol 5 for i >= N; then the read-major copy with rows padded to 16
+// features (16-B aligned loads)
+__device__ void em_build_x(const EmWindow& W, const uint8_t* __restrict__ x, uint8_t* __restrict__ xt,
+                           uint8_t* __restrict__ xr) {
+  const int N = W.n_reads, nf = W.n_feat, tid = threadIdx.x;
+  const int NP = read_pad(N);
+  for (int64_t r = tid; r < static_cast<int64_t>(nf) * NP; r += blockDim.x) {
+    const int f = static_cast<int>(r / NP), i = static_cast<int>(r % NP);
+    xt[r] = i < N ? x[static_cast<int64_t>(i) * nf + f] : 5;
+  }
+  const int nfp = (nf + 15) & ~15;
+  for (int64_t r = tid; r < static_cast<int64_t>(N) * nfp; r += blockDim.x) {
+    const int i = static_cast<int>(r / nfp), f = static_cast<int>(r % nfp);
+    xr[r] = f < nf ? x[static_cast<int64_t>(i) * nf + f] : 0;
+  }
+}
+
+// EM for one K (EMCluster's loop body :245-256, EM :190-209), NaN retries
+// included; the workgroup's RNG position is sh->rng_off.  bic[K-1] is written.
+template <bool MFMA>
+__device__ void em_run_k(const EmWindow& W, int K, const EmK& P, const uint8_t* __restrict__ xt,
+                         const uint8_t* __restrict__ xr, const int32_t* __restrict__ lab,
+                         const double* __restrict__ rng, uint64_t rng_len, const EmConfig& cfg, EmShared* sh,
+                         EmLds* lds, double* __restrict__ bic) {
+  const int N = W.n_reads, nf = W.n_feat, tid = threadIdx.x;
+  const double logN = log(static_cast<double>(N));
+  const int32_t* lk = lab + static_cast<int64_t>(K - 1) * N;
+  double b0 = NAN;
+  for (int tries = 5; isnan(b0) && tries != 0; --tries) {
+    for (int r = tid; r < N * K; r += blockDim.x) P.g[r] = (lk[r / K] - 1 == r % K) ? 1.0 : 0.0;
+    __syncthreads();
+    m_step(W, K, xt, P.g, P.pi, P.gsum, P.th, P.lt, rng, rng_len, cfg.eps, sh, lds);
+    e_step<MFMA>(W, K, xr, P.pi, P.lt, P.A, P.M, P.g, lds);
+    for (int it = 0; it < cfg.n_step; ++it) {
+      m_step(W, K, xt, P.g, P.pi, P.gsum, P.th, P.lt, rng, rng_len, cfg.eps, sh, lds);
+      e_step<MFMA>(W, K, xr, P.pi, P.lt, P.A, P.M, P.g, lds);
+      for (int i = tid; i < N; i += blockDim.x) {
+        double s = 0.0;
+        for (int k = 0; k < K; ++k) s += (P.A[i * K + k] + log(clip_eps(P.pi[k], cfg.eps))) * P.g[i * K + k];
+        P.lik[i] = s;
+      }
+      __syncthreads();
+    }
+    // BIC with ZeroParamNum = 0 decides the NaN retry (EMCluster :249-252)
+    const double tot = np_pairwise(P.lik, N);
+    b0 = 2.0 * tot - static_cast<double>(K - 1 + static_cast<int64_t>(K) * nf * 4) * logN;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const double tot = np_pairwise(P.lik, N);
+    bic[K - 1] = 2.0 * tot - static_cast<double>(K - 1 + static_cast<int64_t>(K) * nf * 4 - W.zero_params) * logN;
+  }
+  __syncthreads();
+}
+
+// Model selection (EMCluster :258-277) by one thread: the best BIC, the K = 1
+// rule, labels of the chosen K and its per-read likelihoods.
+__device__ void em_select(const EmWindow& W, double* ws, double* __restrict__ outd, int32_t* __restrict__ outi,
+                          uint64_t rng_off, bool error) {
+  const int N = W.n_reads, nf = W.n_feat, nk = W.kmax - 1;
+  double* bic = outd + W.outd_off;  // nk BICs, then N lik of the chosen K
+  int32_t* oi = outi + W.outi_off;  // [K, best, status, rerun, rng_used(lo), rng_used(hi), Rclust[N]]
+  const double logN = log(static_cast<double>(N));
+  int best = -1;
+  for (int k = 0; k < nk; ++k)
+    if (!isnan(bic[k]) && (best < 0 || bic[k] > bic[best])) best = k;
+  int status = error ? 2 : 0;
+  if (best < 0) status = 3;  // nanargmax of an all-NaN list (numpy raises)
+  int K = best + 1;
+  if (status == 0 && K == 1) {
+    if (nk < 2) status = 4;  // reference indexes BICList[1] (IndexError)
+    else if (bic[0] - bic[1] <= nf * logN) { K = 2; best = 1; }
+  }
+  oi[0] = K;
+  oi[1] = best;
+  oi[2] = status;
+  oi[3] = 0;
+  oi[4] = static_cast<int32_t>(rng_off & 0xFFFFFFFFu);
+  oi[5] = static_cast<int32_t>(rng_off >> 32);
+  if (status == 0) {
+    const EmK P = em_k_ptrs(W, ws, K);
+    for (int i = 0; i < N; ++i) {
+      int am = 0;
+      for (int k = 1; k < K; ++k)
+        if (P.g[i * K + k] > P.g[i * K + am]) am = k;
+      oi[6 + i] = am;
+      bic[nk + i] = P.lik[i];
+    }
+  }
+}
+
+// gamma / E-step partials: LDS, or (deep windows) the K's workspace scratch
+__device__ __forceinline__ EmLds em_lds(const EmWindow& W, const EmK& P, double* lds_dyn) {
+  const int N = W.n_reads;
+  if (N > kEmLdsReads) return EmLds{P.big, P.big + static_cast<int64_t>(N) * 16};
+  return EmLds{lds_dyn, lds_dyn + static_cast<int64_t>(N) * (W.kmax - 1)};
+}
+
+// The whole EMCluster of a window in one workgroup, K = 1..kmax-1 in order
+// with one RNG stream (the reference's order; also the fallback of the
+// K-parallel path below).
 template <bool MFMA>
 __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restrict__ wins,
                                                          const uint8_t* __restrict__ X,
@@ -365,117 +491,90 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
                                                          EmConfig cfg, double* __restrict__ ws,
                                                          double* __restrict__ outd, int32_t* __restrict__ outi) {
   __shared__ EmShared sh;
-  __shared__ double lds_g[kEmLdsReads * kMaxK], lds_part[kEmLdsReads * kMaxK];
+  // gamma and the E-step partials of windows up to kEmLdsReads reads, sized by
+  // the launch to its largest window (em_lds_doubles): a config-3 window takes
+  // 23 KB instead of a fixed 60 KB, so an EM workgroup fits beside the DP
+  // kernel's workgroups on a CU instead of displacing one
+  extern __shared__ double lds_dyn[];
   const EmWindow W = wins[blockIdx.x];
-  const int N = W.n_reads, nf = W.n_feat, kmax = W.kmax, tid = threadIdx.x;
-  const uint8_t* x = X + W.x_off;
-  const int32_t* lab = labels + W.lab_off;
-  // workspace layout (doubles): per-K theta | lt | gamma per K | pi per K | gsum | A | M | lik per K | XT
-  double* theta_all = ws + W.ws_off;
-  const int nk = kmax - 1;
-  const int64_t th_total = static_cast<int64_t>(nk) * (nk + 1) / 2 * nf * 5;
-  double* lt = theta_all + th_total;
-  double* gamma_all = lt + static_cast<int64_t>(nk) * nf * 5;
-  const int64_t g_total = static_cast<int64_t>(nk) * (nk + 1) / 2 * N;
-  double* pi_all = gamma_all + g_total;
-  double* gsum = pi_all + nk * (nk + 1) / 2;
-  double* A = gsum + 16;
-  double* M = A + static_cast<int64_t>(N) * 16;
-  double* lik_all = M + static_cast<int64_t>(N) * 16;
-  uint8_t* xt = reinterpret_cast<uint8_t*>(
-      (reinterpret_cast<uintptr_t>(lik_all + static_cast<int64_t>(nk) * N) + 63) & ~static_cast<uintptr_t>(63));
-  double* bic = outd + W.outd_off;  // nk BICs, then N lik of the chosen K
-  // feature-major copy of the reads: XT[f][i] (row stride N rounded up to
-  // 64), pad symbol 5 for i >= N
-  const int NP = read_pad(N);
-  for (int64_t r = tid; r < static_cast<int64_t>(nf) * NP; r += blockDim.x) {
-    const int f = static_cast<int>(r / NP), i = static_cast<int>(r % NP);
-    xt[r] = i < N ? x[static_cast<int64_t>(i) * nf + f] : 5;
-  }
-  // read-major copy with rows padded to 16 features (16-B aligned loads)
-  const int nfp = (nf + 15) & ~15;
-  uint8_t* xr = xt + static_cast<int64_t>(nf) * NP;
-  for (int64_t r = tid; r < static_cast<int64_t>(N) * nfp; r += blockDim.x) {
-    const int i = static_cast<int>(r / nfp), f = static_cast<int>(r % nfp);
-    xr[r] = f < nf ? x[static_cast<int64_t>(i) * nf + f] : 0;
-  }
-  // gamma / E-step partials: LDS, or (deep windows) after XR in the workspace
-  EmLds lds{lds_g, lds_part};
-  if (N > kEmLdsReads) {
-    double* big = reinterpret_cast<double*>(
-        (reinterpret_cast<uintptr_t>(xr + static_cast<int64_t>(N) * nfp) + 63) & ~static_cast<uintptr_t>(63));
-    lds.g = big;
-    lds.part = big + static_cast<int64_t>(N) * 16;
-  }
-  if (tid == 0) { sh.rng_off = 0; sh.error = 0; sh.reinit = 0; }
+  const EmWsLayout L = em_ws_layout(W.n_reads, W.n_feat, W.kmax);
+  uint8_t* xt = reinterpret_cast<uint8_t*>(ws + W.ws_off) + L.xt_bytes;
+  uint8_t* xr = xt + L.xr_rel;
+  em_build_x(W, X + W.x_off, xt, xr);
+  if (threadIdx.x == 0) { sh.rng_off = 0; sh.error = 0; sh.reinit = 0; }
   __threadfence_block();
   __syncthreads();
-  const double logN = log(static_cast<double>(N));
+  const int nk = W.kmax - 1;
   for (int K = 1; K <= nk; ++K) {
-    const int64_t kk = static_cast<int64_t>(K) * (K - 1) / 2;  // sum_{k<K} k
-    double* th = theta_all + kk * nf * 5;
-    double* g = gamma_all + kk * N;
-    double* pi = pi_all + kk;
-    double* lik = lik_all + static_cast<int64_t>(K - 1) * N;
-    const int32_t* lk = lab + static_cast<int64_t>(K - 1) * N;
-    double b0 = NAN;
-    for (int tries = 5; isnan(b0) && tries != 0; --tries) {
-      for (int r = tid; r < N * K; r += blockDim.x) g[r] = (lk[r / K] - 1 == r % K) ? 1.0 : 0.0;
-      __syncthreads();
-      m_step(W, K, xt, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh, &lds);
-      e_step<MFMA>(W, K, xr, pi, lt, A, M, g, &lds);
-      for (int it = 0; it < cfg.n_step; ++it) {
-        m_step(W, K, xt, g, pi, gsum, th, lt, rng, rng_len, cfg.eps, &sh, &lds);
-        e_step<MFMA>(W, K, xr, pi, lt, A, M, g, &lds);
-        for (int i = tid; i < N; i += blockDim.x) {
-          double s = 0.0;
-          for (int k = 0; k < K; ++k) s += (A[i * K + k] + log(clip_eps(pi[k], cfg.eps))) * g[i * K + k];
-          lik[i] = s;
-        }
-        __syncthreads();
-      }
-      // BIC with ZeroParamNum = 0 decides the NaN retry (EMCluster :249-252)
-      const double tot = np_pairwise(lik, N);
-      b0 = 2.0 * tot - static_cast<double>(K - 1 + static_cast<int64_t>(K) * nf * 4) * logN;
-      __syncthreads();
-    }
-    if (tid == 0) {
-      const double tot = np_pairwise(lik, N);
-      bic[K - 1] = 2.0 * tot - static_cast<double>(K - 1 + static_cast<int64_t>(K) * nf * 4 - W.zero_params) * logN;
-    }
-    __syncthreads();
+    const EmK P = em_k_ptrs(W, ws, K);
+    EmLds lds = em_lds(W, P, lds_dyn);
+    em_run_k<MFMA>(W, K, P, xt, xr, labels + W.lab_off, rng, rng_len, cfg, &sh, &lds, outd + W.outd_off);
   }
-  if (tid == 0) {
-    int32_t* oi = outi + W.outi_off;  // [K, best, status, pad, rng_used(lo), rng_used(hi), Rclust[N]]
-    int best = -1;
-    for (int k = 0; k < nk; ++k)
-      if (!isnan(bic[k]) && (best < 0 || bic[k] > bic[best])) best = k;
-    int status = sh.error ? 2 : 0;
-    if (best < 0) status = 3;  // nanargmax of an all-NaN list (numpy raises)
-    int K = best + 1;
-    if (status == 0 && K == 1) {
-      if (nk < 2) status = 4;  // reference indexes BICList[1] (IndexError)
-      else if (bic[0] - bic[1] <= nf * logN) { K = 2; best = 1; }
-    }
-    oi[0] = K;
-    oi[1] = best;
-    oi[2] = status;
-    oi[3] = 0;
-    oi[4] = static_cast<int32_t>(sh.rng_off & 0xFFFFFFFFu);
-    oi[5] = static_cast<int32_t>(sh.rng_off >> 32);
-    if (status == 0) {
-      const int64_t kk = static_cast<int64_t>(K) * (K - 1) / 2;
-      const double* g = gamma_all + kk * N;
-      const double* lik = lik_all + static_cast<int64_t>(K - 1) * N;
-      for (int i = 0; i < N; ++i) {
-        int am = 0;
-        for (int k = 1; k < K; ++k)
-          if (g[i * K + k] > g[i * K + am]) am = k;
-        oi[6 + i] = am;
-        bic[nk + i] = lik[i];
-      }
-    }
+  if (threadIdx.x == 0) em_select(W, ws, outd, outi, sh.rng_off, sh.error != 0);
+}
+
+// K-parallel path.  The K values of a window depend on each other only through
+// the RNG stream: K draws from it (a dirichlet re-initialisation) at the
+// position the smaller K left it.  em_k_kernel runs every (window, K) in its
+// own workgroup from position 0 and records how much it drew; em_select_kernel
+// accepts a window when no K drew after an earlier K had drawn (then every
+// draw happened at the position the sequential order gives it, and the
+// results are the sequential kernel's), and flags the others for a rerun in
+// order (oi[3] = 1, em_cluster_kernel on those windows).
+__global__ __launch_bounds__(256) void em_x_kernel(const EmWindow* __restrict__ wins, const uint8_t* __restrict__ X,
+                                                   double* __restrict__ ws) {
+  const EmWindow W = wins[blockIdx.x];
+  const EmWsLayout L = em_ws_layout(W.n_reads, W.n_feat, W.kmax);
+  uint8_t* xt = reinterpret_cast<uint8_t*>(ws + W.ws_off) + L.xt_bytes;
+  em_build_x(W, X + W.x_off, xt, xt + L.xr_rel);
+}
+
+template <bool MFMA>
+__global__ __launch_bounds__(256) void em_k_kernel(const EmWindow* __restrict__ wins,
+                                                   const int32_t* __restrict__ labels,
+                                                   const double* __restrict__ rng, uint64_t rng_len, EmConfig cfg,
+                                                   double* __restrict__ ws, double* __restrict__ outd) {
+  __shared__ EmShared sh;
+  extern __shared__ double lds_dyn[];
+  const EmWindow W = wins[blockIdx.x];
+  const int K = static_cast<int>(blockIdx.y) + 1;
+  if (K > W.kmax - 1) return;
+  const EmWsLayout L = em_ws_layout(W.n_reads, W.n_feat, W.kmax);
+  const uint8_t* xt = reinterpret_cast<const uint8_t*>(ws + W.ws_off) + L.xt_bytes;
+  const EmK P = em_k_ptrs(W, ws, K);
+  EmLds lds = em_lds(W, P, lds_dyn);
+  if (threadIdx.x == 0) { sh.rng_off = 0; sh.error = 0; sh.reinit = 0; }
+  __threadfence_block();
+  __syncthreads();
+  em_run_k<MFMA>(W, K, P, xt, xt + L.xr_rel, labels + W.lab_off, rng, rng_len, cfg, &sh, &lds, outd + W.outd_off);
+  if (threadIdx.x == 0) {
+    uint64_t* spec = reinterpret_cast<uint64_t*>(ws + W.ws_off + L.spec) + 2 * (K - 1);
+    spec[0] = sh.rng_off;
+    spec[1] = static_cast<uint64_t>(sh.error);
   }
+}
+
+__global__ __launch_bounds__(64) void em_select_kernel(const EmWindow* __restrict__ wins, int n,
+                                                       double* __restrict__ ws, double* __restrict__ outd,
+                                                       int32_t* __restrict__ outi) {
+  const int w = blockIdx.x * 64 + static_cast<int>(threadIdx.x);
+  if (w >= n) return;
+  const EmWindow W = wins[w];
+  const EmWsLayout L = em_ws_layout(W.n_reads, W.n_feat, W.kmax);
+  const uint64_t* spec = reinterpret_cast<const uint64_t*>(ws + W.ws_off + L.spec);
+  uint64_t off = 0;
+  bool ok = true, error = false;
+  for (int K = 1; K <= W.kmax - 1; ++K) {
+    const uint64_t used = spec[2 * (K - 1)];
+    if (used != 0 && off != 0) ok = false;  // K drew from a position the speculation did not start it at
+    error |= spec[2 * (K - 1) + 1] != 0;
+    off += used;
+  }
+  if (!ok) {
+    outi[W.outi_off + 3] = 1;
+    return;
+  }
+  em_select(W, ws, outd, outi, off, error);
 }
 
 hipError_t launch_similarity(const EmWindow* wins, int n, const uint8_t* X, const int64_t* s_off, double* S,
@@ -487,18 +586,37 @@ hipError_t launch_similarity(const EmWindow* wins, int n, const uint8_t* X, cons
 
 hipError_t launch_em_cluster(const EmWindow* wins, int n, const uint8_t* X, const int32_t* labels,
                              const double* rng, uint64_t rng_len, const EmConfig& cfg, double* ws, double* outd,
-                             int32_t* outi, hipStream_t stream) {
+                             int32_t* outi, size_t lds_doubles, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
+  const size_t lds = lds_doubles * sizeof(double);
   // SVS_EM_MFMA=1: the E-step contraction on v_mfma_f64_16x16x4_f64 (measured
   // alternative, see e_accumulate_mfma); default: the one-hot gather
   const char* me = std::getenv("SVS_EM_MFMA");  // read per launch (a few per batch): tests switch it
   const bool mfma = me && me[0] == '1';
   if (mfma)
-    hipLaunchKernelGGL(em_cluster_kernel<true>, dim3(n), dim3(256), 0, stream, wins, X, labels, rng, rng_len, cfg,
+    hipLaunchKernelGGL(em_cluster_kernel<true>, dim3(n), dim3(256), lds, stream, wins, X, labels, rng, rng_len, cfg,
                        ws, outd, outi);
   else
-    hipLaunchKernelGGL(em_cluster_kernel<false>, dim3(n), dim3(256), 0, stream, wins, X, labels, rng, rng_len, cfg,
+    hipLaunchKernelGGL(em_cluster_kernel<false>, dim3(n), dim3(256), lds, stream, wins, X, labels, rng, rng_len, cfg,
                        ws, outd, outi);
+  return hipGetLastError();
+}
+
+hipError_t launch_em_parallel(const EmWindow* wins, int n, int max_nk, const uint8_t* X, const int32_t* labels,
+                              const double* rng, uint64_t rng_len, const EmConfig& cfg, double* ws, double* outd,
+                              int32_t* outi, size_t lds_doubles, hipStream_t stream) {
+  if (n <= 0 || max_nk <= 0) return hipSuccess;
+  const size_t lds = lds_doubles * sizeof(double);
+  const char* me = std::getenv("SVS_EM_MFMA");
+  const bool mfma = me && me[0] == '1';
+  hipLaunchKernelGGL(em_x_kernel, dim3(n), dim3(256), 0, stream, wins, X, ws);
+  if (mfma)
+    hipLaunchKernelGGL(em_k_kernel<true>, dim3(n, max_nk), dim3(256), lds, stream, wins, labels, rng, rng_len, cfg,
+                       ws, outd);
+  else
+    hipLaunchKernelGGL(em_k_kernel<false>, dim3(n, max_nk), dim3(256), lds, stream, wins, labels, rng, rng_len, cfg,
+                       ws, outd);
+  hipLaunchKernelGGL(em_select_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, wins, n, ws, outd, outi);
   return hipGetLastError();
 }
 
@@ -515,18 +633,14 @@ __global__ __launch_bounds__(256) void em_gather_kernel(const EmWindow* __restri
   const EmWindow W = wins[blockIdx.x];
   const int32_t* oi = outi + W.outi_off;
   if (oi[2] != 0) return;
-  const int K = oi[0], N = W.n_reads, nf = W.n_feat, nk = W.kmax - 1;
-  const double* theta_all = ws + W.ws_off;
-  const int64_t th_total = static_cast<int64_t>(nk) * (nk + 1) / 2 * nf * 5;
-  const double* gamma_all = theta_all + th_total + static_cast<int64_t>(nk) * nf * 5;
-  const double* pi_all = gamma_all + static_cast<int64_t>(nk) * (nk + 1) / 2 * N;
-  const int64_t kk = static_cast<int64_t>(K) * (K - 1) / 2;
+  const int K = oi[0], N = W.n_reads, nf = W.n_feat;
+  const EmK P = em_k_ptrs(W, const_cast<double*>(ws), K);
   double* p = par + W.par_off;
-  for (int64_t r = threadIdx.x; r < static_cast<int64_t>(N) * K; r += blockDim.x) p[r] = gamma_all[kk * N + r];
-  for (int r = threadIdx.x; r < K; r += blockDim.x) p[static_cast<int64_t>(N) * K + r] = pi_all[kk + r];
+  for (int64_t r = threadIdx.x; r < static_cast<int64_t>(N) * K; r += blockDim.x) p[r] = P.g[r];
+  for (int r = threadIdx.x; r < K; r += blockDim.x) p[static_cast<int64_t>(N) * K + r] = P.pi[r];
   double* t = p + static_cast<int64_t>(N) * K + K;
   for (int64_t r = threadIdx.x; r < static_cast<int64_t>(K) * nf * 5; r += blockDim.x)
-    t[r] = theta_all[kk * nf * 5 + r];
+    t[r] = P.th[r];
 }
 
 hipError_t launch_em_gather(const EmWindow* wins, int n, const double* ws, const int32_t* outi, double* par,

@@ -197,13 +197,6 @@ __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, cons
 #define SVS_FOLD_PRIO_LEVEL 3
 #endif
 #define SVS_FOLD_PRIO() __builtin_amdgcn_s_setprio(SVS_FOLD_PRIO_LEVEL)
-// The sort (the longest fold kernel) may instead start at the DP waves'
-// priority and raise its own once it has run SVS_FOLD_RAISE_TICKS x 10 ns
-// (0: raised from the start), so that early finishers never take issue slots
-// ahead of the DP waves while late ones still meet their group's next launch.
-#ifndef SVS_FOLD_RAISE_TICKS
-#define SVS_FOLD_RAISE_TICKS 0
-#endif
 
 // ---------------------------------------------------------------- update
 // spoa Graph::AddAlignment (poa_graph.cpp add_alignment_nodes): nodes of the
@@ -436,8 +429,6 @@ struct SortState {
   bool err;            // the stack outgrew its spill area
   uint32_t n_exam, n_roots;  // statistics
   uint64_t prof[4];          // SVS_FOLD_PROF: fast roots, DFS runs, window loads, rest (clocks)
-  uint64_t raise_at;         // s_memrealtime at which the wave raises its priority (SVS_FOLD_RAISE_TICKS)
-  bool raised;
 };
 // Profile builds (tools/build_variant.py): SVS_FOLD_PROF: fast-root and DFS-run
 // clocks, window loads; SVS_FOLD_PROF_EXAM: the DFS examination's phases
@@ -530,6 +521,17 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
   // its column) and go out 64 at a time, one store per table per 64 nodes
   // (nothing reads an emitted node's entries during the sort).
   uint32_t eb_node = 0, eb_col = 0, eb_n = 0;
+  // the buffered emissions out (positions cnt - eb_n ..): before any store
+  // that advances cnt otherwise (the bulk path) and at the end
+  auto flush_emit = [&]() {
+    if (lane < eb_n) {
+      const uint32_t rk = cnt - eb_n + lane;
+      r2n[rk] = eb_node;
+      n2r[eb_node] = rk;
+      col[eb_node] = eb_col;
+    }
+    eb_n = 0;
+  };
   auto emit = [&](uint32_t node) {
     const bool mine = lane == eb_n;  // (selects: lane eb_n takes the entry)
     eb_node = mine ? node : eb_node;
@@ -642,11 +644,6 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
     push(root);
     uint32_t cur = root;
     while (!S.err) {
-      if (SVS_FOLD_RAISE_TICKS > 0 && (steps & 255u) == 0 && !S.raised &&
-          __builtin_amdgcn_s_memrealtime() >= S.raise_at) {
-        __builtin_amdgcn_s_setprio(SVS_FOLD_PRIO_LEVEL);
-        S.raised = true;
-      }
       if (++steps > max_steps) {
         S.err = true;
         break;
@@ -727,13 +724,7 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
     SVS_PF_ADD(1, pf0);
     ++root;
   }
-  // the buffered emissions
-  if (lane < eb_n) {
-    const uint32_t rk = cnt - eb_n + lane;
-    r2n[rk] = eb_node;
-    n2r[eb_node] = rk;
-    col[eb_node] = eb_col;
-  }
+  flush_emit();
   *ncol_out = ncol;
   S.n_exam = static_cast<uint32_t>(steps);
   return (cnt == V && !S.err) ? kFoldOk : kFoldErrStack;
@@ -1006,7 +997,7 @@ __device__ void msa_rows(uint32_t n_paths, const gu32* __restrict__ paths, const
 }
 
 __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __restrict__ jobs, uint32_t lds_words) {
-  if (SVS_FOLD_RAISE_TICKS == 0) SVS_FOLD_PRIO();
+  SVS_FOLD_PRIO();
   extern __shared__ uint32_t lds[];
   const uint64_t T0 = __builtin_amdgcn_s_memrealtime();
   const FoldJob J = jobs[blockIdx.x];
@@ -1029,8 +1020,6 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
   S.n_exam = 0;
   S.n_roots = 0;
   S.prof[0] = S.prof[1] = S.prof[2] = S.prof[3] = 0;
-  S.raise_at = T0 + SVS_FOLD_RAISE_TICKS;
-  S.raised = SVS_FOLD_RAISE_TICKS == 0;
   uint32_t ncol = 0;
   if (S.cap < 64) {
     if (lanei() == 0) res->status = kFoldErrStack;
@@ -1060,7 +1049,6 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
   }
   wave_sync_mem();
   const uint64_t T1 = __builtin_amdgcn_s_memrealtime();
-  if (!S.raised) SVS_FOLD_PRIO();  // the export: the last step before the prep kernel
   uint32_t n_slots = 0, max_preds = 0;
   if (J.flags & kFoldExport)
     export_lite(V, g.base, g.in_off, g.in_nbr, g.out_off, g.r2n, g.n2r, g.last, g.pstart, g.pred, g.info, &n_slots,

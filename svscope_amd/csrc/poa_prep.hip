@@ -30,6 +30,15 @@
 #include "poa_graph.hpp"
 #include "svs_device.hpp"
 
+// Issue priority of the device-graph prep kernel: the DP waves' own (the
+// fold waves of poa_fold.hip issue ahead of them).  Its scalar row loops then
+// take issue slots only when the DP waves leave them, and it still ends well
+// inside the other group's DP launch: 240.5 vs 238.2 windows/s, DP launch
+// 26.8 vs 27.3 ms (profiles/r03_em1).
+#ifndef SVS_PREP_PRIO_LEVEL
+#define SVS_PREP_PRIO_LEVEL 0
+#endif
+
 namespace svs {
 
 namespace {
@@ -273,10 +282,7 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
 // The same for the device-resident graphs (poa_dgraph.hpp): the jobs whose
 // fold exported the next alignment's lite tables into their block.
 __global__ __launch_bounds__(192) void poa_dgraph_prep_kernel(const FoldJob* __restrict__ jobs, PoaScore P) {
-#ifndef SVS_FOLD_PRIO_LEVEL
-#define SVS_FOLD_PRIO_LEVEL 3
-#endif
-  __builtin_amdgcn_s_setprio(SVS_FOLD_PRIO_LEVEL);  // beside the DP kernel, on its group's critical chain (poa_fold.hip)
+  __builtin_amdgcn_s_setprio(SVS_PREP_PRIO_LEVEL);
   __shared__ uint32_t fl_ext[kStripPrepMaxSlots - 64];
   const FoldJob J = jobs[blockIdx.x];
   if (!(J.flags & kFoldExport)) return;

@@ -278,6 +278,7 @@ class Pipeline {
     std::unique_ptr<svs_em_result> r = em->fut.get();
     st.em_wall_ms += ms_since(em->t0);
     st.em_kernel_ms += r->kernel_ms;
+    st.em_reruns += r->em_reruns;
     const auto t0 = Clock::now();
     const std::vector<WinRef> ws = std::move(em->windows);
     em.reset();

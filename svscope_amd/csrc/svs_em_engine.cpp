@@ -146,7 +146,7 @@ svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, co
     if (wins[w].n_reads > (1 << 16))
       throw SvsError(SVS_E_UNSUPPORTED, "window " + std::to_string(w) + " has more than 65536 reads");
   std::vector<EmWindow> W(n);
-  uint64_t xbytes = 0, lab = 0, ws = 0, od = 0, oi = 0, par = 0;
+  uint64_t xbytes = 0, lab = 0, ws = 0, od = 0, oi = 0, par = 0, lds = 0;
   for (int32_t w = 0; w < n; ++w) {
     EmWindow& e = W[w];
     e.n_reads = wins[w].n_reads;
@@ -163,6 +163,7 @@ svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, co
     const uint64_t N = e.n_reads, nf = e.n_feat, nk = e.kmax - 1;
     xbytes += N * nf;
     lab += nk * N;
+    lds = std::max(lds, em_lds_doubles(e.n_reads, static_cast<int>(nk)));
     ws += (em_workspace_doubles(e.n_reads, e.n_feat, e.kmax) + 31) / 32 * 32;
     od += nk + N;
     oi += 6 + N;
@@ -171,7 +172,8 @@ svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, co
   const size_t off_w = 0;
   const size_t off_l = (n * sizeof(EmWindow) + 255) / 256 * 256;
   const size_t off_x = off_l + (lab * 4 + 255) / 256 * 256;
-  const size_t total = off_x + xbytes;
+  const size_t off_r = off_x + (xbytes + 255) / 256 * 256;  // the windows rerun in order (K-parallel path)
+  const size_t total = off_r + n * sizeof(EmWindow);
   ctx->h_em_in.ensure(total);
   char* h = ctx->h_em_in.as<char>();
   std::memcpy(h + off_w, W.data(), n * sizeof(EmWindow));
@@ -191,16 +193,44 @@ svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, co
   int32_t* d_outi = reinterpret_cast<int32_t*>(ctx->d_em_out.as<char>() + (od_bytes + 255) / 256 * 256);
   double* d_par = reinterpret_cast<double*>(reinterpret_cast<char*>(d_outi) + oi_bytes);
   EmConfig ec{cfg.n_step, 0, cfg.eps};
+  int max_nk = 0;
+  for (const EmWindow& e : W) max_nk = std::max(max_nk, e.kmax - 1);
+  // K-parallel unless SVS_EM_SEQ=1 (em_kernels.hip: windows the speculation
+  // cannot place are rerun in order below)
+  const char* seq_env = std::getenv("SVS_EM_SEQ");
+  const bool parallel = !(seq_env && seq_env[0] == '1');
   auto* res = new svs_em_result();
   try {
     uint64_t want = std::max<uint64_t>(ctx->rng_len, 1ull << 20);
+    const size_t outi_at = (od_bytes + 255) / 256 * 256;
     for (int attempt = 0;; ++attempt) {
       ensure_rng(ctx, static_cast<uint32_t>(cfg.seed), want);
       SVS_HIP(hipEventRecord(ctx->ev_start, ctx->em_stream));
-      SVS_HIP(launch_em_cluster(reinterpret_cast<const EmWindow*>(d + off_w), n,
-                                reinterpret_cast<const uint8_t*>(d + off_x), reinterpret_cast<const int32_t*>(d + off_l),
-                                ctx->d_rng.as<double>(), ctx->rng_len, ec, ctx->d_em_ws.as<double>(), d_outd, d_outi,
-                                ctx->em_stream));
+      const auto* dW = reinterpret_cast<const EmWindow*>(d + off_w);
+      const auto* dX = reinterpret_cast<const uint8_t*>(d + off_x);
+      const auto* dL = reinterpret_cast<const int32_t*>(d + off_l);
+      if (parallel) {
+        SVS_HIP(launch_em_parallel(dW, n, max_nk, dX, dL, ctx->d_rng.as<double>(), ctx->rng_len, ec,
+                                   ctx->d_em_ws.as<double>(), d_outd, d_outi, static_cast<size_t>(lds), ctx->em_stream));
+        SVS_HIP(hipMemcpyAsync(ctx->h_em_out.as<char>() + outi_at, d_outi, oi * 4, hipMemcpyDeviceToHost, ctx->em_stream));
+        SVS_HIP(hipStreamSynchronize(ctx->em_stream));
+        const int32_t* hi = reinterpret_cast<const int32_t*>(ctx->h_em_out.as<char>() + outi_at);
+        std::vector<EmWindow> rerun;
+        for (int32_t w = 0; w < n; ++w)
+          if (hi[W[w].outi_off + 3] == 1) rerun.push_back(W[w]);
+        res->em_reruns += static_cast<int64_t>(rerun.size());
+        if (!rerun.empty()) {
+          std::memcpy(h + off_r, rerun.data(), rerun.size() * sizeof(EmWindow));
+          SVS_HIP(hipMemcpyAsync(d + off_r, h + off_r, rerun.size() * sizeof(EmWindow), hipMemcpyHostToDevice,
+                                 ctx->em_stream));
+          SVS_HIP(launch_em_cluster(reinterpret_cast<const EmWindow*>(d + off_r), static_cast<int>(rerun.size()), dX,
+                                    dL, ctx->d_rng.as<double>(), ctx->rng_len, ec, ctx->d_em_ws.as<double>(), d_outd,
+                                    d_outi, static_cast<size_t>(lds), ctx->em_stream));
+        }
+      } else {
+        SVS_HIP(launch_em_cluster(dW, n, dX, dL, ctx->d_rng.as<double>(), ctx->rng_len, ec, ctx->d_em_ws.as<double>(),
+                                  d_outd, d_outi, static_cast<size_t>(lds), ctx->em_stream));
+      }
       if (cfg.want_params)
         SVS_HIP(launch_em_gather(reinterpret_cast<const EmWindow*>(d + off_w), n, ctx->d_em_ws.as<double>(), d_outi,
                                  d_par, ctx->em_stream));

@@ -20,6 +20,7 @@ struct svs_em_result {
   };
   std::vector<Win> w;
   double kernel_ms = 0.0;
+  int64_t em_reruns = 0;  // windows the K-parallel path handed to the in-order kernel
 };
 
 // Decision pipeline results (opaque to ABI users).
