@@ -430,23 +430,7 @@ struct SortState {
   uint32_t n_exam, n_roots;  // statistics
   uint64_t prof[4];          // SVS_FOLD_PROF: fast roots, DFS runs, window loads, rest (clocks)
 };
-// Profile builds (tools/build_variant.py): SVS_FOLD_PROF: fast-root and DFS-run
-// clocks, window loads; SVS_FOLD_PROF_EXAM: the DFS examination's phases
-// (record, flag reads, pushes/emits, pop) in prof[0..3].
-#if defined(SVS_FOLD_PROF) || defined(SVS_FOLD_PROF_EXAM)
-#define SVS_PF_CLK() __builtin_readcyclecounter()
-#else
-#define SVS_PF_CLK() 0ull
-#endif
-#ifdef SVS_FOLD_PROF_EXAM
-#define SVS_PF_COUNT(k) ((void)0)
-#define SVS_PF_ADD(k, t) ((void)0)
-#define SVS_PF_EXAM(k, t) (S.prof[k] += SVS_PF_CLK() - (t))
-#else
-#define SVS_PF_COUNT(k) (S.prof[k] += 1)
-#define SVS_PF_ADD(k, t) (S.prof[k] += SVS_PF_CLK() - (t))
-#define SVS_PF_EXAM(k, t) ((void)0)
-#endif
+#include "poa_fold_prof.hpp"  // development profile builds only; no-ops otherwise
 
 __device__ __forceinline__ bool bit_of(const uint32_t* plane, uint32_t v) { return (plane[v >> 5] >> (v & 31u)) & 1u; }
 
@@ -1062,10 +1046,7 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
     res->t_exp = static_cast<uint32_t>(T2 - T1);
     res->n_exam = S.n_exam;
     res->n_roots = S.n_roots;
-    for (int k = 0; k < 4; ++k) res->prof[k] = static_cast<uint32_t>(S.prof[k] >> (k < 2 ? 10 : 0));
-#ifdef SVS_FOLD_PROF_EXAM
-    for (int k = 0; k < 4; ++k) res->prof[k] = static_cast<uint32_t>(S.prof[k] >> 10);
-#endif
+    for (int k = 0; k < 4; ++k) res->prof[k] = static_cast<uint32_t>(S.prof[k] >> SVS_PF_SHIFT(k));
   }
 }
 
