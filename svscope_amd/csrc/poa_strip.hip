@@ -61,9 +61,13 @@ static_assert(kSlotInts * 4 == kStripSlotBytes, "pool slot size");
 // the recurrence and the traceback codes exact (a clamped F' = H - tF gives
 // F' + e = H + g - 1, below the H + g it is compared with, just like the true
 // F).  Halves the pool in LDS, so twice the waves fit on a CU.
-__device__ __forceinline__ uint32_t pack_fo(int32_t H, int32_t F, int32_t O, uint32_t tF, uint32_t tO) {
-  const uint32_t dF = min(static_cast<uint32_t>(H) - static_cast<uint32_t>(F), tF);
-  const uint32_t dO = min(static_cast<uint32_t>(H) - static_cast<uint32_t>(O), tO);
+//
+// The clamp itself is 255 (one literal operand, no SGPR): any clamp T >= tF
+// keeps F' + e < H + g (tF, tO <= 255 host-checked), and below it the stored
+// distance is the true one.
+__device__ __forceinline__ uint32_t pack_fo(int32_t H, int32_t F, int32_t O) {
+  const uint32_t dF = min(static_cast<uint32_t>(H) - static_cast<uint32_t>(F), 255u);
+  const uint32_t dO = min(static_cast<uint32_t>(H) - static_cast<uint32_t>(O), 255u);
   return dF | (dO << 8);
 }
 
@@ -207,7 +211,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   const int job_id = blockIdx.x;
   if (job_id >= n_jobs) return;
   const PoaJob J = jobs[job_id];
-  const uint32_t tF = static_cast<uint32_t>(P.e - P.g + 1), tO = static_cast<uint32_t>(P.c - P.q + 1);
   const int32_t L = static_cast<int32_t>(J.len);
   const uint32_t LS = J.ls;
   const uint32_t V = J.n_rows;
@@ -305,7 +308,9 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     auto ub_of = [&](uint32_t w2, int32_t rr, int32_t mr) -> int32_t {
       const int32_t dmin = static_cast<int32_t>(w2 & 0xFFFFu), dmax = static_cast<int32_t>(w2 >> 16);
       const int32_t d = min(imax(rr, dmin), dmax) - rr;
-      return mr + d * (d >= 0 ? cg : P.m - cg);
+      // 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate): |d| < 2^16
+      // and the scores are host-checked to a few thousand
+      return mr + __mul24(d, d >= 0 ? cg : P.m - cg);
     };
     StripConst K;
     if (!FIRST) {
@@ -324,7 +329,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       const int32_t h0 = row0_h(P, j), fo0 = j == 0 ? 0 : SVS_NEG_INF;
       pool[lane + 1] = h0;
       if (lane == 0) pool[0] = FIRST ? 0 : row0_h(P, j0 - 1);
-      reinterpret_cast<uint16_t*>(pool + 65)[lane] = static_cast<uint16_t>(pack_fo(h0, fo0, fo0, tF, tO));
+      reinterpret_cast<uint16_t*>(pool + 65)[lane] = static_cast<uint16_t>(pack_fo(h0, fo0, fo0));
     }
     __builtin_amdgcn_wave_barrier();
 
@@ -592,7 +597,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         int32_t* q = pool + own * kStride;
         q[lane + 1] = H;
         q[lane] = prevH;
-        reinterpret_cast<uint16_t*>(q + 65)[lane] = static_cast<uint16_t>(pack_fo(H, F, O, tF, tO));
+        reinterpret_cast<uint16_t*>(q + 65)[lane] = static_cast<uint16_t>(pack_fo(H, F, O));
       }
       pH = H;
       pF = F;

@@ -46,6 +46,10 @@ void check_poa_config(const svs_poa_config& c) {
   // the strip kernel stores F and O as 8-bit distances to H clamped at e-g+1, c-q+1
   if (c.e - c.g + 1 > 255 || c.c - c.q + 1 > 255)
     throw SvsError(SVS_E_UNSUPPORTED, "gap parameters too far apart for the packed F/O pool");
+  // the pruning bound multiplies path-length differences (< 2^16) by scores
+  // with 24-bit multiplies
+  for (const int32_t x : {c.m, c.n, c.g, c.e, c.q, c.c})
+    if (x > 4096 || x < -4096) throw SvsError(SVS_E_UNSUPPORTED, "scores beyond +-4096 are not supported");
 }
 
 namespace {

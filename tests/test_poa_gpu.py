@@ -75,6 +75,8 @@ def test_unsupported_modes_raise():
         poa(["ACGT", "ACGA"], 0)
     with pytest.raises(_abi.SvsError):
         poa(["ACGT", "ACGA"], 1, g=-2, e=-6)  # linear subtype
+    with pytest.raises(_abi.SvsError):
+        poa(["ACGT", "ACGA"], 1, m=5000)  # beyond the 24-bit pruning-bound multiplies
 
 
 def test_genmsa_false_and_min_coverage():
