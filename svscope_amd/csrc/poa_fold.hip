@@ -432,6 +432,13 @@ struct SortState {
 };
 #include "poa_fold_prof.hpp"  // development profile builds only; no-ops otherwise
 
+// lane L of x replaced by the uniform s (one v_writelane_b32)
+template <int L> __device__ __forceinline__ uint32_t write_lane_c(uint32_t x, uint32_t s) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(s), "n"(L));
+  return x;
+}
+#define write_lane(x, s, L) write_lane_c<L>((x), (s))
+
 __device__ __forceinline__ bool bit_of(const uint32_t* plane, uint32_t v) { return (plane[v >> 5] >> (v & 31u)) & 1u; }
 
 }  // namespace
@@ -640,15 +647,26 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
       SVS_PF_EXAM(0, px0);
       [[maybe_unused]] const uint64_t px1 = SVS_PF_CLK();
       const uint32_t deg = w1 & 0xFFFFFFu, alc = w1 >> 24;
-      const uint32_t dc = uni(done_of(cur)), ig = uni(bit_of(S.ign, cur) ? 1u : 0u);
-      // (unused slots read cur's word and count as done; they are never looked
-      // at: all eight reads issue together, one wait; ids below the root are
-      // done)
-      auto dn = [&](bool used, uint32_t v) -> uint32_t {
-        return uni(done_of(used ? v : cur) | (used && v >= root ? 0u : 1u));
-      };
-      const uint32_t d0 = dn(deg > 0, t0), d1 = dn(deg > 1, t1), d2 = dn(deg > 2, t2);
-      const uint32_t e0 = dn(alc > 0, m0), e1 = dn(alc > 1, m1), e2 = dn(alc > 2, m2);
+      // The eight flags in one vector read and one ballot: lane k < 3 tail k,
+      // lanes 3..5 aligned node k - 3 (unused slots read cur's word and count
+      // as done; ids below the root are done), lane 6 cur's done bit, lane 7
+      // cur's ignore bit (was eight scalar address computations and reads).
+      uint32_t fid = cur;
+      fid = write_lane(fid, t0, 0);
+      fid = write_lane(fid, t1, 1);
+      fid = write_lane(fid, t2, 2);
+      fid = write_lane(fid, m0, 3);
+      fid = write_lane(fid, m1, 4);
+      fid = write_lane(fid, m2, 5);
+      const bool fused = lane < 3u ? lane < deg : (lane < 6u ? lane - 3u < alc : false);
+      const uint32_t fv = fused ? fid : cur;
+      const uint32_t* fplane = lane == 7u ? S.ign : S.done;
+      const uint32_t fbit = (fplane[fv >> 5] >> (fv & 31u)) & 1u;
+      const uint64_t fm = ballot(fbit != 0u || (lane < 6u && !(fused && fv >= root)));
+      const uint32_t fl = static_cast<uint32_t>(fm);
+      const uint32_t dc = (fl >> 6) & 1u, ig = (fl >> 7) & 1u;
+      const uint32_t d0 = fl & 1u, d1 = (fl >> 1) & 1u, d2 = (fl >> 2) & 1u;
+      const uint32_t e0 = (fl >> 3) & 1u, e1 = (fl >> 4) & 1u, e2 = (fl >> 5) & 1u;
       bool pop = dc != 0;
       SVS_PF_EXAM(1, px1);
       [[maybe_unused]] const uint64_t px2 = SVS_PF_CLK();
