@@ -47,6 +47,7 @@ constexpr uint32_t kChunk = 64;
 constexpr uint32_t kRegEdges = 128;  // in-edges of a chunk held in two VGPRs; more spill to LDS
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t lane_of(uint32_t v, uint32_t l) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(v), static_cast<int32_t>(l)));
 }
@@ -186,29 +187,98 @@ __device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base
     }
     if (ebase + lane < E) pslot[ebase + lane] = ebuf;
   } else if (wave == 1) {
-    // fewest nodes from a source -> column 0: F0 = g + sd e, O0 = q + sd c
-    uint32_t sd_prev = 0;
+    // fewest nodes from a source -> column 0: F0 = g + sd e, O0 = q + sd c.
+    // Lane-parallel per chunk (lane i = row r0 + i), vector issue only:
+    // sd[r] = min over in-edges p of sd[p] + 1 (a source: 0).  In-edges from
+    // earlier chunks are final and fold into a per-row base; the in-edge from
+    // the row just above (the rank chain) makes sd a min-plus scan along
+    // chain segments, sd[i] = min over k in [start(i), i] of y[k] + i - k;
+    // the other in-edges inside the chunk (merge edges) enter y from the
+    // previous estimate, and the chunk repeats until nothing changes.  From
+    // all-INF estimates every round is an upper bound and every row is final
+    // once its in-chunk merge depth is reached, so the fixed point is the
+    // sequential DP's value (an unchanged round is that fixed point).
+    const int32_t ilane = static_cast<int32_t>(lane);
     uint32_t pwin = 0;  // lane i: sd of row r0 - 64 + i (the chunk before)
     Chunk cur = load(0);
     for (;;) {
       const Chunk nxt = cur.r0 + kChunk < V ? load(cur.r0 + kChunk) : cur;
-      uint32_t win = 0;  // lane i: sd of row r0 + i
-      for (uint32_t i = 0; i < cur.n; ++i) {
-        const uint32_t r = cur.r0 + i;
-        const uint32_t a = pstart_of(cur, i), b = pstart_of(cur, i + 1);
-        uint32_t sd = a == b ? 0u : 0x3FFFFFFFu;  // a source: 0
-        for (uint32_t x = a; x < b; ++x) {
-          const uint32_t pr = (edge(cur, x) & 0x7FFFFFFFu) - 1;
-          const uint32_t sdp =
-              pr + 1 == r ? sd_prev
-                          : (pr >= cur.r0 ? lane_of(win, pr - cur.r0)
-                                          : (pr + kChunk >= cur.r0 ? lane_of(pwin, pr + kChunk - cur.r0)
-                                                                   : far(pr)));
-          sd = min(sd, sdp + 1);
+      const bool in = lane < cur.n;
+      const uint32_t a = in ? cur.ps : 0u;
+      const uint32_t bn = static_cast<uint32_t>(__shfl(static_cast<int32_t>(cur.ps), min(ilane + 1, 63), 64));
+      const uint32_t b = in ? (lane + 1 < cur.n ? bn : cur.e1) : 0u;
+      const uint32_t deg = b - a;
+      uint32_t maxdeg = deg;
+      for (int o = 32; o >= 1; o >>= 1) maxdeg = max(maxdeg, static_cast<uint32_t>(__shfl_xor(static_cast<int32_t>(maxdeg), o, 64)));
+      maxdeg = uni(maxdeg);
+      uint32_t base = deg == 0 ? 0u : 0x3FFFFFFFu;  // min over in-edges from earlier chunks (+1)
+      bool chain = false;                           // in-edge from the row just above, inside the chunk
+      uint32_t q = 0xFFFFFFFFu;                     // up to 4 in-chunk merge in-edges (byte = lane, 0xFF none)
+      bool ovf = false;                             // more than 4 of them: re-read each round
+      for (uint32_t x = 0; x < maxdeg; ++x) {
+        const bool has = x < deg;
+        const uint32_t pr = has ? (gpr[a + x] & 0x7FFFFFFFu) - 1u : 0u;
+        const bool inchunk = has && pr >= cur.r0;
+        const bool prevc = has && !inchunk && pr + kChunk >= cur.r0;
+        const bool farp = has && !inchunk && !prevc;
+        const uint32_t pv = static_cast<uint32_t>(
+            __shfl(static_cast<int32_t>(pwin), prevc ? static_cast<int32_t>(pr + kChunk - cur.r0) : ilane, 64));
+        if (prevc) base = min(base, pv + 1u);
+        if (ballot(farp)) {
+          if (dirty) {
+            flush_fence();
+            dirty = false;
+          }
+          if (farp) base = min(base, ld(scr + pr) + 1u);
         }
-        sd_prev = sd;
-        win = set_lane(sd, i, win);
+        if (inchunk) {
+          if (pr + 1u == cur.r0 + lane) {
+            chain = true;
+          } else {
+            const uint32_t off = pr - cur.r0;
+            if ((q >> 24) != 0xFFu) ovf = true;
+            else q = (q << 8) | off;
+          }
+        }
       }
+      // chain segments: lane i's segment starts at the last lane <= i without
+      // a chain in-edge
+      const uint64_t starts = ballot(!chain);
+      const uint64_t upto = starts & (lane == 63u ? ~0ull : ((2ull << lane) - 1ull));
+      const int32_t seg0 = 63 - static_cast<int32_t>(__builtin_clzll(upto));  // lane 0 is always a start
+      uint32_t sd = 0x3FFFFFFFu;
+      const bool any_ovf = ballot(ovf) != 0;
+      for (;;) {
+        uint32_t y = base;
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t off = (q >> (8 * k)) & 0xFFu;
+          const uint32_t v = static_cast<uint32_t>(
+              __shfl(static_cast<int32_t>(sd), off != 0xFFu ? static_cast<int32_t>(off) : ilane, 64));
+          if (off != 0xFFu) y = min(y, v + 1u);
+        }
+        if (any_ovf) {
+          for (uint32_t x = 0; x < maxdeg; ++x) {
+            const bool has = ovf && x < deg;
+            const uint32_t pr = has ? (gpr[a + x] & 0x7FFFFFFFu) - 1u : 0u;
+            const bool use = has && pr >= cur.r0 && pr + 1u != cur.r0 + lane;
+            const uint32_t v = static_cast<uint32_t>(
+                __shfl(static_cast<int32_t>(sd), use ? static_cast<int32_t>(pr - cur.r0) : ilane, 64));
+            if (use) y = min(y, v + 1u);
+          }
+        }
+        // segmented min-plus scan: z[i] = y[i] - i, prefix min within the segment, + i
+        int32_t z = static_cast<int32_t>(y) - ilane;
+        for (int d = 1; d < 64; d <<= 1) {
+          const int32_t o = __shfl(z, max(ilane - d, 0), 64);
+          if (ilane - d >= seg0) z = min(z, o);
+        }
+        // (capped at the all-INF start: every round is then <= the last)
+        const uint32_t nsd = min(static_cast<uint32_t>(z + ilane), 0x3FFFFFFFu);
+        const bool changed = ballot(nsd != sd) != 0;
+        sd = nsd;
+        if (!changed) break;
+      }
+      const uint32_t win = in ? sd : 0u;  // lane i: sd of row r0 + i
       if (lane < cur.n) {
         const uint64_t r = cur.r0 + lane;
         scr[r] = win;
