@@ -463,32 +463,44 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
   // order, so a bit set or a push is seen by the next read without a wait;
   // only the spill area (global memory) needs its stores drained.
   uint32_t top = 0;  // the entry last pushed
-  auto push = [&](uint32_t v) {
-    if (S.sp == S.cap) {
-      // spill the lower half of the LDS part
-      const uint32_t half = S.cap / 2;
-      if (S.spilled + half > S.spill_cap) {
-        S.err = true;
-        return;
-      }
-      // (loops with uniform trip counts and predicated lanes: a loop whose
-      // lanes leave at different trips makes the whole DFS loop divergent)
-      for (uint32_t k0 = 0; k0 < half; k0 += 64) {
-        const uint32_t k = k0 + lane;
-        if (k < half) S.spill[S.spilled + k] = S.st[k];
-      }
-      for (uint32_t k0 = 0; k0 < half; k0 += 64) {
-        const uint32_t k = k0 + lane;
-        const uint32_t x = k < half ? S.st[k + half] : 0u;
-        __builtin_amdgcn_wave_barrier();
-        if (k < half) S.st[k] = x;
-      }
-      S.spilled += half;
-      S.sp -= half;
+  // spill the lower half of the LDS part (S.sp >= half); false: no room
+  auto spill_half = [&]() -> bool {
+    const uint32_t half = S.cap / 2;
+    if (S.spilled + half > S.spill_cap) {
+      S.err = true;
+      return false;
     }
+    // (loops with uniform trip counts and predicated lanes: a loop whose
+    // lanes leave at different trips makes the whole DFS loop divergent)
+    for (uint32_t k0 = 0; k0 < half; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      if (k < half) S.spill[S.spilled + k] = S.st[k];
+    }
+    for (uint32_t k0 = 0; k0 < half; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      const uint32_t x = k < half ? S.st[k + half] : 0u;
+      __builtin_amdgcn_wave_barrier();
+      if (k < half) S.st[k] = x;
+    }
+    S.spilled += half;
+    S.sp -= half;
+    return true;
+  };
+  auto push = [&](uint32_t v) {
+    if (S.sp == S.cap && !spill_half()) return;
     S.st[S.sp] = v;  // (every lane the same word: no divergent branch)
     ++S.sp;
     top = v;
+  };
+  // The lanes of pm push their val, in lane order (one store for all); the
+  // highest one ends on top.
+  auto push_lanes = [&](uint64_t pm, uint32_t val) {
+    const uint32_t np = popc64(pm);
+    if (np == 0) return;
+    if (S.sp + np > S.cap && !spill_half()) return;  // (np <= 6, S.cap >= 64)
+    if ((pm >> lane) & 1u) S.st[S.sp + popc64(pm & below())] = val;
+    S.sp += np;
+    top = lane_val(val, 63u - static_cast<uint32_t>(__builtin_clzll(pm)));
   };
   auto refill = [&]() {
     // the LDS part is empty: bring back up to half of it from the spill area
@@ -665,37 +677,29 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
       const uint64_t fm = ballot(fbit != 0u || (lane < 6u && !(fused && fv >= root)));
       const uint32_t fl = static_cast<uint32_t>(fm);
       const uint32_t dc = (fl >> 6) & 1u, ig = (fl >> 7) & 1u;
-      const uint32_t d0 = fl & 1u, d1 = (fl >> 1) & 1u, d2 = (fl >> 2) & 1u;
-      const uint32_t e0 = (fl >> 3) & 1u, e1 = (fl >> 4) & 1u, e2 = (fl >> 5) & 1u;
       bool pop = dc != 0;
       SVS_PF_EXAM(1, px1);
       [[maybe_unused]] const uint64_t px2 = SVS_PF_CLK();
       if (!pop) {
-        bool valid = true;
-        for (uint32_t x = 0; x < deg; ++x) {
-          uint32_t t, dt;
-          if (x < 3) {
-            t = x == 0 ? t0 : (x == 1 ? t1 : t2);
-            dt = x == 0 ? d0 : (x == 1 ? d1 : d2);
-          } else {
-            t = uni(in_nbr[off + x]);
-            dt = t < root ? 1u : uni(done_of(t));
-          }
+        // unfinished tails in in-edge order (the first three from the flag
+        // lanes, one store; more from memory), then, unless cur was itself
+        // pushed as an aligned node, its unfinished aligned nodes (flagged)
+        const uint64_t tpm = ~fm & ballot(lane < 3u && lane < deg);
+        push_lanes(tpm, fid);
+        bool valid = tpm == 0;
+        for (uint32_t x = 3; x < deg; ++x) {
+          const uint32_t t = uni(in_nbr[off + x]);
+          const uint32_t dt = t < root ? 1u : uni(done_of(t));
           if (!dt) {
             push(t);
             valid = false;
           }
         }
         if (!ig) {
-          for (uint32_t k = 0; k < alc; ++k) {
-            const uint32_t m = k == 0 ? m0 : (k == 1 ? m1 : m2);
-            const uint32_t dm = k == 0 ? e0 : (k == 1 ? e1 : e2);
-            if (!dm) {
-              push(m);
-              set_bit(S.ign, m);
-              valid = false;
-            }
-          }
+          const uint64_t apm = ~fm & ballot(lane >= 3u && lane < 6u && lane - 3u < alc);
+          push_lanes(apm, fid);
+          if ((apm >> lane) & 1u) set_bit(S.ign, fid);
+          valid = valid && apm == 0;
         }
         if (valid) {
           set_bit(S.done, cur);

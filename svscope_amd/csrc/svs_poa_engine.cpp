@@ -766,11 +766,19 @@ struct PoaScheduler::Impl {
 
   bool dev;      // device-resident graphs (poa_dgraph.hpp)
   bool verify;   // SVS_POA_VERIFY_GRAPH
+  // entries of the sort kernel's DFS stack held in LDS (deeper stacks spill
+  // to the task block); SVS_POA_SORT_STACK (>= 64) lowers it in tests so the
+  // spill path runs
+  uint32_t sort_stack = 1024;
   DevArena* darena = nullptr;
 
   Impl(svs_context* c, const svs_poa_config& k, svs_poa_stats& s)
       : ctx(c), cfg(k), score{k.m, k.n, k.g, k.e, k.q, k.c}, st(s), cap(active_jobs_per_group()),
         budget(c->device_budget / 2), dev(device_graphs(k)), verify(verify_graph()) {
+    if (const char* e = std::getenv("SVS_POA_SORT_STACK")) {
+      const long v = std::atol(e);
+      if (v >= 64 && v <= 1024) sort_stack = static_cast<uint32_t>(v) & ~1u;
+    }
     if (dev) {
       if (!ctx->dgraph_arena) ctx->dgraph_arena.reset(new DevArena());
       darena = ctx->dgraph_arena.get();
@@ -1268,7 +1276,7 @@ struct PoaScheduler::Impl {
       const uint32_t W = (F.V + F.len + 31) / 32;
       lds_words = std::max(lds_words, 2 * W);
     }
-    lds_words += 1024;  // the DFS stack's LDS part (deeper stacks spill)
+    lds_words += sort_stack;  // the DFS stack's LDS part (deeper stacks spill)
     // the final kernel's LDS per job (6 B per node, up to 64 KiB; larger
     // graphs score in global memory), 0 when a fold range has no final fold
     auto final_lds = [&](size_t i0, size_t i1) -> uint32_t {

@@ -104,6 +104,7 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "-0.3", "SVS_POA_PRUNE_MAX_RETRIES": "100"},
     {"SVS_POA_VERIFY_GRAPH": "1"},
     {"SVS_POA_VERIFY_GRAPH": "1", "SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_WPJ": "2"},
+    {"SVS_POA_VERIFY_GRAPH": "1", "SVS_POA_SORT_STACK": "64"},
     {"SVS_POA_HOST_GRAPH": "1"},
     {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_VERIFY_PREP": "1"},
     {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_VERIFY_PREP": "1", "SVS_POA_PRUNE_SLACK": "-0.3"},
@@ -121,7 +122,8 @@ def test_kernel_variants_match_oracle(env):
     tables packed from per-task vectors (SVS_POA_STAGING=vec); with the
     device-resident graphs (the default) checked fold by fold against a host
     replay (SVS_POA_VERIFY_GRAPH=1: rank order, row tables, consensus, MSA),
-    pruned retries included; and with the host graphs (SVS_POA_HOST_GRAPH=1),
+    pruned retries included, also with a 64-entry LDS part of the sort's DFS
+    stack so that deep DFS paths spill to the task block; and with the host graphs (SVS_POA_HOST_GRAPH=1),
     their row tables completed on the device and checked table for table
     against the host's export (SVS_POA_VERIFY_PREP=1), or exported on the host
     only (SVS_POA_DEVICE_PREP=0)."""
