@@ -6,9 +6,11 @@
 // path lengths of w2.  The tables come out identical to the host's; the
 // engine can check that (SVS_POA_VERIFY_PREP=1, svs_poa_engine.cpp).
 //
-// Three waves per job, one per sequential pass (a slot is handed out from a
-// LIFO free list in rank order; the path lengths are forward and backward DPs
-// over the rows), each running its row loop in lockstep with uniform values:
+// Three waves per job, one per pass (a slot is handed out from a LIFO free
+// list in rank order; the path lengths are forward and backward DPs over the
+// rows).  The forward path-length pass (wave 1) is lane-parallel per 64-row
+// chunk (see there); the other two run their row loops in lockstep with
+// uniform values:
 //  * inputs come in chunks of 64 rows, loaded by all lanes with coalesced
 //    loads one chunk ahead, held in VGPRs (lane i = row r0 + i; the chunk's
 //    first 128 in-edges likewise) and read with v_readlane;
