@@ -8,8 +8,8 @@
 //
 // Three waves per job, one per pass (a slot is handed out from a LIFO free
 // list in rank order; the path lengths are forward and backward DPs over the
-// rows).  The forward path-length pass (wave 1) is lane-parallel per 64-row
-// chunk (see there); the other two run their row loops in lockstep with
+// rows).  The two path-length passes (waves 1 and 2) are lane-parallel per
+// 64-row chunk (see there); the slot pass runs its row loop in lockstep with
 // uniform values:
 //  * inputs come in chunks of 64 rows, loaded by all lanes with coalesced
 //    loads one chunk ahead, held in VGPRs (lane i = row r0 + i; the chunk's
@@ -79,7 +79,7 @@ struct Chunk {
 __device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base, const uint32_t* __restrict__ gps,
                                const uint32_t* __restrict__ gpr, const uint32_t* __restrict__ ginfo,
                                uint32_t* __restrict__ rec, uint32_t* __restrict__ pslot, int32_t* __restrict__ c0,
-                               uint32_t* fl_ext) {
+                               uint32_t* fl_ext, uint32_t* w2l) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = uni(threadIdx.x >> 6);
   // this wave's scratch words, one per row (after the job's in-edge slots)
@@ -295,48 +295,138 @@ __device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base
       cur = nxt;
     }
   } else {
-    // fewest / most nodes to a sink (record word w2); every out-edge leads to
-    // a higher rank, so a row is final when the scan reaches it.  Pushes into
-    // rows of the chunk in use go to its register window, pushes into the
-    // chunk before it to a second register window (nwin), pushes further back
-    // to scratch (picked up when that chunk's turn comes).
+    // fewest / most nodes to a sink (record word w2: lo = fewest, 0xFFFF for
+    // none; hi = most), backwards over chunks of 64 rows, lane-parallel
+    // within a chunk (vector issue only).  A row's successors have higher
+    // ranks: those in later chunks pushed into this chunk already (the chunk
+    // just after through the LDS window plo/phi, older ones through scratch);
+    // inside the chunk, the successor just below on the rank chain makes lo
+    // (hi) a min-plus (max-plus) suffix scan along chain segments, and the
+    // other in-chunk successors push through LDS atomics from the previous
+    // round's estimates, until a round changes nothing (lo falls from 0xFFFF
+    // and hi rises from 0, each round a bound on the sequential DP's value,
+    // so the fixed point is that value).  Every step saturates at 0xFFFF as
+    // the sequential min(x + 1, 0xFFFF) does.
     for (uint32_t r = lane; r < V; r += 64) scr[r] = 0xFFFFu;  // lo 0xFFFF (none seen), hi 0
+    uint32_t* clo = w2l;        // this chunk's pushes (lo, atomic min)
+    uint32_t* chi = w2l + 64;   // (hi, atomic max)
+    uint32_t* plo = w2l + 128;  // pushes into the chunk processed next
+    uint32_t* phi = w2l + 192;
+    plo[lane] = 0xFFFFu;
+    phi[lane] = 0u;
     flush_fence();
-    auto merge = [](uint32_t a, uint32_t b) -> uint32_t {
-      return min(a & 0xFFFFu, b & 0xFFFFu) | (max(a >> 16, b >> 16) << 16);
+    const int32_t ilane = static_cast<int32_t>(lane);
+    auto lds_fence = [&]() {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     Chunk cur = load((V - 1) / kChunk * kChunk);
-    uint32_t nwin = 0xFFFFu;  // pushes into the chunk processed next (every chunk before the last is full)
     for (;;) {
       const Chunk nxt = cur.r0 > 0 ? load(cur.r0 - kChunk) : cur;
-      uint32_t win = lane < cur.n ? merge(ld(scr + cur.r0 + lane), nwin) : 0xFFFFu;
-      nwin = 0xFFFFu;
-      uint32_t ow2 = 0;
-      for (uint32_t i = cur.n; i-- > 0;) {
-        const uint32_t v = lane_of(win, i);
-        uint32_t lo = v & 0xFFFFu;
-        const uint32_t hi = v >> 16;
-        if ((lane_of(cur.info, i) >> 8) & 1u) lo = 0;  // a sink
-        const uint32_t l1 = min(lo + 1, 0xFFFFu), h1 = min(hi + 1, 0xFFFFu);
-        const uint32_t a = pstart_of(cur, i), b = pstart_of(cur, i + 1);
-        for (uint32_t x = a; x < b; ++x) {
-          const uint32_t p = (edge(cur, x) & 0x7FFFFFFFu) - 1;
-          if (p >= cur.r0) {
-            const uint32_t pv = lane_of(win, p - cur.r0);
-            win = set_lane(min(pv & 0xFFFFu, l1) | (max(pv >> 16, h1) << 16), p - cur.r0, win);
-          } else if (p + kChunk >= cur.r0) {
-            const uint32_t q = p + kChunk - cur.r0;
-            const uint32_t pv = lane_of(nwin, q);
-            nwin = set_lane(min(pv & 0xFFFFu, l1) | (max(pv >> 16, h1) << 16), q, nwin);
+      const bool in = lane < cur.n;
+      const uint32_t sv = in ? ld(scr + cur.r0 + lane) : 0xFFFFu;
+      const uint32_t blo = in ? min(sv & 0xFFFFu, plo[lane]) : 0xFFFFu;
+      const uint32_t bhi = in ? max(sv >> 16, phi[lane]) : 0u;
+      lds_fence();
+      plo[lane] = 0xFFFFu;
+      phi[lane] = 0u;
+      const bool sink = in && ((cur.info >> 8) & 1u);
+      const uint32_t a = in ? cur.ps : 0u;
+      const uint32_t bn = static_cast<uint32_t>(__shfl(static_cast<int32_t>(cur.ps), min(ilane + 1, 63), 64));
+      const uint32_t b = in ? (lane + 1 < cur.n ? bn : cur.e1) : 0u;
+      const uint32_t deg = b - a;
+      uint32_t maxdeg = deg;
+      for (int o = 32; o >= 1; o >>= 1) maxdeg = max(maxdeg, static_cast<uint32_t>(__shfl_xor(static_cast<int32_t>(maxdeg), o, 64)));
+      maxdeg = uni(maxdeg);
+      // in-edges inside the chunk: the rank chain (from the row just above)
+      // and up to four merge edges (byte = lane, 0xFF none; more: re-read)
+      bool chain_prev = false, ovf = false;
+      uint32_t q = 0xFFFFFFFFu;
+      for (uint32_t x = 0; x < maxdeg; ++x) {
+        const bool has = x < deg;
+        const uint32_t pr = has ? (gpr[a + x] & 0x7FFFFFFFu) - 1u : 0u;
+        if (has && pr >= cur.r0) {
+          if (pr + 1u == cur.r0 + lane) {
+            chain_prev = true;
+          } else if ((q >> 24) != 0xFFu) {
+            ovf = true;
           } else {
-            const uint32_t pv = uni(ld(scr + p));
-            if (lane == 0) scr[p] = min(pv & 0xFFFFu, l1) | (max(pv >> 16, h1) << 16);
-            flush_fence();
+            q = (q << 8) | (pr - cur.r0);
           }
         }
-        ow2 = set_lane(lo | (hi << 16), i, ow2);
       }
-      if (lane < cur.n) rec[4ull * (cur.r0 + lane) + 2] = ow2;
+      const bool any_ovf = ballot(ovf) != 0;
+      // lane i continues its segment into lane i + 1 when row i + 1's chain
+      // in-edge comes from row i
+      const bool cnext = __shfl(chain_prev ? 1 : 0, min(ilane + 1, 63), 64) != 0 && lane + 1 < cur.n;
+      const uint64_t ends = ballot(!cnext);  // lane 63 always ends a segment
+      const int32_t seg1 = static_cast<int32_t>(__builtin_ctzll(ends >> lane)) + ilane;
+      uint32_t lo = 0xFFFFu, hi = 0u;
+      for (;;) {
+        clo[lane] = blo;
+        chi[lane] = bhi;
+        lds_fence();
+        const uint32_t l1 = min(lo + 1u, 0xFFFFu), h1 = min(hi + 1u, 0xFFFFu);
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t off = (q >> (8 * k)) & 0xFFu;
+          if (off != 0xFFu) {
+            __hip_atomic_fetch_min(clo + off, l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_max(chi + off, h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+        if (any_ovf) {
+          for (uint32_t x = 0; x < maxdeg; ++x) {
+            const bool has = ovf && x < deg;
+            const uint32_t pr = has ? (gpr[a + x] & 0x7FFFFFFFu) - 1u : 0u;
+            if (has && pr >= cur.r0 && pr + 1u != cur.r0 + lane) {
+              __hip_atomic_fetch_min(clo + (pr - cur.r0), l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_fetch_max(chi + (pr - cur.r0), h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
+        }
+        lds_fence();
+        const uint32_t pl = sink ? 0u : clo[lane], ph = chi[lane];
+        // suffix scans over [i, seg1(i)]: lo = min_k pl[k] + k - i, hi = max_k ph[k] + k - i
+        int32_t zl = static_cast<int32_t>(pl) + ilane, zh = static_cast<int32_t>(ph) + ilane;
+        for (int d = 1; d < 64; d <<= 1) {
+          const int32_t ol = __shfl(zl, min(ilane + d, 63), 64), oh = __shfl(zh, min(ilane + d, 63), 64);
+          if (ilane + d <= seg1) {
+            zl = min(zl, ol);
+            zh = max(zh, oh);
+          }
+        }
+        const uint32_t nlo = in ? min(static_cast<uint32_t>(zl - ilane), 0xFFFFu) : 0xFFFFu;
+        const uint32_t nhi = in ? min(static_cast<uint32_t>(zh - ilane), 0xFFFFu) : 0u;
+        const bool changed = ballot(nlo != lo || nhi != hi) != 0;
+        lo = nlo;
+        hi = nhi;
+        if (!changed) break;
+      }
+      if (in) rec[4ull * (cur.r0 + lane) + 2] = lo | (hi << 16);
+      // pushes out of the chunk: into the chunk processed next (LDS window),
+      // and further back (scratch, one at a time)
+      const uint32_t l1 = min(lo + 1u, 0xFFFFu), h1 = min(hi + 1u, 0xFFFFu);
+      for (uint32_t x = 0; x < maxdeg; ++x) {
+        const bool has = x < deg;
+        const uint32_t pr = has ? (gpr[a + x] & 0x7FFFFFFFu) - 1u : 0u;
+        const bool prevc = has && pr < cur.r0 && pr + kChunk >= cur.r0;
+        const bool farp = has && pr + kChunk < cur.r0;
+        if (prevc) {
+          __hip_atomic_fetch_min(plo + (pr + kChunk - cur.r0), l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_max(phi + (pr + kChunk - cur.r0), h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        uint64_t fm = ballot(farp);
+        while (fm) {
+          const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(fm));
+          fm &= fm - 1;
+          const uint32_t p = lane_of(pr, l), ql = lane_of(l1, l), qh = lane_of(h1, l);
+          const uint32_t pv = uni(ld(scr + p));
+          if (lane == 0) scr[p] = min(pv & 0xFFFFu, ql) | (max(pv >> 16, qh) << 16);
+          flush_fence();
+        }
+      }
+      lds_fence();
       if (cur.r0 == 0) break;
       cur = nxt;
     }
@@ -345,10 +435,11 @@ __device__ void strip_prep_job(const PoaScore& P, uint32_t V, uint32_t slot_base
 
 __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __restrict__ jobs, PoaScore P) {
   __shared__ uint32_t fl_ext[kStripPrepMaxSlots - 64];
+  __shared__ uint32_t w2l[4 * 64];
   const PoaJob J = jobs[blockIdx.x];
   if (!(J.prep & 1u)) return;
   strip_prep_job(P, J.n_rows, J.prep >> 1, J.pstart, J.pred, J.info, const_cast<uint32_t*>(J.rec),
-                 const_cast<uint32_t*>(J.pslot), const_cast<int32_t*>(J.col0), fl_ext);
+                 const_cast<uint32_t*>(J.pslot), const_cast<int32_t*>(J.col0), fl_ext, w2l);
 }
 
 // The same for the device-resident graphs (poa_dgraph.hpp): the jobs whose
@@ -356,6 +447,7 @@ __global__ __launch_bounds__(192) void poa_strip_prep_kernel(const PoaJob* __res
 __global__ __launch_bounds__(192) void poa_dgraph_prep_kernel(const FoldJob* __restrict__ jobs, PoaScore P) {
   __builtin_amdgcn_s_setprio(SVS_PREP_PRIO_LEVEL);
   __shared__ uint32_t fl_ext[kStripPrepMaxSlots - 64];
+  __shared__ uint32_t w2l[4 * 64];
   const FoldJob J = jobs[blockIdx.x];
   if (!(J.flags & kFoldExport)) return;
   const FoldResult* res = J.result;
@@ -366,7 +458,7 @@ __global__ __launch_bounds__(192) void poa_dgraph_prep_kernel(const FoldJob* __r
   uint8_t* b = J.blk;
   strip_prep_job(P, V, 1u, reinterpret_cast<const uint32_t*>(b + L.pstart), reinterpret_cast<const uint32_t*>(b + L.pred),
                  reinterpret_cast<const uint32_t*>(b + L.info), reinterpret_cast<uint32_t*>(b + L.rec),
-                 reinterpret_cast<uint32_t*>(b + L.pslot), reinterpret_cast<int32_t*>(b + L.col0), fl_ext);
+                 reinterpret_cast<uint32_t*>(b + L.pslot), reinterpret_cast<int32_t*>(b + L.col0), fl_ext, w2l);
 }
 
 }  // namespace
