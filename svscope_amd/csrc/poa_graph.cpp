@@ -352,11 +352,6 @@ void PoaGraph::export_strip_rows(RowTables* t, const int32_t* gaps, const StripD
   // pass 3 (backward): fewest / most nodes on a path to a sink; every out-edge
   // leads to a higher rank, so a row is final when the scan reaches it and
   // pushes its values to its in-edge rows
-#ifdef SVS_NO_DMINMAX
-  // development: no path lengths (dmin = 0, dmax = 0xFFFF: the loosest bound)
-  for (uint32_t r = 0; r < V; ++r) rec[static_cast<size_t>(r) * kRecWords + 2] = 0xFFFFu << 16;
-  return;
-#endif
   dmin.assign(V, 0xFFFFFFFFu);
   dmax.assign(V, 0);
   uint32_t* __restrict__ lo = dmin.data();

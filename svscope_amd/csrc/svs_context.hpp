@@ -112,13 +112,11 @@ struct PoaArena {
   // results, and the finished tasks' consensus + MSA rows
   DeviceBuf d_desc, d_fin;
   PinnedBuf h_desc, h_fin;
-  hipStream_t stream = nullptr;       // kernel stream (shared, or this group's own)
+  hipStream_t stream = nullptr;       // kernel stream (shared by both groups)
   hipStream_t copy_stream = nullptr;  // this group's copies
-  bool own = false;                   // stream is this group's, copies ride on it too
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr, h2d = nullptr;
   hipEvent_t evp = nullptr, evp1 = nullptr;  // around the launch's poa_strip_prep_kernel
   hipEvent_t evf0 = nullptr, evf1 = nullptr;  // around the launch's fold kernels (device-resident graphs)
-  hipStream_t prep_stream = nullptr;          // SVS_POA_PREP_STREAM=1: that kernel's own stream (made on first use)
   // Staging of the next launch's strip tables in h_in: the fold exports each
   // job's tables straight into a block claimed with an atomic bump (st_cur), so
   // packing the launch copies nothing.  A new generation (st_gen) starts when
@@ -126,25 +124,16 @@ struct PoaArena {
   std::atomic<size_t> st_cur{0};
   uint32_t st_gen = 1;
   size_t st_peak = 0;
-  // s == nullptr: the group gets one stream of its own for copies and kernels,
-  // so its kernel can start while the other group's launch is still draining
-  // (its last, longest jobs leave most CUs idle); otherwise kernels of both
-  // groups alternate on the shared stream s and copies go to a copy stream.
+  // Kernels of both groups alternate on the shared stream s; the group's
+  // copies and (device-resident graphs) its fold kernels go to its copy
+  // stream, at the highest stream priority, so that as the other group's DP
+  // workgroups finish, the fold's workgroups are dispatched first and the
+  // group's next launch is ready when the DP stream gets to it.
   PoaArena(int device, hipStream_t s) : stream(s) {
     SVS_HIP(hipSetDevice(device));
-    if (!s) {
-      own = true;
-      SVS_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-      copy_stream = stream;
-    } else {
-      // the group's copies and (device-resident graphs) its fold kernels: at
-      // the highest stream priority, so that as the other group's DP
-      // workgroups finish, the fold's workgroups are dispatched first and the
-      // group's next launch is ready when the DP stream gets to it
-      int least = 0, greatest = 0;
-      SVS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      SVS_HIP(hipStreamCreateWithPriority(&copy_stream, hipStreamNonBlocking, greatest));
-    }
+    int least = 0, greatest = 0;
+    SVS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    SVS_HIP(hipStreamCreateWithPriority(&copy_stream, hipStreamNonBlocking, greatest));
     SVS_HIP(hipEventCreate(&ev0));
     SVS_HIP(hipEventCreate(&ev1));
     SVS_HIP(hipEventCreate(&evp));
@@ -165,13 +154,9 @@ struct PoaArena {
     if (evp1) (void)hipEventDestroy(evp1);
     if (evf0) (void)hipEventDestroy(evf0);
     if (evf1) (void)hipEventDestroy(evf1);
-    if (prep_stream) {
-      (void)hipStreamSynchronize(prep_stream);
-      (void)hipStreamDestroy(prep_stream);
-    }
     if (done) (void)hipEventDestroy(done);
     if (h2d) (void)hipEventDestroy(h2d);
-    if (copy_stream) (void)hipStreamDestroy(copy_stream);  // == stream when own
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
   }
   PoaArena(const PoaArena&) = delete;
   PoaArena& operator=(const PoaArena&) = delete;

@@ -57,6 +57,7 @@ struct PoaLaunch {
   uint32_t lds_slots;    // pool slots per wave held in LDS (max n_slots of the launch)
   bool prune;            // some job has a pruning bound: the pruning kernel variant
   bool wide;             // some row has more than 31 in-edges: 32-bit codes (TbFmt, poa_wave.hpp)
+  bool dual;             // LDS pools: strips swept in pairs (poa_strip.hip, 2 x kStripSlotBytes per slot)
 };
 
 // One block copy of launch_scatter_copy (bytes a multiple of 64, both ends

@@ -180,21 +180,11 @@ struct KernelEnv {
   bool global_pool = strip_pool_forced_global();
 };
 
-// Strip tables go straight into the group's pinned staging buffer
-// (PoaArena::st_*) unless SVS_POA_STAGING=vec keeps them in each task's
-// vectors, copied into the buffer when the launch is packed.
-bool direct_staging() {
-  const char* e = std::getenv("SVS_POA_STAGING");
-  return !(e && std::string(e) == "vec");
-}
-
-// The device completes the strip tables (poa_prep.hip) of graphs it can hold
-// unless SVS_POA_DEVICE_PREP=0; SVS_POA_VERIFY_PREP=1 checks them against the
-// host's export after every launch (tests).
-bool device_prep() {
-  const char* e = std::getenv("SVS_POA_DEVICE_PREP");
-  return !(e && std::string(e) == "0");
-}
+// Host graphs: strip tables go straight into the group's pinned staging
+// buffer (PoaArena::st_*); a table that does not fit stays in the task's
+// vectors and is copied in when the launch is packed.  The device completes
+// the tables (poa_prep.hip) of graphs it can hold; SVS_POA_VERIFY_PREP=1
+// checks them against the host's export after every launch (tests).
 bool verify_prep() {
   const char* e = std::getenv("SVS_POA_VERIFY_PREP");
   return e && std::string(e) == "1";
@@ -213,7 +203,7 @@ bool export_direct(PoaTask& t, const int32_t* gaps, PoaArena& A) {
   const std::string& s = t.seqs[t.next];
   const uint32_t ls = strip_ls(static_cast<uint32_t>(s.size()));
   const uint32_t V = t.graph.num_nodes(), E = t.graph.num_edges();
-  if (device_prep() && V <= kStripPrepMaxRows && gaps[1] <= 0 && gaps[3] <= 0) {
+  if (V <= kStripPrepMaxRows && gaps[1] <= 0 && gaps[3] <= 0) {
     // host pass 1 only; the device derives the rest (poa_prep.hip)
     const StripBlock b = strip_block_lite(V, E, ls);
     const size_t off = A.st_cur.fetch_add(b.bytes, std::memory_order_relaxed);
@@ -270,11 +260,11 @@ void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks);
 // Waves per job of a strip launch: enough strip-pipeline waves to fill the
 // CUs, only for reads wide enough to give every wave several strips, and only
 // as many as the per-wave LDS pools of one workgroup fit; SVS_POA_WPJ overrides.
-int choose_wpj(size_t nj, uint32_t max_slots, uint32_t min_strips, bool lds_pool) {
+int choose_wpj(size_t nj, uint32_t max_slots, uint32_t min_strips, bool lds_pool, bool dual) {
   int wpj = 1;
   const char* we = std::getenv("SVS_POA_WPJ");
   const int wenv = we ? std::atoi(we) : 0;
-  if ((wenv == 1 || wenv == 2 || wenv == 4 || wenv == 8) || (wenv == 16 && lds_pool)) {
+  if ((wenv == 1 || wenv == 2 || wenv == 4 || wenv == 8) || (wenv == 16 && lds_pool && !dual)) {
     wpj = wenv;
   } else {
     // ~6 waves per SIMD (1024 SIMDs); each wave keeps >= 6 strips.  Measured
@@ -284,9 +274,20 @@ int choose_wpj(size_t nj, uint32_t max_slots, uint32_t min_strips, bool lds_pool
     // the small launches at the end of a batch: 16 waves per job (>= 2 strips
     // each), or the few remaining jobs leave most SIMDs idle
     if (lds_pool && wpj == 8 && nj < 512 && min_strips >= 32u) wpj = 16;
+    // a dual wave sweeps two strips at a time: half the waves for the same
+    // strip pipeline
+    if (dual && wpj > 1) wpj /= 2;
   }
-  while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * kStripSlotBytes > kStripLdsBytes) wpj /= 2;
+  const uint64_t slot_bytes = static_cast<uint64_t>(kStripSlotBytes) * (dual ? 2 : 1);
+  while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * slot_bytes > kStripLdsBytes) wpj /= 2;
   return wpj;
+}
+
+// Strips swept in pairs (poa_strip.hip DUAL) for launches whose pools sit in
+// LDS, unless SVS_POA_DUAL=0.
+bool dual_sweeps() {
+  const char* e = std::getenv("SVS_POA_DUAL");
+  return !(e && std::string(e) == "0");
 }
 
 void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, const PoaScore& score,
@@ -317,7 +318,8 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     const uint32_t ls = job_ls(tasks[la.ids[k]].seqs[tasks[la.ids[k]].next].size());
     min_strips = std::min(min_strips, ls / 64);
   }
-  const int wpj = choose_wpj(nj, max_slots, min_strips, lds_pool);
+  const bool dual = lds_pool && dual_sweeps();
+  const int wpj = choose_wpj(nj, max_slots, min_strips, lds_pool, dual);
   if (std::getenv("SVS_POA_DEBUG"))
     std::fprintf(stderr, "[svs] strip launch: %zu jobs, wpj %d, slots %u\n", nj, wpj, max_slots);
   const PruneEnv penv;
@@ -459,20 +461,12 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   SVS_HIP(hipEventRecord(A.h2d, A.copy_stream));
   SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
   if (n_prep > 0) {
-    // on the kernel stream, or (SVS_POA_PREP_STREAM=1) on a stream of its own
-    // so that it can run beside the other group's DP kernel
-    static const bool own = [] {
-      const char* e = std::getenv("SVS_POA_PREP_STREAM");
-      return e && std::string(e) == "1";
-    }();
-    if (own && !A.prep_stream) SVS_HIP(hipStreamCreateWithFlags(&A.prep_stream, hipStreamNonBlocking));
-    hipStream_t ps = own ? A.prep_stream : A.stream;
-    if (own) SVS_HIP(hipStreamWaitEvent(ps, A.h2d, 0));
+    // on the kernel stream (a stream of its own measured no faster, r02_v28)
+    hipStream_t ps = A.stream;
     SVS_HIP(hipEventRecord(A.evp, ps));
     SVS_HIP(launch_poa_strip_prep(reinterpret_cast<const PoaJob*>(dg + s_jobs), static_cast<int>(nj), score,
                                   prep_rows, ps));
     SVS_HIP(hipEventRecord(A.evp1, ps));
-    if (own) SVS_HIP(hipStreamWaitEvent(A.stream, A.evp1, 0));
     if (verify_prep()) {
       // before the DP kernel reads them: a wrong table fails here, not there
       SVS_HIP(hipStreamSynchronize(ps));
@@ -491,6 +485,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.lds_slots = lds_pool ? max_slots : 0;
   pl.prune = any_prune;
   pl.wide = la.code_bytes == 4;
+  pl.dual = dual;
   pl.waves_per_job = wpj;
   la.wpj = wpj;
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
@@ -572,13 +567,10 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   SVS_HIP(hipEventSynchronize(A.done));  // the other group's launch may still be queued behind it
   st.gpu_wait_ms += ms_since(tw0);
   // the launch's staging copy is consumed: a new generation for the next one
-  PoaArena* stage = nullptr;
-  if (direct_staging()) {
-    A.st_gen += 1;
-    A.st_cur.store(0, std::memory_order_relaxed);
-    A.h_in.ensure(A.st_peak + A.st_peak / 4);
-    stage = &A;
-  }
+  A.st_gen += 1;
+  A.st_cur.store(0, std::memory_order_relaxed);
+  A.h_in.ensure(A.st_peak + A.st_peak / 4);
+  PoaArena* stage = &A;
   float ms = 0.f;
   SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
   st.kernel_ms += ms;
@@ -779,20 +771,20 @@ struct PoaScheduler::Impl {
       const long v = std::atol(e);
       if (v >= 64 && v <= 1024) sort_stack = static_cast<uint32_t>(v) & ~1u;
     }
+    if (const char* e = std::getenv("SVS_POA_TEST_SORT_LDS_WORDS")) {
+      const long v = std::atol(e);
+      if (v > 0 && static_cast<uint64_t>(v) < kSortLdsWordsMax) sort_lds_max = static_cast<uint64_t>(v);
+    }
     if (dev) {
       if (!ctx->dgraph_arena) ctx->dgraph_arena.reset(new DevArena());
       darena = ctx->dgraph_arena.get();
     }
-    // Both groups' kernels alternate on the context's one stream.
-    // SVS_POA_STREAMS=2 gives each group a stream of its own so the next
-    // launch can overlap the other's tail: measured no faster (196.9 vs 202.0
-    // windows/s, profiles/r01_v40), so it stays a development option.
-    const char* ns = std::getenv("SVS_POA_STREAMS");
-    const bool shared = !(ns && std::atoi(ns) == 2);
-    while (ctx->poa_arenas.size() < 2)
-      ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, shared ? ctx->stream : nullptr));
+    // Both groups' DP kernels alternate on the context's one stream (a stream
+    // per group measured no faster: 196.9 vs 202.0 windows/s, r01_v40; 237.4
+    // vs 240.2 with device graphs, r03_s3c).
+    while (ctx->poa_arenas.size() < 2) ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
     for (int g = 0; g < 2; ++g) groups[g].arena = ctx->poa_arenas[g].get();
-    if (shared) split_cus();
+    split_cus();
   }
 
   // SVS_POA_FOLD_CUS=n (device-resident graphs, shared DP stream): n CUs,
@@ -911,6 +903,16 @@ struct PoaScheduler::Impl {
     release_dev(t);
     g.completed.push_back(id);
   }
+  // LDS words of the sort kernel for a graph of n nodes: the done and ignore
+  // bit planes, then the DFS stack's LDS part (poa_fold_sort_kernel).  A
+  // launch takes the maximum over its folds, so every fold must fit the
+  // 160 KiB a workgroup may declare; a graph past it fails alone
+  // (advance_dev) instead of failing the launch.
+  // (SVS_POA_TEST_SORT_LDS_WORDS lowers the limit in tests)
+  static constexpr uint64_t kSortLdsWordsMax = 160 * 1024 / 4 - 64;
+  uint64_t sort_lds_max = kSortLdsWordsMax;
+  uint64_t sort_lds_words(uint64_t n) const { return 2 * ((n + 31) / 32) + sort_stack; }
+
   // the row limit of the device table planner (SVS_POA_TEST_MAX_ROWS lowers it
   // in tests, to fail one window of a batch on purpose)
   static uint32_t planner_max_rows() {
@@ -979,6 +981,8 @@ struct PoaScheduler::Impl {
           why = "a graph node has more than 4094 in-edges (traceback code limit)";
         else if (len > 0 && rows * strip_ls(static_cast<uint32_t>(len)) > 0x7FFFFFFFull)
           why = "an alignment's traceback matrix exceeds 2^31 cells";
+        else if (sort_lds_words(rows + len) > sort_lds_max)
+          why = "a POA graph too large for the sort kernel's LDS node flags (about 630,000 nodes)";
         if (why) fail_task(g, id, why);
         else keep.push_back(id);
       }
@@ -1094,7 +1098,8 @@ struct PoaScheduler::Impl {
       min_strips = std::min(min_strips, strip_ls(static_cast<uint32_t>(t.seqs[t.next].size())) / 64);
     }
     const bool lds_pool = max_slots <= kStripMaxLdsSlots && !strip_pool_forced_global();
-    const int wpj = nj ? choose_wpj(nj, max_slots, min_strips, lds_pool) : 1;
+    const bool dual = lds_pool && dual_sweeps();
+    const int wpj = nj ? choose_wpj(nj, max_slots, min_strips, lds_pool, dual) : 1;
     const PruneEnv penv;
     for (size_t k = 0; k < nj; ++k) {
       const PoaTask& t = tasks[dp[k]];
@@ -1272,11 +1277,10 @@ struct PoaScheduler::Impl {
                                  static_cast<uint32_t>(m[4]), static_cast<uint32_t>(m[5]), static_cast<uint32_t>(m[6]),
                                  static_cast<uint32_t>(m[7]), static_cast<uint32_t>(m[8]), side));
     uint32_t lds_words = 0;
-    for (const FoldJob& F : D.folds) {
-      const uint32_t W = (F.V + F.len + 31) / 32;
-      lds_words = std::max(lds_words, 2 * W);
-    }
-    lds_words += sort_stack;  // the DFS stack's LDS part (deeper stacks spill)
+    for (const FoldJob& F : D.folds) lds_words = std::max(lds_words, static_cast<uint32_t>(sort_lds_words(F.V + F.len)));
+    // (the DFS stack's LDS part is in it; deeper stacks spill)
+    if (lds_words > sort_lds_max)
+      throw SvsError(SVS_E_INTERNAL, "sort kernel LDS over the workgroup limit despite the per-task check");
     // the final kernel's LDS per job (6 B per node, up to 64 KiB; larger
     // graphs score in global memory), 0 when a fold range has no final fold
     auto final_lds = [&](size_t i0, size_t i1) -> uint32_t {
@@ -1325,6 +1329,7 @@ struct PoaScheduler::Impl {
       pl.lds_slots = lds_pool ? max_slots : 0;
       pl.prune = any_prune;
       pl.wide = wide;
+      pl.dual = dual;
       pl.waves_per_job = wpj;
       SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
       SVS_HIP(hipEventRecord(A.ev0, A.stream));
@@ -1582,7 +1587,7 @@ struct PoaScheduler::Impl {
       if (g.active.empty()) return;
       auto th0 = Clock::now();
       needs.assign(g.active.size(), 0);
-      PoaArena* stage = direct_staging() ? g.arena : nullptr;
+      PoaArena* stage = g.arena;
       // sequences landing on an empty graph become a fresh chain (no DP)
       ctx->pool->parallel_for(g.active.size(), [&](size_t i) {
         PoaTask& t = tasks[g.active[i]];

@@ -19,7 +19,8 @@ Differences, all deliberate:
   * multi-GPU: one process per GPU (torch.distributed, backend "nccl" = RCCL);
     windows are dealt to ranks longest-first by estimated cost N*L^2, each rank
     runs its shard on its own GPU, and rank 0 receives every rank's packed
-    records with one RCCL all_gather over xGMI.  No other collective exists:
+    records with one RCCL gather over xGMI (after an 8-byte all_gather of
+    the byte counts).  No other collective exists:
     windows are independent (per-window RNG reseed).
 """
 import argparse
@@ -126,19 +127,43 @@ def run_windows(rows, batch_size=512, context=None):
     return out
 
 
-def write_journal(path, mode, rows, batch_size):
+def write_journal(path, mode, rows, batch_size, failed=None):
     """Runs the windows and appends each batch's records to ``path`` as soon as
     the batch completes, flushed (the reference writes and flushes every
     record as it arrives, SVscope.py:227-233, which is what makes --Continue
-    resume after a crash).  Returns the record lines."""
+    resume after a crash).  Returns the record lines.  Windows past an engine
+    limit are left out of the journal; with ``failed`` (a dict) given, their
+    TDRecord keys and reasons go there and the call returns normally, so that
+    the caller still gathers and sorts every other record."""
+    from .decision_maker import WindowFailed
     lines = []
     with open(path, mode) as fh:
-        for recs in iter_batches(rows, batch_size):
-            chunk = [record_line(x) for x in recs if x is not None]
-            fh.write("".join(line + "\n" for line in chunk))
-            fh.flush()
-            lines.extend(chunk)
+        try:
+            for recs in iter_batches(rows, batch_size):
+                chunk = [record_line(x) for x in recs if x is not None]
+                fh.write("".join(line + "\n" for line in chunk))
+                fh.flush()
+                lines.extend(chunk)
+        except WindowFailed as e:
+            if failed is None:
+                raise
+            failed.update({window_key(rows[i]): why for i, why in e.failed.items()})
     return lines
+
+
+def window_key(row):
+    """chrom, start, end of a bundle row's TDRecord (the --Continue key)."""
+    return "\t".join(row[4].strip().split("\t")[0:3])
+
+
+def _report_failed(failed, rank):
+    """After the output is complete: every window past an engine limit, named
+    by its TDRecord key, in one WindowFailed (each rank its own)."""
+    from .decision_maker import WindowFailed
+    if failed:
+        for key, why in sorted(failed.items()):
+            log.error("rank %d: window %s not written: %s", rank, key.replace("\t", ":"), why)
+        raise WindowFailed(failed, None)
 
 
 def part_path(path, rank):
@@ -163,7 +188,10 @@ def merge_parts(path):
 
 
 def gather_lines(lines, device):
-    """RCCL all_gather of every rank's packed record lines (rank 0 keeps them)."""
+    """Every rank's packed record lines to rank 0: the byte counts with one
+    all_gather (8 B per rank: every rank pads its buffer to the largest), then
+    the padded buffers with one RCCL gather to rank 0.  Rank 0 returns all
+    lines, the other ranks []."""
     import torch
     import torch.distributed as dist
     payload = "\n".join(lines).encode()
@@ -174,13 +202,15 @@ def gather_lines(lines, device):
     buf = torch.zeros(max(cap, 1), dtype=torch.uint8, device=device)
     if payload:
         buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
-    bufs = [torch.zeros_like(buf) for _ in sizes]
-    dist.all_gather(bufs, buf)
+    root = dist.get_rank() == 0
+    bufs = [torch.zeros_like(buf) for _ in sizes] if root else None
+    dist.gather(buf, bufs, dst=0)
     out = []
-    for s, b in zip(sizes, bufs):
-        k = int(s.item())
-        if k:
-            out.extend(bytes(b[:k].cpu().numpy()).decode().split("\n"))
+    if root:
+        for s, b in zip(sizes, bufs):
+            k = int(s.item())
+            if k:
+                out.extend(bytes(b[:k].cpu().numpy()).decode().split("\n"))
     return out
 
 
@@ -201,16 +231,21 @@ def localGraph_npz(args):
     if cont and os.path.exists(path):
         with open(path) as fh:
             finished = {"\t".join(x.strip().split("\t")[0:3]) for x in fh if x.strip()}
-    rows = [r for r in rows if "\t".join(r[4].strip().split("\t")[0:3]) not in finished]
+    rows = [r for r in rows if window_key(r) not in finished]
+    # a window past an engine limit fails alone: every other record is still
+    # written, gathered and sorted on every rank, then the failures are raised
+    failed = {}
     if dist is not None:
         # each rank journals its records as batches complete; rank 0 receives
-        # every rank's records with one RCCL all_gather and writes the output
+        # every rank's records with one RCCL gather and writes the output
         owner = shard_lpt(rows, world)
         mine = [r for r, o in zip(rows, owner) if o == rank]
-        lines = write_journal(part_path(path, rank), "w", mine, args.batch)
+        lines = write_journal(part_path(path, rank), "w", mine, args.batch, failed)
     else:
-        lines = write_journal(path, "a" if finished else "w", rows, args.batch)
-    return _finish(path, lines, rank, world, dist, device, finished, t0, "Local Graph")
+        lines = write_journal(path, "a" if finished else "w", rows, args.batch, failed)
+    out = _finish(path, lines, rank, world, dist, device, finished, t0, "Local Graph")
+    _report_failed(failed, rank)
+    return out
 
 
 def _dist_setup():
@@ -272,6 +307,7 @@ def localGraph(args, readers=None):
     import multiprocessing as mp
     import sys
     from .data_maker import DataMaker, DataMaker2
+    from .decision_maker import WindowFailed
     from .som_td_detector import TDscope_batch
     t0 = time.time()
     tumor, normal = args.Tumorbam.split(","), args.Normalbam.split(",")
@@ -313,14 +349,19 @@ def localGraph(args, readers=None):
     chunks = [mine[k:k + B] for k in range(0, len(mine), B)]
     out_path = part_path(path, rank) if dist is not None else path
     lines = []
+    failed = {}  # windows past an engine limit: reported after the output is complete
     try:
         with open(out_path, "w" if dist is not None else ("a" if finished else "w")) as fh:
             nxt = pool.map_async(dm, chunks[0]) if (pool and chunks) else None
             for k, chunk in enumerate(chunks):
                 bundles = nxt.get() if nxt is not None else [dm(r) for r in chunk]
                 nxt = pool.map_async(dm, chunks[k + 1]) if (pool and k + 1 < len(chunks)) else None
-                recs = TDscope_batch(chunk, dm, dm2, map_fn=map_fn, bundles=bundles)
-                chunk_lines = [record_line(x) for x in recs]
+                try:
+                    recs = TDscope_batch(chunk, dm, dm2, map_fn=map_fn, bundles=bundles)
+                except WindowFailed as e:
+                    recs = e.records
+                    failed.update({"\t".join(chunk[i].split("\t")[0:3]): why for i, why in e.failed.items()})
+                chunk_lines = [record_line(x) for x in recs if x is not None]
                 fh.write("".join(line + "\n" for line in chunk_lines))
                 fh.flush()
                 lines.extend(chunk_lines)
@@ -328,7 +369,9 @@ def localGraph(args, readers=None):
         if pool:
             pool.close()
             pool.join()
-    return _finish(path, lines, rank, world, dist, device, finished, t0, "Local Graph")
+    out = _finish(path, lines, rank, world, dist, device, finished, t0, "Local Graph")
+    _report_failed(failed, rank)
+    return out
 
 
 def main(argv=None):

@@ -16,7 +16,7 @@ import time
 
 import numpy as np
 
-from .decision_maker import Decision, DecisionBatch
+from .decision_maker import Decision, DecisionBatch, WindowFailed
 
 log = logging.getLogger("svscope_amd")
 
@@ -59,30 +59,50 @@ def TDscope_batch(TDRecords, DataMaker, DataMaker2, map_fn=map, context=None, Tl
     one DecisionBatch for all of them, then for the DUP windows without an
     EMOutput one DataMaker2 each, one DecisionBatch for their 5' corners, one
     for the 3' corners of those still without, and the flag rewrite of
-    :55-58.  ``bundles``, if given, is the precomputed DataMaker output."""
+    :55-58.  ``bundles``, if given, is the precomputed DataMaker output.
+
+    A window past an engine limit in any of its Decision rounds fails alone:
+    the other windows' records are completed, then one WindowFailed carries
+    them (None for the failed windows) and the failed indices."""
     data = list(bundles) if bundles is not None else list(map_fn(DataMaker, TDRecords))
     kw = dict(Tlabel=Tlabel, readcutoff=readcutoff, hcutoff=hcutoff, scutoff=scutoff, context=context)
+    failed = {}
+
+    def batch(windows, owners):
+        # one Decision round; a failed window's owner (an index into data) fails
+        try:
+            return DecisionBatch(windows, **kw)
+        except WindowFailed as e:
+            for j, why in e.failed.items():
+                failed.setdefault(owners[j], why)
+            return e.records
+
     # the window record's column 4 (IndexError on a 3-column record, as :39)
     sv_types = [d[4].strip().split("\t")[3].split(",")[0] for d in data]
-    records = DecisionBatch([(d[4], d[0], d[1], d[2], d[3], d[5]) for d in data], **kw)
-    dup = [i for i, rec in enumerate(records) if not _emoutput(rec) and sv_types[i] == "DUP"]
-    if not dup:
-        return records
-    rescans = list(map_fn(DataMaker2, [data[i][4] for i in dup]))
-    rec5 = DecisionBatch([tuple(r[0][k] for k in (4, 0, 1, 2, 3, 5)) for r in rescans], **kw)
-    left = [j for j in range(len(dup)) if not _emoutput(rec5[j])]
-    rec3 = DecisionBatch([tuple(rescans[j][1][k] for k in (4, 0, 1, 2, 3, 5)) for j in left], **kw)
-    rec3 = dict(zip(left, rec3))
-    for j, i in enumerate(dup):
-        c5, c3 = rescans[j]
-        if _emoutput(rec5[j]):
-            records[i] = rec5[j]
-        elif _emoutput(rec3[j]):
-            records[i] = rec3[j]
-        elif len([x for x in np.setdiff1d(c5[1], data[i][1]) if re.search("_tumor", x)]) >= 3:
-            records[i][-1] = c5[5]
-        elif len([x for x in np.setdiff1d(c3[1], data[i][1]) if re.search("_tumor", x)]) >= 3:
-            records[i][-1] = c3[5]
+    records = batch([(d[4], d[0], d[1], d[2], d[3], d[5]) for d in data], list(range(len(data))))
+    dup = [i for i, rec in enumerate(records) if rec is not None and not _emoutput(rec) and sv_types[i] == "DUP"]
+    if dup:
+        rescans = list(map_fn(DataMaker2, [data[i][4] for i in dup]))
+        rec5 = batch([tuple(r[0][k] for k in (4, 0, 1, 2, 3, 5)) for r in rescans], dup)
+        left = [j for j in range(len(dup)) if rec5[j] is not None and not _emoutput(rec5[j])]
+        rec3 = batch([tuple(rescans[j][1][k] for k in (4, 0, 1, 2, 3, 5)) for j in left], [dup[j] for j in left])
+        rec3 = dict(zip(left, rec3))
+        for j, i in enumerate(dup):
+            if i in failed:
+                continue
+            c5, c3 = rescans[j]
+            if _emoutput(rec5[j]):
+                records[i] = rec5[j]
+            elif _emoutput(rec3[j]):
+                records[i] = rec3[j]
+            elif len([x for x in np.setdiff1d(c5[1], data[i][1]) if re.search("_tumor", x)]) >= 3:
+                records[i][-1] = c5[5]
+            elif len([x for x in np.setdiff1d(c3[1], data[i][1]) if re.search("_tumor", x)]) >= 3:
+                records[i][-1] = c3[5]
+    if failed:
+        for i in failed:
+            records[i] = None
+        raise WindowFailed(failed, records)
     return records
 
 

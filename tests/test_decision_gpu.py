@@ -258,19 +258,23 @@ def test_big_windows_mixed_into_config3_batch_match_oracle():
     assert not bad, f"windows {bad} differ from the oracle"
 
 
-def test_window_past_an_engine_limit_fails_alone():
+@pytest.mark.parametrize("env,why", [({"SVS_POA_TEST_MAX_ROWS": "4000"}, "planner"),
+                                     ({"SVS_POA_TEST_SORT_LDS_WORDS": "1300"}, "sort kernel")])
+def test_window_past_an_engine_limit_fails_alone(env, why):
     """a window that goes past an engine limit fails alone
     (status SVS_DEC_FAILED, decision_maker.WindowFailed naming it) while the
     other windows of its batch and of the session get the oracle's records.
-    The device planner's row limit is lowered for the test
-    (SVS_POA_TEST_MAX_ROWS) so that one 64-read x 3 kb window crosses it."""
+    The device planner's row limit (SVS_POA_TEST_MAX_ROWS), or the LDS the
+    sort kernel's node flags may take (SVS_POA_TEST_SORT_LDS_WORDS, ADVICE
+    r03: a graph past it used to fail the whole launch), is lowered for the
+    test so that one 64-read x 3 kb window crosses it."""
     from svscope_amd import synth
     from svscope_amd.decision_maker import DecisionSession, WindowFailed
     from svscope_amd.local_graph import _window, record_line
     small = [synth.make_window(w, 8, 600) for w in range(40, 46)]
     big = synth.make_window(50, 64, 3000)
     rows = small[:3] + [big] + small[3:]
-    os.environ["SVS_POA_TEST_MAX_ROWS"] = "4000"
+    os.environ.update(env)
     try:
         with DecisionSession() as s:
             t1 = s.submit([_window(r) for r in rows])
@@ -279,9 +283,10 @@ def test_window_past_an_engine_limit_fails_alone():
                 s.wait(t1)
             again = s.wait(t2)
     finally:
-        os.environ.pop("SVS_POA_TEST_MAX_ROWS", None)
+        for k in env:
+            os.environ.pop(k, None)
     e = ei.value
-    assert list(e.failed) == [3] and "planner" in e.failed[3], e.failed
+    assert list(e.failed) == [3] and why in e.failed[3], e.failed
     assert e.records[3] is None
     exp = [_oracle_record(r) for r in small]
     got = [record_line(x) for k, x in enumerate(e.records) if k != 3]

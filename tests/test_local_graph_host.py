@@ -1,0 +1,156 @@
+"""Per-window failure isolation of the batched callers: a window
+past an engine limit (decision_maker.WindowFailed) must not stop the other
+windows' records from being written, gathered and sorted, on one rank or
+several (gloo, world_size 2), in localGraph_npz and in the BAM-reading
+localGraph's TDscope_batch.  The per-window decision is the CPU oracle (test
+infrastructure) with one window forced to fail."""
+import argparse
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from svscope_amd import local_graph, synth, som_td_detector
+from svscope_amd.decision_maker import WindowFailed
+
+
+def _oracle_records(rows):
+    from oracle import decision_oracle
+    return [decision_oracle.tdscope_npz(r[4], r[0], np.asarray(r[1]), r[2], r[3]) for r in rows]
+
+
+def _failing_batches(bad_keys):
+    """iter_batches stand-in: oracle records, None for windows whose TDRecord
+    key is in bad_keys, and a WindowFailed naming them after the last batch
+    (as iter_batches does)."""
+    def gen(rows, batch_size=512, context=None, depth=4):
+        failed = {}
+        for k in range(0, len(rows), batch_size):
+            part = rows[k:k + batch_size]
+            recs = _oracle_records(part)
+            for i, r in enumerate(part):
+                if local_graph.window_key(r) in bad_keys:
+                    recs[i] = None
+                    failed[k + i] = "test: past an engine limit"
+            yield recs
+        if failed:
+            raise WindowFailed(failed, None)
+    return gen
+
+
+def _write_bundles(d, rows):
+    for k in range(0, len(rows), 5):
+        arr = np.empty(len(rows[k:k + 5]), dtype=object)
+        for i, r in enumerate(rows[k:k + 5]):
+            arr[i] = r
+        np.savez(os.path.join(d, f"part{k // 5}.npz"), DatSet=arr)
+
+
+def test_npz_failed_window_rest_written_and_sorted(tmp_path, monkeypatch):
+    rows = [synth.make_window(w, 6, 160) for w in range(11)]
+    bad = local_graph.window_key(rows[4])
+    savedir = tmp_path / "b"
+    savedir.mkdir()
+    _write_bundles(str(savedir), rows)
+    monkeypatch.setattr(local_graph, "iter_batches", _failing_batches({bad}))
+    args = argparse.Namespace(TSampleID="T1", NSampleID="N1", savedir=str(savedir), Continue=False, batch=3)
+    with pytest.raises(WindowFailed) as ei:
+        local_graph.localGraph_npz(args)
+    assert list(ei.value.failed) == [bad]
+    good = [r for r in rows if local_graph.window_key(r) != bad]
+    exp = local_graph.sort_lines([local_graph.record_line(x) for x in _oracle_records(good)])
+    got = [x.rstrip("\n") for x in open(savedir / "T1.vs.N1.TandemRepeat.Raw.bed")]
+    assert got == exp
+    # --Continue: the written windows are skipped, the failed one is retried
+    # (and fails again), the output keeps every other record, sorted
+    with pytest.raises(WindowFailed):
+        local_graph.localGraph_npz(argparse.Namespace(**{**vars(args), "Continue": True}))
+    assert [x.rstrip("\n") for x in open(savedir / "T1.vs.N1.TandemRepeat.Raw.bed")] == exp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, savedir, outdir, bad):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    local_graph.iter_batches = _failing_batches({bad})
+    args = argparse.Namespace(TSampleID="T1", NSampleID="N1", savedir=savedir, Continue=False, batch=2)
+    raised = []
+    try:
+        local_graph.localGraph_npz(args)
+    except WindowFailed as e:
+        raised = list(e.failed)
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+    with open(os.path.join(outdir, f"failed{rank}.txt"), "w") as fh:
+        fh.write("\n".join(raised))
+
+
+def test_npz_failed_window_world2_gloo_no_stall(tmp_path):
+    """One rank's window fails: both ranks still reach the gather, rank 0
+    writes every other record sorted, and only the owning rank reports it."""
+    rows = [synth.make_window(w, 6, 160) for w in range(10)]
+    bad = local_graph.window_key(rows[3])
+    savedir = tmp_path / "b"
+    savedir.mkdir()
+    _write_bundles(str(savedir), rows)
+    mp.start_processes(_rank_main, args=(2, _free_port(), str(savedir), str(tmp_path), bad), nprocs=2, join=True,
+                       start_method="fork")
+    good = [r for r in rows if local_graph.window_key(r) != bad]
+    exp = local_graph.sort_lines([local_graph.record_line(x) for x in _oracle_records(good)])
+    assert [x.rstrip("\n") for x in open(savedir / "T1.vs.N1.TandemRepeat.Raw.bed")] == exp
+    reported = [open(tmp_path / f"failed{r}.txt").read().split("\n") for r in range(2)]
+    assert sorted(x for rep in reported for x in rep if x) == [bad]
+
+
+def test_tdscope_batch_isolates_failures_in_every_round(monkeypatch):
+    """TDscope_batch: a window failing in the first Decision round, and a DUP
+    window failing in its 5' re-scan round, come back as None in the
+    WindowFailed's records; the other windows' records (including a DUP
+    window rescued by its 3' corner) are complete."""
+    def rec(td, flag="NormalOutput"):
+        return [td, "", "", "", "", 0, "", "", 0, flag]
+
+    def fake_batch(windows, **kw):
+        out, failed = [], {}
+        for j, w in enumerate(windows):
+            td = w[0]
+            if "fail1" in td and not w[5].startswith("corner"):
+                failed[j] = "round 1"
+                out.append(None)
+            elif "fail5" in td and w[5] == "corner5":
+                failed[j] = "round 5'"
+                out.append(None)
+            elif "rescue3" in td and w[5] == "corner3":
+                out.append(rec(td, "corner3|EMOutput"))
+            else:
+                out.append(rec(td, w[5]))
+        if failed:
+            raise WindowFailed(failed, out)
+        return out
+
+    def dm(td):
+        return (["A"], np.array(["r1_tumor"]), "", "", td, "NormalOutput")
+
+    def dm2(td):
+        return [(["A"], np.array(["r1_tumor"]), "", "", td, "corner5"),
+                (["A"], np.array(["r1_tumor"]), "", "", td, "corner3")]
+
+    monkeypatch.setattr(som_td_detector, "DecisionBatch", fake_batch)
+    tds = ["chr1\t10\t20\tDEL,ok", "chr1\t30\t40\tDEL,fail1", "chr1\t50\t60\tDUP,fail5",
+           "chr1\t70\t80\tDUP,rescue3", "chr1\t90\t99\tDUP,plain"]
+    with pytest.raises(WindowFailed) as ei:
+        som_td_detector.TDscope_batch(tds, dm, dm2)
+    e = ei.value
+    assert sorted(e.failed) == [1, 2]
+    assert e.records[1] is None and e.records[2] is None
+    assert e.records[0][-1] == "NormalOutput"
+    assert e.records[3][-1] == "corner3|EMOutput"
+    assert e.records[4][-1] == "NormalOutput"

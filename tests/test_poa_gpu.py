@@ -92,7 +92,10 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_WPJ": "2"},
     {"SVS_POA_WPJ": "4"},
     {"SVS_POA_WPJ": "8"},
-    {"SVS_POA_WPJ": "16"},
+    {"SVS_POA_DUAL": "0"},
+    {"SVS_POA_DUAL": "0", "SVS_POA_WPJ": "16"},
+    {"SVS_POA_DUAL": "0", "SVS_POA_WPJ": "2"},
+    {"SVS_POA_DUAL": "0", "SVS_POA_PRUNE_SLACK": "0", "SVS_POA_WPJ": "8"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "1"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "4"},
     {"SVS_POA_PRUNE": "0"},
@@ -108,25 +111,23 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_HOST_GRAPH": "1"},
     {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_VERIFY_PREP": "1"},
     {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_VERIFY_PREP": "1", "SVS_POA_PRUNE_SLACK": "-0.3"},
-    {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_DEVICE_PREP": "0"},
-    {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_STAGING": "vec"},
-    {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_STAGING": "vec", "SVS_POA_PRUNE_SLACK": "-0.3"},
+    {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_DUAL": "0", "SVS_POA_PRUNE_SLACK": "-0.3"},
 ])
 def test_kernel_variants_match_oracle(env):
     """Every POA kernel instance the engine selects gives the oracle's result:
-    1/2/4/8/16 pipelined waves per job, the pool in global memory, and the
-    exact pruning off, at its tightest slack, and with a bound above the
-    optimum (every pruned job retried: with the looser retry slack, unpruned,
-    or twice, the second time unpruned; with the tables exported straight into
-    the staging buffer a retried job's block is exported again), and with the
-    tables packed from per-task vectors (SVS_POA_STAGING=vec); with the
-    device-resident graphs (the default) checked fold by fold against a host
-    replay (SVS_POA_VERIFY_GRAPH=1: rank order, row tables, consensus, MSA),
-    pruned retries included, also with a 64-entry LDS part of the sort's DFS
-    stack so that deep DFS paths spill to the task block; and with the host graphs (SVS_POA_HOST_GRAPH=1),
-    their row tables completed on the device and checked table for table
-    against the host's export (SVS_POA_VERIFY_PREP=1), or exported on the host
-    only (SVS_POA_DEVICE_PREP=0)."""
+    strips swept in pairs (the default with LDS pools) and one at a time
+    (SVS_POA_DUAL=0), 1/2/4/8 (single: also 16) pipelined waves per job, the
+    pool in global memory, and the exact pruning off, at its tightest slack,
+    and with a bound above the optimum (every pruned job retried: with the
+    looser retry slack, unpruned, or twice, the second time unpruned; with
+    the tables exported straight into the staging buffer a retried job's
+    block is exported again); with the device-resident graphs (the default)
+    checked fold by fold against a host replay (SVS_POA_VERIFY_GRAPH=1: rank
+    order, row tables, consensus, MSA), pruned retries included, also with a
+    64-entry LDS part of the sort's DFS stack so that deep DFS paths spill to
+    the task block; and with the host graphs (SVS_POA_HOST_GRAPH=1), their
+    row tables completed on the device and checked table for table against
+    the host's export (SVS_POA_VERIFY_PREP=1)."""
     import os
     from svscope_amd import synth
     from svscope_amd.poa import poa_batch
