@@ -340,9 +340,16 @@ def main():
             "oracle_check": digests,
             "breakdown": {"poa_cells": cells, "poa_cells_computed": cells_done,
                           "prune_retries": poa["prune_retries"],
-                          "poa_prep_kernel_ms": round(poa.get("prep_ms", 0.0), 2),
-                          "poa_prep_jobs": poa.get("prep_jobs", 0),
+                          # HIP events between the kernels on each group's fold stream
+                          # (device-resident graphs), timed steps only; they run beside
+                          # the other group's DP kernel
+                          "fold_kernel_ms": {"poa_fold_update_kernel": round(poa["fold_update_ms"], 1),
+                                             "poa_fold_sort_kernel": round(poa["fold_sort_ms"], 1),
+                                             "poa_fold_final_kernel": round(poa["fold_final_ms"], 1),
+                                             "poa_dgraph_prep_kernel": round(poa["fold_prep_ms"], 1)},
+                          "poa_table_exports": poa.get("prep_jobs", 0),
                           "poa_kernel_ms": round(kms, 2), "poa_launches": launches,
+                          "poa_dual_launches": poa.get("dual_launches", 0),
                           "gcups": round(cells_done / (kms * 1e-3) / 1e9, 3) if kms else None,
                           "gcups_full_matrix_equivalent": round(cells / (kms * 1e-3) / 1e9, 3) if kms else None,
                           "host_graph_ms": round(poa["host_graph_ms"], 1),

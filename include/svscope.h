@@ -67,6 +67,11 @@ typedef struct svs_poa_stats {
   uint64_t fold_jobs;       /* alignments (and first reads) folded into device-resident graphs */
   uint64_t wide_launches;   /* DP launches with 32-bit traceback codes (a graph node with more
                                than 31 in-edges) */
+  /* fold_ms by kernel (HIP events between the kernels on the fold stream):
+     poa_fold_update_kernel, poa_fold_sort_kernel, poa_fold_final_kernel,
+     poa_dgraph_prep_kernel */
+  double fold_update_ms, fold_sort_ms, fold_final_ms, fold_prep_ms;
+  uint64_t dual_launches;   /* DP launches sweeping strips in pairs */
 } svs_poa_stats;
 
 /* One context per host thread; owns a HIP stream and device arenas. */
@@ -141,6 +146,9 @@ int svs_ward_maxclust_batch(int32_t n_windows, const svs_em_window* wins, const 
 int svs_em_cluster_batch(svs_context* ctx, int32_t n_windows, const svs_em_window* wins, const uint8_t* X,
                          const svs_em_config* cfg, svs_em_result** out);
 int svs_em_result_get(const svs_em_result* r, int32_t window, int32_t field, const void** data, int64_t* count);
+/* The batch's EM kernel time (HIP events) and the windows the K-parallel
+ * kernel handed to the in-order one (its speculation could not place them). */
+int svs_em_result_stats(const svs_em_result* r, double* kernel_ms, int64_t* reruns);
 void svs_em_result_free(svs_em_result* r);
 /* Host-only: numpy legacy RandomState(seed).standard_exponential(n), bitwise. */
 int svs_rng_exponential_table(uint32_t seed, int64_t n, double* out);

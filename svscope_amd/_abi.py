@@ -42,7 +42,10 @@ class PoaStats(ctypes.Structure):
                 ("wall_ms", ctypes.c_double), ("gpu_wait_ms", ctypes.c_double),
                 ("cells_computed", ctypes.c_uint64), ("prune_retries", ctypes.c_uint64),
                 ("prep_ms", ctypes.c_double), ("prep_jobs", ctypes.c_uint64),
-                ("fold_ms", ctypes.c_double), ("fold_jobs", ctypes.c_uint64), ("wide_launches", ctypes.c_uint64)]
+                ("fold_ms", ctypes.c_double), ("fold_jobs", ctypes.c_uint64), ("wide_launches", ctypes.c_uint64),
+                ("fold_update_ms", ctypes.c_double), ("fold_sort_ms", ctypes.c_double),
+                ("fold_final_ms", ctypes.c_double), ("fold_prep_ms", ctypes.c_double),
+                ("dual_launches", ctypes.c_uint64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -174,6 +177,8 @@ def _declare_em(lib):
     lib.svs_msa_features.restype = ctypes.c_int
     lib.svs_em_result_get.argtypes = [P, I32, I32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64)]
     lib.svs_em_result_get.restype = ctypes.c_int
+    lib.svs_em_result_stats.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
+    lib.svs_em_result_stats.restype = ctypes.c_int
     lib.svs_em_result_free.argtypes = [P]
     lib.svs_em_result_free.restype = None
     lib.svs_aligment_score_batch.argtypes = [P, I32, P, P, I32, P, P, I32, P, P, P, ctypes.POINTER(MisscoreStats)]

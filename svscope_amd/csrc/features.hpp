@@ -16,9 +16,10 @@ struct WindowFeatures {
   int32_t rows = 0;               // rows of seqdatamx (encoded rows - 1)
   int32_t n_feat = 0;             // columns of seqdatamx
   std::vector<uint8_t> feat;      // rows x n_feat, symbols 0..4
-  std::vector<uint8_t> encoded;   // (rows + 1) x width, row 0 = MSA row 0
-  int32_t width = 0;
   std::vector<int32_t> id_map;    // returned readIDList[k] = ReadIDs[id_map[k]]
+  // SeqDecoder(seqencode[r + 1]) of every seqdatamx row r: the ungapped,
+  // upper-case read a cluster's consensus POA takes (DecisionMaker.py:157-171)
+  std::vector<std::string> row_reads;
 };
 
 // msa: the window MSA rows (all of one width); read_lens: len() of
@@ -27,6 +28,25 @@ struct WindowFeatures {
 void msa_feature_select(const std::vector<std::string>& msa, const std::string& flank_5, const std::string& flank_3,
                         const std::vector<int32_t>& read_lens, int32_t n_ids, int32_t hcutoff, double scutoff,
                         WindowFeatures* out);
+
+// The device's form of the same selection (poa_fold.hip msa_features): the
+// host works out from the window's reads and flanks what does not need the
+// MSA, the device selects the columns.
+struct DeviceFeatureParams {
+  int32_t f5_take = 0, f3_take = 0;  // CallMargin's stops (FoldJob::f5_take / f3_take)
+  uint32_t extra = 0;                // all-gap rows after the MSA rows (full-DEL reads)
+  uint32_t cut = 0;                  // FindNonSameSite: second-largest count >= cut
+  int32_t msa_rows = 0;              // MSA rows (non-empty sequences)
+  bool ok = true;                    // false: a read holds '-' (the MSA's gaps and its letters mix): host path
+};
+// seqs: the window's sequenceList (MSA row k = the k-th non-empty one).
+// Throws SvsError(SVS_E_INVALID) on a letter SeqEncoder would reject.
+DeviceFeatureParams device_feature_params(const std::vector<std::string>& seqs, const std::string& flank_5,
+                                          const std::string& flank_3, const std::vector<int32_t>& read_lens,
+                                          int32_t n_ids, int32_t hcutoff, double scutoff);
+// WindowFeatures from the device's seqdatamx (rows x n_feat).
+void device_features(const std::vector<std::string>& seqs, const std::vector<int32_t>& read_lens, int32_t n_ids,
+                     const DeviceFeatureParams& p, int32_t n_feat, std::vector<uint8_t>&& feat, WindowFeatures* out);
 
 struct ClusterPlan {
   bool som = false;

@@ -120,6 +120,13 @@ constexpr uint32_t kFoldChain = 1;   // the sequence lands on an empty graph (no
 constexpr uint32_t kFoldExport = 2;  // a next sequence follows: export its lite tables
 constexpr uint32_t kFoldFinal = 4;   // the task is complete: consensus (+ MSA rows with kFoldMsa)
 constexpr uint32_t kFoldMsa = 8;
+// With kFoldFinal | kFoldMsa: the window's MSAFeatureSelection on the device
+// (poa_fold_final_kernel, DataScanner.py:146-179,195-219): seqdatamx goes to
+// feat_out, the MSA rows stay in device scratch
+constexpr uint32_t kFoldFeat = 16;
+// FoldJob::f5_take / f3_take beyond a column count: every row-0 column of its
+// end (the flank did not match), or the empty-flank rule of CallMargin
+constexpr int32_t kTakeAll = -1, kTakeEmptyFlank = -2;
 
 struct FoldJob {
   uint8_t* blk;
@@ -135,11 +142,17 @@ struct FoldJob {
   const int32_t* aln;       // traceback pairs (reversed), from the DP launch
   const int32_t* aln_status;  // the DP job's aln_len entry (pair count / kPruneRetry / < 0)
   FoldResult* result;
-  // kFoldFinal outputs (pinned host-visible staging on the device side)
+  // kFoldFinal outputs (device buffers the host copies back)
   char* cons_out;           // consensus, <= V + len bytes
   char* msa_out;            // n_paths + 1 rows of msa_stride bytes
   uint32_t msa_stride;
   uint32_t pad;
+  // kFoldFeat: seqdatamx, (n_paths + extra) rows x n_feat symbols 0..4, into
+  // host-mapped pinned memory (FoldResult::pad1 = n_feat)
+  uint8_t* feat_out;
+  int32_t f5_take, f3_take;  // CallMargin: row-0 columns kept from the start / the end (>= 0), or kTake*
+  uint32_t extra;            // all-gap rows after the MSA rows (the full-DEL read quirk, DataScanner.py:204)
+  uint32_t cut;              // FindNonSameSite: keep a column whose second-largest count is >= cut
 };
 
 }  // namespace svs

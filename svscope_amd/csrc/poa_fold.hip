@@ -439,8 +439,6 @@ template <int L> __device__ __forceinline__ uint32_t write_lane_c(uint32_t x, ui
 }
 #define write_lane(x, s, L) write_lane_c<L>((x), (s))
 
-__device__ __forceinline__ bool bit_of(const uint32_t* plane, uint32_t v) { return (plane[v >> 5] >> (v & 31u)) & 1u; }
-
 }  // namespace
 
 // The sort, export and finalize helpers take the arrays as restrict
@@ -982,6 +980,92 @@ __device__ uint32_t consensus_rev_lds(uint32_t V, const gu8* __restrict__ base, 
   return n;
 }
 
+// DataScanner.SeqEncoder: A0 T1 C2 G3 -4, case-folded (the host checks the
+// window's reads for other letters before it asks for features).
+__device__ __forceinline__ uint32_t seq_code(uint32_t ch) {
+  const uint32_t u = ch & 0xDFu;  // upper case ('-' becomes 0x0D)
+  return u == 'A' ? 0u : (u == 'T' ? 1u : (u == 'C' ? 2u : (u == 'G' ? 3u : 4u)));
+}
+
+// MSAFeatureSelection (DataScanner.py:195-219) over the MSA rows this wave
+// has just written: CallMargin on row 0 (:146-165; the walks' stops are
+// worked out on the host from the flanks, only which columns row 0 occupies
+// is known here), then FindNonSameSite (:167-179) over rows 1 .. R-1 (R0
+// MSA rows and `extra` all-gap rows), then the kept columns of rows 1 .. R-1
+// as seqdatamx.  Lane per column; the kept column indices go through `keep`
+// (task block scratch).  Returns n_feat.
+__device__ uint32_t msa_features(const FoldJob& J, const gu32* __restrict__ col, uint32_t ncol,
+                                 const gch* __restrict__ msa, gu32* __restrict__ keep) {
+  const uint32_t lane = lanei();
+  const uint32_t R0 = J.n_paths + 1, stride = J.msa_stride;
+  const gu32* paths = glb(J.paths);
+  const gu32* poff = glb(J.path_off);
+  // row 0's columns in order are col[] of path 0's nodes
+  const uint32_t a0 = uni(poff[0]), L0 = uni(poff[1]) - a0;
+  const uint32_t c_first = L0 ? uni(col[uni(paths[a0])]) : kNone;
+  const uint32_t c_last = L0 ? uni(col[uni(paths[a0 + L0 - 1])]) : kNone;
+  // forward walk: the first m5 row-0 columns
+  uint32_t m5;
+  if (J.f5_take >= 0) m5 = min(L0, static_cast<uint32_t>(J.f5_take));
+  else if (J.f5_take == kTakeAll) m5 = L0;
+  else m5 = (L0 && c_first == 0u) ? L0 : 0u;  // empty f5: stops at once on a leading gap
+  // backward walk over columns ncol-1 .. 1: the last m3 row-0 columns >= 1
+  const uint32_t n3 = L0 - ((L0 && c_first == 0u) ? 1u : 0u);
+  uint32_t m3;
+  if (J.f3_take >= 0) m3 = min(n3, static_cast<uint32_t>(J.f3_take));
+  else if (J.f3_take == kTakeAll) m3 = n3;
+  else m3 = (n3 && ncol >= 2u && c_last == ncol - 1u) ? n3 : 0u;
+  // row-0 columns <= lo or >= hi are in the flank pool
+  const int64_t lo = m5 ? static_cast<int64_t>(uni(col[uni(paths[a0 + m5 - 1])])) : -1;
+  const int64_t hi = m3 ? static_cast<int64_t>(uni(col[uni(paths[a0 + L0 - m3])])) : static_cast<int64_t>(ncol);
+  uint32_t n_feat = 0;
+  for (uint32_t c0 = 0; c0 < ncol; c0 += 64) {
+    const uint32_t c = c0 + lane;
+    bool kept = false;
+    if (c < ncol) {
+      const bool in_pool = msa[c] != '-' && (static_cast<int64_t>(c) <= lo || static_cast<int64_t>(c) >= hi);
+      if (!in_pool) {
+        // (counters in named registers: no dynamically indexed array)
+        uint32_t n0 = 0, n1 = 0, n2 = 0, n3c = 0, n4 = J.extra;
+        for (uint32_t r = 1; r < R0; ++r) {
+          const uint32_t x = seq_code(static_cast<uint8_t>(msa[static_cast<uint64_t>(r) * stride + c]));
+          n0 += x == 0u;
+          n1 += x == 1u;
+          n2 += x == 2u;
+          n3c += x == 3u;
+          n4 += x == 4u;
+        }
+        // second-largest count (sorted(counts)[3])
+        uint32_t m1 = 0, m2 = 0;
+        for (const uint32_t v : {n0, n1, n2, n3c, n4}) {
+          m2 = v > m1 ? m1 : max(m2, v);
+          m1 = max(m1, v);
+        }
+        kept = m2 >= J.cut;
+      }
+    }
+    const uint64_t km = ballot(kept);
+    if (kept) keep[n_feat + popc64(km & below())] = c;
+    n_feat += popc64(km);
+  }
+  wave_sync_mem();
+  // seqdatamx: rows 1 .. R0-1 of the MSA, then `extra` all-gap rows
+  gu8* out = glb(J.feat_out);
+  const uint32_t rows = R0 - 1 + J.extra;
+  for (uint32_t k0 = 0; k0 < n_feat; k0 += 64) {
+    const uint32_t k = k0 + lane;
+    const uint32_t c = k < n_feat ? keep[k] : 0u;
+    for (uint32_t r = 1; r < R0; ++r) {
+      if (k < n_feat)
+        out[static_cast<uint64_t>(r - 1) * n_feat + k] =
+            static_cast<uint8_t>(seq_code(static_cast<uint8_t>(msa[static_cast<uint64_t>(r) * stride + c])));
+    }
+    for (uint32_t r = R0 - 1; r < rows; ++r)
+      if (k < n_feat) out[static_cast<uint64_t>(r) * n_feat + k] = 4u;
+  }
+  return n_feat;
+}
+
 // MSA rows: every sequence's path nodes at their columns, '-' elsewhere.
 __device__ void msa_rows(uint32_t n_paths, const gu32* __restrict__ paths, const gu32* __restrict__ path_off,
                          const gu32* __restrict__ colv, const gu8* __restrict__ base, uint32_t ncol,
@@ -1097,7 +1181,13 @@ __global__ __launch_bounds__(64) void poa_fold_final_kernel(const FoldJob* __res
   }
   if (J.flags & kFoldMsa)
     msa_rows(J.n_paths + 1, glb(J.paths), glb(J.path_off), g.col, g.base, ncol, glb(J.msa_out), J.msa_stride);
+  uint32_t n_feat = 0;
+  if (J.flags & kFoldFeat) {
+    wave_sync_mem();  // the MSA rows this wave has just stored
+    n_feat = msa_features(J, g.col, ncol, glb(static_cast<const char*>(J.msa_out)), g.last);
+  }
   if (lanei() == 0) {
+    res->pad1 = n_feat;
     res->pad0 = nc;
     res->t_fin = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime() - T0);
   }
@@ -1140,13 +1230,16 @@ __global__ __launch_bounds__(256) void poa_dgraph_move_kernel(const uint8_t* __r
 }
 
 hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, uint32_t final_lds_words,
-                           hipStream_t stream) {
+                           hipStream_t stream, const hipEvent_t* marks) {
   if (n_jobs <= 0) return hipSuccess;
   hipLaunchKernelGGL(poa_fold_update_kernel, dim3(n_jobs), dim3(64), 0, stream, jobs);
+  if (marks) (void)hipEventRecord(marks[0], stream);
   hipLaunchKernelGGL(poa_fold_sort_kernel, dim3(n_jobs), dim3(64), lds_words * 4, stream, jobs, lds_words);
+  if (marks) (void)hipEventRecord(marks[1], stream);
   if (final_lds_words)
     hipLaunchKernelGGL(poa_fold_final_kernel, dim3(n_jobs), dim3(64), final_lds_words * 4, stream, jobs,
                        final_lds_words);
+  if (marks) (void)hipEventRecord(marks[2], stream);
   return hipGetLastError();
 }
 

@@ -91,6 +91,8 @@ int svs_init(int device_ordinal, svs_context** out) {
     SVS_HIP(hipStreamCreateWithFlags(&ctx->em_stream, hipStreamNonBlocking));
     SVS_HIP(hipEventCreate(&ctx->ev_start));
     SVS_HIP(hipEventCreate(&ctx->ev_stop));
+    SVS_HIP(hipEventCreate(&ctx->ev_mid));
+    SVS_HIP(hipEventCreate(&ctx->ev_rerun));
     size_t free_b = 0, total_b = 0;
     SVS_HIP(hipMemGetInfo(&free_b, &total_b));
     size_t budget = free_b / 2;
@@ -126,6 +128,8 @@ void svs_release(svs_context* ctx) {
   for (svs::PinnedBuf* b : {&ctx->h_em_in, &ctx->h_em_out}) b->release();
   if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
   if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
+  if (ctx->ev_mid) (void)hipEventDestroy(ctx->ev_mid);
+  if (ctx->ev_rerun) (void)hipEventDestroy(ctx->ev_rerun);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->em_stream) (void)hipStreamDestroy(ctx->em_stream);
   delete ctx->pool;

@@ -72,13 +72,14 @@ struct DeviceBuf {
 struct PinnedBuf {
   void* ptr = nullptr;
   size_t cap = 0;
+  unsigned flags = hipHostMallocDefault;  // hipHostMallocMapped: kernels write it (hipHostGetDevicePointer)
   void ensure(size_t bytes) {
     if (bytes <= cap) return;
     if (ptr) SVS_HIP(hipHostFree(ptr));
     ptr = nullptr;
     const size_t want = std::max(bytes + bytes / 4 + 4096, 2 * cap);  // geometric: few regrows
     cap = 0;
-    SVS_HIP(hipHostMalloc(&ptr, want, hipHostMallocDefault));
+    SVS_HIP(hipHostMalloc(&ptr, want, flags));
     cap = want;
   }
   // grows to at least `bytes`, keeping the first `keep` bytes
@@ -112,11 +113,15 @@ struct PoaArena {
   // results, and the finished tasks' consensus + MSA rows
   DeviceBuf d_desc, d_fin;
   PinnedBuf h_desc, h_fin;
+  PinnedBuf h_feat;  // window seqdatamx written by the final fold kernel (zero-copy)
   hipStream_t stream = nullptr;       // kernel stream (shared by both groups)
   hipStream_t copy_stream = nullptr;  // this group's copies
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr, h2d = nullptr;
   hipEvent_t evp = nullptr, evp1 = nullptr;  // around the launch's poa_strip_prep_kernel
   hipEvent_t evf0 = nullptr, evf1 = nullptr;  // around the launch's fold kernels (device-resident graphs)
+  // after the update, sort and final fold kernels: of the folds after the DP
+  // kernel (evk) and of the new tasks' chains before it (evpk)
+  hipEvent_t evk[3] = {nullptr, nullptr, nullptr}, evpk[3] = {nullptr, nullptr, nullptr};
   // Staging of the next launch's strip tables in h_in: the fold exports each
   // job's tables straight into a block claimed with an atomic bump (st_cur), so
   // packing the launch copies nothing.  A new generation (st_gen) starts when
@@ -131,6 +136,7 @@ struct PoaArena {
   // group's next launch is ready when the DP stream gets to it.
   PoaArena(int device, hipStream_t s) : stream(s) {
     SVS_HIP(hipSetDevice(device));
+    h_feat.flags = hipHostMallocMapped;
     int least = 0, greatest = 0;
     SVS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
     SVS_HIP(hipStreamCreateWithPriority(&copy_stream, hipStreamNonBlocking, greatest));
@@ -140,6 +146,10 @@ struct PoaArena {
     SVS_HIP(hipEventCreate(&evp1));
     SVS_HIP(hipEventCreate(&evf0));
     SVS_HIP(hipEventCreate(&evf1));
+    for (int k = 0; k < 3; ++k) {
+      SVS_HIP(hipEventCreate(&evk[k]));
+      SVS_HIP(hipEventCreate(&evpk[k]));
+    }
     SVS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
     SVS_HIP(hipEventCreateWithFlags(&h2d, hipEventDisableTiming));
   }
@@ -147,13 +157,17 @@ struct PoaArena {
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     for (DeviceBuf* b : {&d_in, &d_tb, &d_pool, &d_aln, &d_alen, &d_desc, &d_fin}) b->release();
-    for (PinnedBuf* b : {&h_in, &h_aln, &h_alen, &h_desc, &h_fin}) b->release();
+    for (PinnedBuf* b : {&h_in, &h_aln, &h_alen, &h_desc, &h_fin, &h_feat}) b->release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (evp) (void)hipEventDestroy(evp);
     if (evp1) (void)hipEventDestroy(evp1);
     if (evf0) (void)hipEventDestroy(evf0);
     if (evf1) (void)hipEventDestroy(evf1);
+    for (int k = 0; k < 3; ++k) {
+      if (evk[k]) (void)hipEventDestroy(evk[k]);
+      if (evpk[k]) (void)hipEventDestroy(evpk[k]);
+    }
     if (done) (void)hipEventDestroy(done);
     if (h2d) (void)hipEventDestroy(h2d);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
@@ -171,6 +185,9 @@ struct svs_context {
   hipStream_t stream = nullptr;     // POA launches (task groups alternate on it)
   hipStream_t em_stream = nullptr;  // similarity + EM kernels, concurrent with POA
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  // EM K-parallel path: after its kernel, and before the in-order rerun (the
+  // host check between them is not kernel time)
+  hipEvent_t ev_mid = nullptr, ev_rerun = nullptr;
   svs::ThreadPool* pool = nullptr;
   size_t device_budget = 0;  // bytes usable for traceback + row pool per launch
   // POA arenas, one per concurrently in-flight task group

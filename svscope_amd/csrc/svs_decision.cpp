@@ -124,6 +124,10 @@ class Pipeline {
     // unpruned).
     const char* e = std::getenv("SVS_POA_CONS_PRIOR");
     cons_prior = e ? std::atof(e) : 1.5;
+    // SVS_DEVICE_FEATURES=0: the window MSA rows come back and the host
+    // selects the features (the round-3 path)
+    const char* df = std::getenv("SVS_DEVICE_FEATURES");
+    device_features_on = !(df && std::string(df) == "0");
     ecfg = cfg.em;
     ecfg.want_params = 0;
     t_wall = Clock::now();
@@ -186,6 +190,15 @@ class Pipeline {
       }
       b.f5[w].assign(W.flank5_len ? b.text + W.flank5_off : "", W.flank5_len);
       b.f3[w].assign(W.flank3_len ? b.text + W.flank3_off : "", W.flank3_len);
+      // the window's feature selection on the device when its graph is there
+      // (else, or for a letter SeqEncoder rejects, the host's from the MSA rows)
+      t.features = device_features_on;
+      try {
+        t.feat_params = device_feature_params(t.seqs, b.f5[w], b.f3[w], b.read_lens[w], W.n_ids, cfg.hcutoff,
+                                              cfg.scutoff);
+      } catch (const SvsError&) {
+        t.feat_params.ok = false;
+      }
       sched.add(std::move(t));
     }
     st.msa_tasks += b.n;
@@ -297,7 +310,7 @@ class Pipeline {
         out.status = (!out.som.empty() && !out.germ.empty()) ? SVS_DEC_EMOUTPUT : SVS_DEC_EM;
       }
       std::vector<uint8_t>().swap(b.feats[w].feat);
-      std::vector<uint8_t>().swap(b.feats[w].encoded);
+      std::vector<std::string>().swap(b.feats[w].row_reads);
     });
     for (const WinRef& wr : ws) {
       Batch& b = *wr.b;
@@ -366,8 +379,26 @@ class Pipeline {
       PoaTask& t = sched.task(msa_ids[i].first);
       Batch& b = *msa_ids[i].second.b;
       const int32_t w = msa_ids[i].second.w;
-      msa_feature_select(t.msa, b.f5[w], b.f3[w], b.read_lens[w], b.wins[w].n_ids, cfg.hcutoff, cfg.scutoff,
-                         &b.feats[w]);
+      if (t.n_feat >= 0) {
+        // seqdatamx from the final fold kernel (poa_fold.hip msa_features)
+        device_features(t.seqs, b.read_lens[w], b.wins[w].n_ids, t.feat_params, t.n_feat, std::move(t.feat),
+                        &b.feats[w]);
+        if (!t.msa.empty()) {
+          // SVS_POA_VERIFY_GRAPH: the MSA rows came back too; the host's
+          // selection from them must be the same
+          WindowFeatures h;
+          msa_feature_select(t.msa, b.f5[w], b.f3[w], b.read_lens[w], b.wins[w].n_ids, cfg.hcutoff, cfg.scutoff, &h);
+          const WindowFeatures& d = b.feats[w];
+          if (h.rows != d.rows || h.n_feat != d.n_feat || h.feat != d.feat || h.id_map != d.id_map ||
+              h.row_reads != d.row_reads)
+            throw SvsError(SVS_E_INTERNAL, "device feature selection differs from the host's (window " +
+                                               std::to_string(w) + ": " + std::to_string(d.n_feat) + " vs " +
+                                               std::to_string(h.n_feat) + " columns)");
+        }
+      } else {
+        msa_feature_select(t.msa, b.f5[w], b.f3[w], b.read_lens[w], b.wins[w].n_ids, cfg.hcutoff, cfg.scutoff,
+                           &b.feats[w]);
+      }
       std::vector<std::string>().swap(t.msa);
     });
     for (const auto& m : msa_ids) {
@@ -382,7 +413,7 @@ class Pipeline {
       // EMCluster with < 3 rows reads BICList[1] past its end (ReadsCluster.py:270)
       b.res->w[w].status = (f.rows != 0 && f.n_feat >= 10) ? SVS_DEC_INDEX_ERROR : SVS_DEC_NO_EM;
       std::vector<uint8_t>().swap(f.feat);
-      std::vector<uint8_t>().swap(f.encoded);
+      std::vector<std::string>().swap(f.row_reads);
       window_complete(b);
     }
     st.features_ms += ms_since(t0);
@@ -439,6 +470,7 @@ class Pipeline {
   PoaScheduler sched;
   size_t em_batch = 512;
   double cons_prior = 1.5;
+  bool device_features_on = true;
   svs_em_config ecfg{};
   Clock::time_point t_wall;
   size_t msa_outstanding = 0;  // window MSAs queued or running, all batches

@@ -212,6 +212,7 @@ svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, co
       if (parallel) {
         SVS_HIP(launch_em_parallel(dW, n, max_nk, dX, dL, ctx->d_rng.as<double>(), ctx->rng_len, ec,
                                    ctx->d_em_ws.as<double>(), d_outd, d_outi, static_cast<size_t>(lds), ctx->em_stream));
+        SVS_HIP(hipEventRecord(ctx->ev_mid, ctx->em_stream));
         SVS_HIP(hipMemcpyAsync(ctx->h_em_out.as<char>() + outi_at, d_outi, oi * 4, hipMemcpyDeviceToHost, ctx->em_stream));
         SVS_HIP(hipStreamSynchronize(ctx->em_stream));
         const int32_t* hi = reinterpret_cast<const int32_t*>(ctx->h_em_out.as<char>() + outi_at);
@@ -219,6 +220,7 @@ svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, co
         for (int32_t w = 0; w < n; ++w)
           if (hi[W[w].outi_off + 3] == 1) rerun.push_back(W[w]);
         res->em_reruns += static_cast<int64_t>(rerun.size());
+        SVS_HIP(hipEventRecord(ctx->ev_rerun, ctx->em_stream));
         if (!rerun.empty()) {
           std::memcpy(h + off_r, rerun.data(), rerun.size() * sizeof(EmWindow));
           SVS_HIP(hipMemcpyAsync(d + off_r, h + off_r, rerun.size() * sizeof(EmWindow), hipMemcpyHostToDevice,
@@ -238,9 +240,16 @@ svs_em_result* run_em(svs_context* ctx, int32_t n, const svs_em_window* wins, co
       SVS_HIP(hipMemcpyAsync(ctx->h_em_out.ptr, ctx->d_em_out.ptr,
                              (od_bytes + 255) / 256 * 256 + oi_bytes + par_bytes, hipMemcpyDeviceToHost, ctx->em_stream));
       SVS_HIP(hipStreamSynchronize(ctx->em_stream));
-      float ms = 0.f;
-      SVS_HIP(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
-      res->kernel_ms += ms;
+      // kernel time only: in the K-parallel path the host's rerun check
+      // between ev_mid and ev_rerun is left out
+      float ms = 0.f, ms2 = 0.f;
+      if (parallel) {
+        SVS_HIP(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_mid));
+        SVS_HIP(hipEventElapsedTime(&ms2, ctx->ev_rerun, ctx->ev_stop));
+      } else {
+        SVS_HIP(hipEventElapsedTime(&ms, ctx->ev_start, ctx->ev_stop));
+      }
+      res->kernel_ms += ms + ms2;
       const int32_t* hi = reinterpret_cast<const int32_t*>(ctx->h_em_out.as<char>() + (od_bytes + 255) / 256 * 256);
       bool overflow = false;
       for (int32_t w = 0; w < n; ++w) overflow |= hi[W[w].outi_off + 2] == 2;
@@ -298,6 +307,13 @@ int svs_em_result_get(const svs_em_result* r, int32_t window, int32_t field, con
     case SVS_EM_RNG_USED: *data = &w.rng_used; *count = 1; break;
     default: return SVS_E_INVALID;
   }
+  return SVS_OK;
+}
+
+int svs_em_result_stats(const svs_em_result* r, double* kernel_ms, int64_t* reruns) {
+  if (!r) return SVS_E_INVALID;
+  if (kernel_ms) *kernel_ms = r->kernel_ms;
+  if (reruns) *reruns = r->em_reruns;
   return SVS_OK;
 }
 

@@ -75,6 +75,13 @@ struct PoaTask {
 
   std::string consensus;
   std::vector<std::string> msa;
+  // decision pipeline: the window's MSAFeatureSelection on the device (device
+  // graphs, FoldJob kFoldFeat) instead of the MSA rows; n_feat >= 0 on
+  // completion when it ran, with seqdatamx in feat
+  bool features = false;
+  DeviceFeatureParams feat_params;
+  int32_t n_feat = -1;
+  std::vector<uint8_t> feat;
   // set when the task went past an engine limit (a per-task failure: the task
   // completes with no consensus / MSA, the others go on)
   std::string error;

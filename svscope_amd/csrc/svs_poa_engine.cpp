@@ -353,6 +353,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   const bool wide = max_preds > kMaxInEdgesNarrow || force_wide();
   la.code_bytes = wide ? 4 : 2;
   st.wide_launches += wide ? 1 : 0;
+  st.dual_launches += dual ? 1 : 0;
   // the pruning variant prunes every job of its launch: the others get no bound
   if (any_prune)
     for (PoaJob& J : la.jobs)
@@ -647,7 +648,9 @@ struct DevLaunch {
   std::vector<uint8_t> moved;                    // fold i's graph moved to a larger block
   std::vector<std::pair<void*, size_t>> old_blocks;  // freed once the launch is done
   std::vector<size_t> cons_off, msa_off;         // fold i's final outputs in the fin buffer
+  std::vector<size_t> feat_off;                  // fold i's seqdatamx in the group's h_feat (kFoldFeat)
   size_t n_aln = 0, s_fold = 0, s_res = 0, fin_bytes = 0;
+  size_t fin_copy = 0;  // bytes of the fin buffer copied back (consensus first; MSA rows when wanted)
   int wpj = 0;
   bool timed_dp = false;
 };
@@ -1139,6 +1142,7 @@ struct PoaScheduler::Impl {
     D.n_aln = n_aln;
     D.wpj = wpj;
     st.wide_launches += wide ? 1 : 0;
+    st.dual_launches += (dual && nj) ? 1 : 0;
     A.d_tb.ensure(n_tb * (wide ? 4 : 2) + 4096, ctx->device_budget / 2);
     A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096);
     A.d_aln.ensure(n_aln * 8 + 64);
@@ -1148,7 +1152,31 @@ struct PoaScheduler::Impl {
     D.moved.assign(nf, 0);
     D.cons_off.assign(nf, 0);
     D.msa_off.assign(nf, 0);
-    size_t fin = 0;
+    D.feat_off.assign(nf, 0);
+    // the fin buffer: every final fold's consensus, then the MSA rows (their
+    // offsets from the MSA part's start until the consensus part is sized);
+    // a window MSA of the decision pipeline keeps its rows on the device and
+    // writes seqdatamx into the group's h_feat (kFoldFeat)
+    size_t fin = 0, fin_msa = 0, feat = 0;
+    bool msa_back = false;
+    auto final_outputs = [&](size_t i, PoaTask& t, FoldJob& F, size_t bound, uint32_t rows) {
+      D.cons_off[i] = fin;
+      fin = round_up(fin + bound, 64);
+      F.msa_stride = static_cast<uint32_t>(round_up(bound, 64));
+      if (!t.genmsa) return;
+      D.msa_off[i] = fin_msa;
+      fin_msa += static_cast<size_t>(rows) * F.msa_stride;
+      if (t.features && t.feat_params.ok) {
+        F.flags |= kFoldFeat;
+        F.f5_take = t.feat_params.f5_take;
+        F.f3_take = t.feat_params.f3_take;
+        F.extra = t.feat_params.extra;
+        F.cut = t.feat_params.cut;
+        D.feat_off[i] = feat;
+        feat = round_up(feat + static_cast<size_t>(rows - 1 + F.extra) * F.msa_stride, 64);
+      }
+      if (!(F.flags & kFoldFeat) || verify) msa_back = true;
+    };
     std::vector<std::array<uint64_t, 9>> moves;  // src, cv0, ce0, dst, cv1, ce1, V, E, par
     for (size_t i = 0; i < nf; ++i) {
       PoaTask& t = tasks[D.fold_ids[i]];
@@ -1170,15 +1198,7 @@ struct PoaScheduler::Impl {
         F.len = len;
         F.paths = t.d_paths;
         F.path_off = t.d_path_off;
-        if (last) {
-          D.cons_off[i] = fin;
-          fin = round_up(fin + len, 64);
-          F.msa_stride = static_cast<uint32_t>(round_up(len, 64));
-          if (t.genmsa) {
-            D.msa_off[i] = fin;
-            fin += F.msa_stride;
-          }
-        }
+        if (last) final_outputs(i, t, F, len, 1);
         continue;
       }
       if (t.dg.V + len > t.dg.cv || t.dg.E + len + 1 > t.dg.ce) {
@@ -1212,18 +1232,13 @@ struct PoaScheduler::Impl {
       F.n_paths = t.n_paths;
       F.paths = t.d_paths;
       F.path_off = t.d_path_off;
-      if (last) {
-        const size_t bound = t.dg.V + len;
-        D.cons_off[i] = fin;
-        fin = round_up(fin + bound, 64);
-        F.msa_stride = static_cast<uint32_t>(round_up(bound, 64));
-        if (t.genmsa) {
-          D.msa_off[i] = fin;
-          fin += static_cast<size_t>(t.n_paths + 1) * F.msa_stride;
-        }
-      }
+      if (last) final_outputs(i, t, F, t.dg.V + len, t.n_paths + 1);
     }
+    const size_t fin_cons = round_up(fin, 256);
+    for (size_t i = 0; i < nf; ++i) D.msa_off[i] += fin_cons;
+    fin = fin_cons + fin_msa;
     D.fin_bytes = fin;
+    D.fin_copy = msa_back ? fin : fin_cons;
     // descriptors: DP jobs, fold jobs, fold results; then the new tasks' reads
     // and the scatter list that copies them into their blocks
     const size_t s_fold = round_up(nj * sizeof(PoaJob), 256);
@@ -1236,7 +1251,10 @@ struct PoaScheduler::Impl {
     A.h_desc.ensure(total);
     A.d_desc.ensure(total);
     A.d_fin.ensure(fin + 64);
-    A.h_fin.ensure(fin + 64);
+    A.h_fin.ensure(D.fin_copy + 64);
+    A.h_feat.ensure(feat + 64);
+    uint8_t* d_feat = nullptr;  // the device's view of the pinned h_feat (zero-copy writes)
+    if (feat) SVS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_feat), A.h_feat.ptr, 0));
     char* dd = A.d_desc.as<char>();
     for (size_t i = 0; i < nf; ++i) {
       FoldJob& F = D.folds[i];
@@ -1248,6 +1266,7 @@ struct PoaScheduler::Impl {
       if (F.flags & kFoldFinal) {
         F.cons_out = A.d_fin.as<char>() + D.cons_off[i];
         F.msa_out = A.d_fin.as<char>() + D.msa_off[i];
+        F.feat_out = (F.flags & kFoldFeat) ? d_feat + D.feat_off[i] : nullptr;
       }
     }
     char* hd = A.h_desc.as<char>();
@@ -1295,7 +1314,7 @@ struct PoaScheduler::Impl {
     SVS_HIP(hipEventRecord(A.evp, side));
     if (npre) {
       // the new tasks' first reads, and their tables, before the DP kernel
-      SVS_HIP(launch_poa_fold(dfold, static_cast<int>(npre), lds_words, final_lds(0, npre), side));
+      SVS_HIP(launch_poa_fold(dfold, static_cast<int>(npre), lds_words, final_lds(0, npre), side, A.evpk));
       SVS_HIP(launch_dgraph_prep(dfold, static_cast<int>(npre), score, side));
     }
     SVS_HIP(hipEventRecord(A.evp1, side));
@@ -1340,14 +1359,14 @@ struct PoaScheduler::Impl {
     // graph update, sort, export and table completion beside the other group's DP
     SVS_HIP(hipEventRecord(A.evf0, side));
     if (nj) {
-      SVS_HIP(launch_poa_fold(dfold + npre, static_cast<int>(nj), lds_words, final_lds(npre, npre + nj), side));
+      SVS_HIP(launch_poa_fold(dfold + npre, static_cast<int>(nj), lds_words, final_lds(npre, npre + nj), side, A.evk));
       SVS_HIP(launch_dgraph_prep(dfold + npre, static_cast<int>(nj), score, side));
     }
     SVS_HIP(hipEventRecord(A.evf1, side));
     A.h_alen.ensure(nj * 12 + 64);
     if (nj) SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, A.d_alen.ptr, nj * 12, hipMemcpyDeviceToHost, side));
     SVS_HIP(hipMemcpyAsync(hd + s_res, dd + s_res, nf * sizeof(FoldResult), hipMemcpyDeviceToHost, side));
-    if (fin) SVS_HIP(hipMemcpyAsync(A.h_fin.ptr, A.d_fin.ptr, fin, hipMemcpyDeviceToHost, side));
+    if (D.fin_copy) SVS_HIP(hipMemcpyAsync(A.h_fin.ptr, A.d_fin.ptr, D.fin_copy, hipMemcpyDeviceToHost, side));
     if (verify) {
       A.h_aln.ensure(n_aln * 8 + 64);
       if (nj) SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, A.d_aln.ptr, n_aln * 8, hipMemcpyDeviceToHost, side));
@@ -1366,7 +1385,7 @@ struct PoaScheduler::Impl {
     st.tb_bytes += n_tb * 2;
     st.pool_bytes += (n_bnd + n_pool) * 4;
     st.h2d_bytes += total;
-    st.d2h_bytes += nj * 12 + nf * sizeof(FoldResult) + fin;
+    st.d2h_bytes += nj * 12 + nf * sizeof(FoldResult) + D.fin_copy;
     st.fold_jobs += nf;
     for (const FoldJob& F : D.folds) st.prep_jobs += (F.flags & kFoldExport) ? 1 : 0;
   }
@@ -1400,6 +1419,20 @@ struct PoaScheduler::Impl {
       SVS_HIP(hipEventElapsedTime(&ms, A.evf0, A.evf1));
       SVS_HIP(hipEventElapsedTime(&pms, A.evp, A.evp1));
       st.fold_ms += ms + pms;
+      // per fold kernel: update, sort, final, then the table completion
+      auto phases = [&](hipEvent_t e0, const hipEvent_t* k, hipEvent_t e1) {
+        float t[4] = {0.f, 0.f, 0.f, 0.f};
+        SVS_HIP(hipEventElapsedTime(&t[0], e0, k[0]));
+        SVS_HIP(hipEventElapsedTime(&t[1], k[0], k[1]));
+        SVS_HIP(hipEventElapsedTime(&t[2], k[1], k[2]));
+        SVS_HIP(hipEventElapsedTime(&t[3], k[2], e1));
+        st.fold_update_ms += t[0];
+        st.fold_sort_ms += t[1];
+        st.fold_final_ms += t[2];
+        st.fold_prep_ms += t[3];
+      };
+      if (nj) phases(A.evf0, A.evk, A.evf1);
+      if (D.n_pre) phases(A.evp, A.evpk, A.evp1);
     }
     if (g_trace.f) {
       uint64_t cells = 0;
@@ -1477,10 +1510,18 @@ struct PoaScheduler::Impl {
         t.consensus.assign(h + D.cons_off[i], nc);
         std::reverse(t.consensus.begin(), t.consensus.end());
         t.msa.clear();
-        if (F.flags & kFoldMsa) {
+        if ((F.flags & kFoldMsa) && D.fin_copy > D.msa_off[i]) {
           t.msa.reserve(t.n_paths);
           for (uint32_t s = 0; s < t.n_paths; ++s)
             t.msa.emplace_back(h + D.msa_off[i] + static_cast<size_t>(s) * F.msa_stride, r.ncol);
+        }
+        if (F.flags & kFoldFeat) {
+          // seqdatamx, written by the final kernel straight into pinned memory
+          // (counted as D2H: it crosses PCIe)
+          const uint8_t* fx = A.h_feat.as<uint8_t>() + D.feat_off[i];
+          t.n_feat = static_cast<int32_t>(r.pad1);
+          t.feat.assign(fx, fx + static_cast<size_t>(t.n_paths - 1 + F.extra) * r.pad1);
+          st.d2h_bytes += t.feat.size();
         }
         if (verify) verify_final(t);
         release_dev(t);

@@ -262,12 +262,19 @@ def _dist_setup():
     import torch.distributed as dist
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = torch.cuda.is_available()
+    # SVS_DIST_BACKEND=gloo with SVS_DEVICE=d (tests on a one-GPU box): every
+    # rank's engine on GPU d, the record gather over gloo on the host
+    backend = os.environ.get("SVS_DIST_BACKEND") or ("nccl" if gpu else "gloo")
+    device = torch.device("cpu")
     if gpu:
-        torch.cuda.set_device(local)
-        os.environ.setdefault("SVS_DEVICE", str(local))
+        ordinal = int(os.environ.get("SVS_DEVICE", local))
+        torch.cuda.set_device(ordinal)
+        os.environ["SVS_DEVICE"] = str(ordinal)
+        if backend == "nccl":
+            device = torch.device("cuda", ordinal)
     if not dist.is_initialized():
-        dist.init_process_group("nccl" if gpu else "gloo")
-    return world, rank, dist, torch.device("cuda", local) if gpu else torch.device("cpu")
+        dist.init_process_group(backend)
+    return world, rank, dist, device
 
 
 def _finish(path, lines_by_rank, rank, world, dist, device, finished, t0, what):

@@ -87,6 +87,11 @@ def em_cluster_batch(mats, max_C=9, n_step=20, seed=2023, want_params=False, con
         timing["em_cluster_call_s"] = time.perf_counter() - t0
     out = []
     try:
+        if timing is not None:
+            kms, reruns = ctypes.c_double(), ctypes.c_int64()
+            _abi.check(ctx.lib.svs_em_result_stats(res, ctypes.byref(kms), ctypes.byref(reruns)))
+            timing["em_kernel_ms"] = kms.value
+            timing["em_reruns"] = reruns.value
         ptr = ctypes.c_void_p()
         cnt = ctypes.c_int64()
 

@@ -12,8 +12,16 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "decision_goldens.json")
 
 
-def test_decision_batch_matches_reference_goldens():
+@pytest.mark.parametrize("env", [{}, {"SVS_POA_VERIFY_GRAPH": "1"}, {"SVS_DEVICE_FEATURES": "0"}])
+def test_decision_batch_matches_reference_goldens(env, monkeypatch):
+    """The reference's own records (full-deletion read, gate failures,
+    germline-only window, empty flanks): with the window's feature selection
+    on the device (default), with it checked against the host's selection from
+    the returned MSA rows (SVS_POA_VERIFY_GRAPH=1), and on the host
+    (SVS_DEVICE_FEATURES=0)."""
     from svscope_amd.decision_maker import DecisionBatch
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     cases = json.load(open(GOLD))
     wins = [(c["TDRecord"], c["sequenceList"], np.array(c["ReadIDs"]), c["flank_5"], c["flank_3"]) for c in cases]
     for c, rec in zip(cases, DecisionBatch(wins)):
@@ -226,6 +234,61 @@ def test_bench_windows_match_oracle_digests():
     bad = [k for k, (a, b) in enumerate(zip(digests, gold["digests"])) if a != b]
     assert not bad, f"{len(bad)} windows differ from the oracle, first {bad[:8]}"
     assert hashlib.sha256("\n".join(digests).encode()).hexdigest() == gold["all"]
+
+
+def _session_digests(rows, batch, depth=4):
+    """Records of rows through one streaming DecisionSession (batches of
+    `batch`, `depth` in flight, as bench.py and localGraph_npz run), as the
+    SHA-256 of each Raw.bed line; and the session's statistics."""
+    import hashlib
+    from collections import deque
+    from svscope_amd.decision_maker import DecisionSession
+    from svscope_amd.local_graph import _window, record_line
+    got = []
+    with DecisionSession() as s:
+        q = deque()
+        for k in range(0, len(rows), batch):
+            q.append(s.submit([_window(r) for r in rows[k:k + batch]]))
+            if len(q) >= depth:
+                got += s.wait(q.popleft())
+        while q:
+            got += s.wait(q.popleft())
+        st = s.stats()
+    return [hashlib.sha256(record_line(r).encode()).hexdigest() for r in got], st
+
+
+def test_device_features_verified_on_config3_windows(monkeypatch):
+    """Config-3 windows (64 reads x 3 kb, bench window ids 0..11) with the
+    graphs replayed on the host fold by fold and the device's seqdatamx,
+    read ids and cluster reads compared with the host's selection from the
+    MSA rows (SVS_POA_VERIFY_GRAPH=1), and the records equal to the oracle's
+    digests (tests/golden/bench_config3_digests.json)."""
+    from svscope_amd import synth
+    monkeypatch.setenv("SVS_POA_VERIFY_GRAPH", "1")
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_config3_digests.json")))
+    rows = [synth.make_window(w, 64, 3000) for w in range(12)]
+    digests, st = _session_digests(rows, 6)
+    assert digests == gold["digests"][:12]
+
+
+@pytest.mark.parametrize("name,batch", [("config2", 16), ("harsh", 8)])
+def test_unbenched_paths_match_oracle_digests(name, batch):
+    """the paths bench.py does not run, pinned against the
+    CPU oracle (tests/golden/gen_path_goldens.py): 64 config-2 windows (32
+    reads x 2 kb) through the streaming session, and 24 windows of
+    tools/prune_probe.py's harsh profile (15 % error, 1.5-2.5 kb insertions),
+    where the exact pruning's bound misses and retried alignments must still
+    give the oracle's records (the test asserts that retries ran)."""
+    from svscope_amd import synth
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", f"{name}_digests.json")))
+    kw = {k: tuple(v) if isinstance(v, list) else v for k, v in gold["make_window_kw"].items()}
+    rows = [synth.make_window(w, gold["reads"], gold["ref_len"], **kw) for w in range(gold["n"])]
+    digests, st = _session_digests(rows, batch)
+    bad = [k for k, (a, b) in enumerate(zip(digests, gold["digests"])) if a != b]
+    assert not bad, f"{len(bad)} windows differ from the oracle, first {bad[:8]}"
+    assert len(digests) == gold["n"]
+    if name == "harsh":
+        assert st["poa"]["prune_retries"] > 0, st["poa"]
 
 
 def test_big_windows_mixed_into_config3_batch_match_oracle():
