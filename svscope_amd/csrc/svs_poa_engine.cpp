@@ -284,10 +284,13 @@ int choose_wpj(size_t nj, uint32_t max_slots, uint32_t min_strips, bool lds_pool
 }
 
 // Strips swept in pairs (poa_strip.hip DUAL) for launches whose pools sit in
-// LDS, unless SVS_POA_DUAL=0.
+// LDS with SVS_POA_DUAL=1.  Measured slower (profiles/r04_d2, r04_ab1: MSA
+// probe kernel 3668 vs 2903 ms, bench 205.8 vs 252.0 windows/s): a dual wave
+// does about 1.6x the cells of a single one at half the waves per CU (LDS and
+// 128 VGPRs with 81 SGPR spills), so it stays a development variant.
 bool dual_sweeps() {
   const char* e = std::getenv("SVS_POA_DUAL");
-  return !(e && std::string(e) == "0");
+  return e && std::string(e) == "1";
 }
 
 void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, const PoaScore& score,

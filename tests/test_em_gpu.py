@@ -120,8 +120,8 @@ def em_mfma(monkeypatch):
 def test_em_mfma_variant_matches_reference_goldens(em_mfma):
     """The v_mfma_f64_16x16x4_f64 E-step contraction (SVS_EM_MFMA=1) keeps the
     reference's K and labels exactly, BIC / log-likelihood within 1e-5."""
-    test_em_matches_reference_goldens()
+    test_em_matches_reference_goldens("parallel")
 
 
 def test_em_mfma_variant_matches_oracle(em_mfma):
-    test_em_matches_oracle_random_and_reinit_heavy()
+    test_em_matches_oracle_random_and_reinit_heavy("parallel")
