@@ -93,12 +93,17 @@ struct PoaTrace {
   void host(const char* what, int g, Clock::time_point a, size_t n) {
     if (f) std::fprintf(f, "host %s %d %.3f %.3f %zu\n", what, g, at(a), at(Clock::now()), n);
   }
-  void kernel(int g, hipEvent_t k0, hipEvent_t k1, size_t n, int wpj, uint64_t cells) {
+  // DP launches also log their kernel instance (prune, dual, wide code flags)
+  // and the cells the kernel evaluated (tools/profile_bench_*.sh: per-row
+  // counter figures of one instance)
+  void kernel(int g, hipEvent_t k0, hipEvent_t k1, size_t n, int wpj, uint64_t cells, int prune = 0, int dual = 0,
+              int wide = 0, uint64_t computed = 0) {
     if (!f) return;
     float a = 0.f, b = 0.f;
     SVS_HIP(hipEventElapsedTime(&a, e0, k0));
     SVS_HIP(hipEventElapsedTime(&b, e0, k1));
-    std::fprintf(f, "kern %d %.3f %.3f %zu %d %llu\n", g, a, b, n, wpj, static_cast<unsigned long long>(cells));
+    std::fprintf(f, "kern %d %.3f %.3f %zu %d %llu %d %d %d %llu\n", g, a, b, n, wpj,
+                 static_cast<unsigned long long>(cells), prune, dual, wide, static_cast<unsigned long long>(computed));
   }
   void close() {
     if (!f) return;
@@ -656,6 +661,7 @@ struct DevLaunch {
   size_t fin_copy = 0;  // bytes of the fin buffer copied back (consensus first; MSA rows when wanted)
   int wpj = 0;
   bool timed_dp = false;
+  bool prune = false, dual = false, wide = false;  // the DP kernel instance
 };
 
 // Task group: a disjoint subset of the active tasks with its own arena.
@@ -1144,6 +1150,9 @@ struct PoaScheduler::Impl {
         if (J.lb == kNoPrune) J.lb = kPruneAll;
     D.n_aln = n_aln;
     D.wpj = wpj;
+    D.prune = any_prune;
+    D.dual = dual;
+    D.wide = wide;
     st.wide_launches += wide ? 1 : 0;
     st.dual_launches += (dual && nj) ? 1 : 0;
     A.d_tb.ensure(n_tb * (wide ? 4 : 2) + 4096, ctx->device_budget / 2);
@@ -1441,7 +1450,10 @@ struct PoaScheduler::Impl {
       uint64_t cells = 0;
       for (const PoaJob& J : D.jobs) cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);
       g_trace.host("wait", gid(g), tw0, nf);
-      if (D.timed_dp) g_trace.kernel(gid(g), A.ev0, A.ev1, nj, D.wpj, cells);
+      uint64_t computed = 0;
+      const int32_t* al = A.h_alen.as<int32_t>();
+      for (size_t k = 0; k < nj; ++k) computed += 64ull * static_cast<uint32_t>(al[2 * nj + k]);
+      if (D.timed_dp) g_trace.kernel(gid(g), A.ev0, A.ev1, nj, D.wpj, cells, D.prune, D.dual, D.wide, computed);
       g_trace.kernel(10 + gid(g), A.evf0, A.evf1, nj, 0, 0);  // the fold chain after the DP kernel
       if (D.n_pre) g_trace.kernel(20 + gid(g), A.evp, A.evp1, D.n_pre, 0, 0);  // the chains before it
     }
