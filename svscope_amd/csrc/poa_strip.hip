@@ -174,6 +174,26 @@ __device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, con
 #define SVS_POLL_S2 8
 #endif
 constexpr long kStripSpinLimit = 1l << 26;
+
+// SVS_STRIP_PROF (development builds, tools/build_variant.py): per wave, the
+// shader clocks spent waiting for the producing wave's progress, in
+// fast_forward, in sweeps, in the traceback and at the job's final barrier,
+// and the wave's lifetime, summed over the launch into svs_strip_prof
+// (tools/poa_probe.py reads them through svs_debug_strip_prof).
+#ifdef SVS_STRIP_PROF
+__device__ unsigned long long svs_strip_prof[8];
+#define SVS_SP_T() __builtin_amdgcn_s_memtime()
+#define SVS_SP_DECL uint64_t sp_acc[6] = {0, 0, 0, 0, 0, 0}; const uint64_t sp_t0 = SVS_SP_T()
+#define SVS_SP(i, stmt)                  \
+  do {                                   \
+    const uint64_t sp_a = SVS_SP_T();    \
+    stmt;                                \
+    sp_acc[i] += SVS_SP_T() - sp_a;      \
+  } while (0)
+#else
+#define SVS_SP_DECL
+#define SVS_SP(i, stmt) stmt
+#endif
 __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, int32_t* err) {
   long n = 0;
   int32_t v;
@@ -224,6 +244,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   extern __shared__ int32_t lds[];
   using TF = TbFmt<CodeT>;
   const PoaScore P = Parg;
+  SVS_SP_DECL;
   __shared__ int32_t prog[WPJ];  // per wave: strip * (V + 1) + rows done, carries published
   __shared__ int32_t s_err;
   __shared__ int32_t s_brow[WPJ], s_best[WPJ];
@@ -378,7 +399,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         if (WPJ > 1) {
           const int32_t need = need0 + static_cast<int32_t>(rr) + 1;
           if (avail < need) {
-            avail = strip_wait_ge(&prog[pw], need, &s_err);
+            SVS_SP(0, avail = strip_wait_ge(&prog[pw], need, &s_err));
           }
         }
         const svs_i32x4 v = *reinterpret_cast<const GLB svs_i32x4*>(bin + (rr << 2));
@@ -652,7 +673,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
           // is not waited for, so the scan keeps pace with its producer
           const int32_t least = need0 + static_cast<int32_t>(min(V, r + 8));
           if (avail < least) {
-            avail = strip_wait_ge(&prog[pw], least, &s_err);
+            SVS_SP(0, avail = strip_wait_ge(&prog[pw], least, &s_err));
           }
           lim = min(lim, static_cast<uint32_t>(min(static_cast<int32_t>(V), avail - need0)) - r);
         }
@@ -697,14 +718,14 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     // loads still in flight when a set is refilled)
     RowIn A, B;
     uint32_t r = 0;
-    if (prune) r = fast_forward(0);
+    if (prune) SVS_SP(1, r = fast_forward(0));
     pub_left = 8u - (r & 7u);
     fetch(A, r);
     fetch(B, r + 1);
     while (r < V) {
       step(r, A);
       if (prune && dead_strip()) {
-        r = fast_forward(r + 1);
+        SVS_SP(1, r = fast_forward(r + 1));
         pub_left = 8u - (r & 7u);
         fetch(A, r);
         fetch(B, r + 1);
@@ -714,7 +735,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       if (r + 1 >= V) break;
       step(r + 1, B);
       if (prune && dead_strip()) {
-        r = fast_forward(r + 2);
+        SVS_SP(1, r = fast_forward(r + 2));
         pub_left = 8u - (r & 7u);
         fetch(A, r);
         fetch(B, r + 1);
@@ -1183,14 +1204,14 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       const int32_t nsweeps = 1 + nstrips / 2;
       for (int32_t t = wave; t < nsweeps; t += WPJ) {
         const int32_t s = 2 * t - 1;
-        if (t == 0) sweep(TrueT{}, 0);
-        else if (s + 1 < nstrips) sweep2(s);
-        else sweep(FalseT{}, s);
+        if (t == 0) SVS_SP(2, sweep(TrueT{}, 0));
+        else if (s + 1 < nstrips) SVS_SP(2, sweep2(s));
+        else SVS_SP(2, sweep(FalseT{}, s));
       }
     } else {
       for (int32_t s = wave; s < nstrips; s += WPJ) {
-        if (s == 0) sweep(TrueT{}, 0);
-        else sweep(FalseT{}, s);
+        if (s == 0) SVS_SP(2, sweep(TrueT{}, 0));
+        else SVS_SP(2, sweep(FalseT{}, s));
       }
     }
   }
@@ -1210,8 +1231,18 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
+    SVS_SP(4, __syncthreads());
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#ifdef SVS_STRIP_PROF
+    if (wave != 0 && lane == 0) {
+      atomicAdd(&svs_strip_prof[0], sp_acc[0]);
+      atomicAdd(&svs_strip_prof[1], sp_acc[1]);
+      atomicAdd(&svs_strip_prof[2], sp_acc[2]);
+      atomicAdd(&svs_strip_prof[4], sp_acc[4]);
+      atomicAdd(&svs_strip_prof[5], SVS_SP_T() - sp_t0);
+      atomicAdd(&svs_strip_prof[7], 1ull);
+    }
+#endif
     if (wave != 0) return;
     best_row = s_brow[sink_wave];
     best = s_best[sink_wave];
@@ -1291,8 +1322,17 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       out[2 * n + 1] = b;
     }
   };
-  const int32_t nout = poa_traceback<TF>(P, V, L, best_row, tbc, pred_of, emit);
+  int32_t nout;
+  SVS_SP(3, nout = poa_traceback<TF>(P, V, L, best_row, tbc, pred_of, emit));
   if (lane == 0) aln_len[job_id] = nout;
+#ifdef SVS_STRIP_PROF
+  if (lane == 0) {
+    for (int i = 0; i < 5; ++i) atomicAdd(&svs_strip_prof[i], sp_acc[i]);
+    atomicAdd(&svs_strip_prof[5], SVS_SP_T() - sp_t0);
+    atomicAdd(&svs_strip_prof[6], static_cast<unsigned long long>(rows_done));
+    atomicAdd(&svs_strip_prof[7], 1ull);
+  }
+#endif
 }
 
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
@@ -1382,6 +1422,22 @@ __global__ void wave_scan_selftest_kernel(const int32_t* in, int32_t* out_scan, 
   const int32_t x = in[blockIdx.x * 64 + lane];
   out_scan[blockIdx.x * 64 + lane] = wave_prefix_max(x);
   out_shift[blockIdx.x * 64 + lane] = wave_shr1(x, -7, lane);
+}
+
+// SVS_STRIP_PROF builds: the counters above (out[8]); reset = 1 zeroes them.
+// Other builds report zeros.
+extern "C" int svs_debug_strip_prof(unsigned long long* out, int reset) {
+#ifdef SVS_STRIP_PROF
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(svs_strip_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return -3;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(svs_strip_prof), z, sizeof(z)) != hipSuccess) return -3;
+  }
+#else
+  (void)reset;
+  for (int i = 0; i < 8; ++i) out[i] = 0;
+#endif
+  return 0;
 }
 
 hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
