@@ -181,9 +181,9 @@ constexpr long kStripSpinLimit = 1l << 26;
 // and the wave's lifetime, summed over the launch into svs_strip_prof
 // (tools/poa_probe.py reads them through svs_debug_strip_prof).
 #ifdef SVS_STRIP_PROF
-__device__ unsigned long long svs_strip_prof[8];
+__device__ unsigned long long svs_strip_prof[10];
 #define SVS_SP_T() __builtin_amdgcn_s_memtime()
-#define SVS_SP_DECL uint64_t sp_acc[6] = {0, 0, 0, 0, 0, 0}; const uint64_t sp_t0 = SVS_SP_T()
+#define SVS_SP_DECL uint64_t sp_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}; const uint64_t sp_t0 = SVS_SP_T()
 #define SVS_SP(i, stmt)                  \
   do {                                   \
     const uint64_t sp_a = SVS_SP_T();    \
@@ -673,7 +673,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
           // is not waited for, so the scan keeps pace with its producer
           const int32_t least = need0 + static_cast<int32_t>(min(V, r + 8));
           if (avail < least) {
-            SVS_SP(0, avail = strip_wait_ge(&prog[pw], least, &s_err));
+            SVS_SP(8, avail = strip_wait_ge(&prog[pw], least, &s_err));
           }
           lim = min(lim, static_cast<uint32_t>(min(static_cast<int32_t>(V), avail - need0)) - r);
         }
@@ -1241,6 +1241,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       atomicAdd(&svs_strip_prof[4], sp_acc[4]);
       atomicAdd(&svs_strip_prof[5], SVS_SP_T() - sp_t0);
       atomicAdd(&svs_strip_prof[7], 1ull);
+      atomicAdd(&svs_strip_prof[8], sp_acc[8]);
     }
 #endif
     if (wave != 0) return;
@@ -1331,6 +1332,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     atomicAdd(&svs_strip_prof[5], SVS_SP_T() - sp_t0);
     atomicAdd(&svs_strip_prof[6], static_cast<unsigned long long>(rows_done));
     atomicAdd(&svs_strip_prof[7], 1ull);
+    atomicAdd(&svs_strip_prof[8], sp_acc[8]);
   }
 #endif
 }
@@ -1424,18 +1426,18 @@ __global__ void wave_scan_selftest_kernel(const int32_t* in, int32_t* out_scan, 
   out_shift[blockIdx.x * 64 + lane] = wave_shr1(x, -7, lane);
 }
 
-// SVS_STRIP_PROF builds: the counters above (out[8]); reset = 1 zeroes them.
+// SVS_STRIP_PROF builds: the counters above (out[10]); reset = 1 zeroes them.
 // Other builds report zeros.
 extern "C" int svs_debug_strip_prof(unsigned long long* out, int reset) {
 #ifdef SVS_STRIP_PROF
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(svs_strip_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return -3;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(svs_strip_prof), 10 * sizeof(unsigned long long)) != hipSuccess) return -3;
   if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(svs_strip_prof), z, sizeof(z)) != hipSuccess) return -3;
   }
 #else
   (void)reset;
-  for (int i = 0; i < 8; ++i) out[i] = 0;
+  for (int i = 0; i < 10; ++i) out[i] = 0;
 #endif
   return 0;
 }

@@ -31,12 +31,13 @@ if os.environ.get("SVS_STRIP_PROF"):
     import ctypes
     from svscope_amd import _abi
     lib = _abi.load_library()
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 10)()
     lib.svs_debug_strip_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.svs_debug_strip_prof(buf, 0)
     # poa_strip.hip SVS_STRIP_PROF: shader clocks summed over waves (ff and
     # waits nest in sweeps; the traceback is wave 0's), strip rows computed
-    names = ["wait_cyc", "ff_cyc", "sweep_cyc", "tb_cyc", "end_barrier_cyc", "life_cyc", "rows_computed", "waves"]
+    names = ["fetch_wait_cyc", "ff_cyc", "sweep_cyc", "tb_cyc", "end_barrier_cyc", "life_cyc", "rows_computed", "waves",
+             "ff_wait_cyc", "unused"]
     st["strip_prof"] = dict(zip(names, list(buf)))
 print(json.dumps(st), flush=True)
 if a.check:
