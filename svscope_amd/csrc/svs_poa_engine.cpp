@@ -748,7 +748,13 @@ size_t active_jobs_per_group() {
     const long v = std::atol(e);
     if (v > 0) return static_cast<size_t>(v);
   }
-  return 1024;  // x WPJ waves fills the 1024 SIMDs of MI355X about 4 deep
+  // 1536 tasks per group: with choose_wpj's 4 waves per job a launch holds
+  // 6144 waves, 6 per SIMD.  Fewer waves per job shorten each job's strip
+  // pipeline: at 8 waves per job a wave spends about 30 % of its life waiting
+  // for the wave sweeping the strip before it (at 4, 6 %; SVS_STRIP_PROF,
+  // profiles/r04_sp1), but a launch then needs more jobs to fill the CUs
+  // (1024 -> 1536: +1.2-1.6 % windows/s, r04_ab2, r04_ab3)
+  return 1536;
 }
 
 }  // namespace
