@@ -207,10 +207,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("SVS_BENCH_BATCH", "512")))
-    # 6 batches in flight, as localGraph_npz streams (local_graph.iter_batches):
-    # 3072 windows keep both task groups at 1536 active POA tasks (profiles/r04_ab2,
-    # r04_ab3: 4 -> 6 batches 239.5 -> 265.0 windows/s, 1024 -> 1536 active +1.2-1.6 %)
-    ap.add_argument("--depth", type=int, default=int(os.environ.get("SVS_BENCH_DEPTH", "6")),
+    # 10 batches in flight, as localGraph_npz streams (local_graph.iter_batches):
+    # 5120 windows keep both task groups near their 1792 active POA tasks
+    # (driver-shape A/B, profiles/r04_ab4..r04_ab6: 4 batches / 1024 tasks 273.7,
+    # 8 / 1536 302.5-304.6, 10 / 1792 301.4-311.1 windows/s)
+    ap.add_argument("--depth", type=int, default=int(os.environ.get("SVS_BENCH_DEPTH", "10")),
                     help="batches in flight in the streaming session")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="CPU baseline: -1 both modes, 0 off")
     ap.add_argument("--gen-procs", type=int, default=0, help="window generator processes (0: all host cores)")

@@ -748,13 +748,15 @@ size_t active_jobs_per_group() {
     const long v = std::atol(e);
     if (v > 0) return static_cast<size_t>(v);
   }
-  // 1536 tasks per group: with choose_wpj's 4 waves per job a launch holds
-  // 6144 waves, 6 per SIMD.  Fewer waves per job shorten each job's strip
-  // pipeline: at 8 waves per job a wave spends about 30 % of its life waiting
-  // for the wave sweeping the strip before it (at 4, 6 %; SVS_STRIP_PROF,
-  // profiles/r04_sp1), but a launch then needs more jobs to fill the CUs
-  // (1024 -> 1536: +1.2-1.6 % windows/s, r04_ab2, r04_ab3)
-  return 1536;
+  // 1792 tasks per group: with choose_wpj's 4 waves per job a launch holds
+  // 7168 waves, 7 per SIMD (the pruning kernel's 72-VGPR cap).  Fewer waves
+  // per job shorten each job's strip pipeline: at 8 waves per job a wave
+  // spends about 30 % of its life waiting for the wave sweeping the strip
+  // before it (at 4, 6 %; SVS_STRIP_PROF, profiles/r04_sp1), but a launch
+  // then needs more jobs to fill the CUs.  Driver-shape A/B with 10 batches in
+  // flight (profiles/r04_ab5, r04_ab6): 1536 tasks 296.8 / 297.1, 1792 tasks
+  // 301.4 / 310.2 / 311.1 windows/s; DP kernel 30.1-30.9 vs 31.7-31.9 s.
+  return 1792;
 }
 
 }  // namespace

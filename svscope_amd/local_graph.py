@@ -81,7 +81,7 @@ def _window(r):
     return (r[4], list(r[0]), np.asarray(r[1]), r[2], r[3])
 
 
-def iter_batches(rows, batch_size=512, context=None, depth=6):
+def iter_batches(rows, batch_size=512, context=None, depth=10):
     """Yields the records of each batch of ``rows``, in order, streamed through
     one DecisionSession with up to ``depth`` batches in flight (the engine's
     scheduler never drains between batches).  A window past an engine limit
