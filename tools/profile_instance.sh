@@ -1,12 +1,15 @@
 #!/bin/bash
-# Counters of the DP kernel instance that dominates the driver's timed region,
-# poa_strip_kernel<true, 8, true, unsigned short, false> (LDS pools, 8 waves per
-# job, pruning, 16-bit codes, single sweep), on the driver's shape: bench.py
+# Counters of the DP kernel instances of the driver's timed region,
+# poa_strip_kernel<true, WPJ, true, unsigned short, false> (LDS pools, WPJ waves
+# per job, pruning, 16-bit codes, single sweep) for WPJ 4, 8 and 16, on the
+# driver's shape: bench.py
 # with 512-window steps (--steps 4 --warmup 1).  Two SQ passes (8 counters
 # each) and FETCH_SIZE / WRITE_SIZE passes, each a rocprofv3 run of its own;
 # counters summed over that instance's dispatches only, and divided by the
 # cells those launches evaluated (SVS_POA_TRACE: per launch its instance and
-# cells computed).  Writes gpurun_out/NAME/{sq,pmc}_instance.json.
+# cells computed).  Writes gpurun_out/NAME/{sq,pmc}_instance.json (one entry
+# per instance; the one with the most DP time first) and pmc_dp_all.json (every
+# DP dispatch: the figure profiles/pmc_poa_traffic.json carries).
 #   tools/profile_instance.sh NAME [STEPS]
 set -o pipefail
 N=${1:?name}; STEPS=${2:-4}
@@ -24,64 +27,97 @@ run sq2 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_
 run fetch FETCH_SIZE || exit 1
 run write WRITE_SIZE || exit 1
 python3 - "$OUT" "$STEPS" <<'PY'
-import collections, csv, glob, json, re, sys
+import collections, csv, glob, json, sys
 out, steps = sys.argv[1], int(sys.argv[2])
-INST = re.compile(r"poa_strip_kernel<true, 8, true, unsigned short, false>")
 
 
-def cells(p):
-    """cells computed and launches of the instance (trace: kern g a b n wpj cells prune dual wide computed)"""
+def name(wpj):
+    """an instance, or (wpj None) every DP kernel instance"""
+    return "poa_strip_kernel<" if wpj is None else f"poa_strip_kernel<true, {wpj}, true, unsigned short, false>"
+
+
+def cells(p, wpj):
+    """cells computed and launches of an instance (trace: kern g a b n wpj cells prune dual wide computed)"""
     c = n = 0
     for line in open(f"{out}/{p}.trace"):
         f = line.split()
-        if f and f[0] == "kern" and len(f) >= 11 and int(f[1]) < 10 and f[5] == "8" and f[7] == "1" \
-                and f[8] == "0" and f[9] == "0":
+        if f and f[0] == "kern" and len(f) >= 11 and int(f[1]) < 10 and (
+                wpj is None or (f[5] == str(wpj) and f[7] == "1" and f[8] == "0" and f[9] == "0")):
             c += int(f[10])
             n += 1
     return c, n
 
 
-def counters(p):
+def counters(p, wpj):
     s = collections.defaultdict(float)
     disp = set()
     for f in glob.glob(f"{out}/{p}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            if INST.search(row["Kernel_Name"]):
+            if name(wpj) in row["Kernel_Name"]:
                 s[row["Counter_Name"]] += float(row["Counter_Value"])
                 disp.add((f, row.get("Dispatch_Id")))
     return dict(s), len(disp)
 
 
 work = f"bench.py --steps {steps} --warmup 1 --cpu-sample 0 (512-window config-3 steps, the driver's shape)"
-sq, per_row, meta = {}, {}, {}
-for p in ("sq1", "sq2"):
-    s, nd = counters(p)
-    c, nl = cells(p)
-    meta[p] = {"dispatches": nd, "launches_in_trace": nl, "cells_computed": c}
-    sq.update(s)
-    for k, v in s.items():
-        if k.startswith("SQ_INSTS"):
-            per_row[k] = v / (c / 64)
-    if "SQ_WAVE_CYCLES" in s:
-        per_row["wait_any_over_wave_cycles"] = s["SQ_WAIT_ANY"] / s["SQ_WAVE_CYCLES"]
-        per_row["active_valu_over_wave_cycles"] = s["SQ_ACTIVE_INST_VALU"] / s["SQ_WAVE_CYCLES"]
-json.dump({"kernel": "poa_strip_kernel<true, 8, true, unsigned short, false>", "workload": work,
-           "per": "64-cell strip row the instance evaluated", "per_strip_row": per_row, "counter_sums": sq,
-           "passes": meta}, open(f"{out}/sq_instance.json", "w"), indent=1)
-f, nf = counters("fetch")
-w, nw = counters("write")
-cf, _ = cells("fetch")
-cw, _ = cells("write")
-fb = f.get("FETCH_SIZE", 0.0) * 1024 * 2
-wb = w.get("WRITE_SIZE", 0.0) * 1024
-json.dump({"kernel": "poa_strip_kernel<true, 8, true, unsigned short, false>", "workload": work,
-           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; kB x 1024; FETCH_SIZE "
-                     "doubled (gfx950 under-count, MI355X_MICROARCH.md HBM section); this instance's dispatches only",
-           "fetch_bytes_per_cell": fb / cf, "fetch_bytes_per_cell_raw": fb / 2 / cf,
-           "write_bytes_per_cell": wb / cw, "hbm_bytes_per_cell": fb / cf + wb / cw,
-           "per": "DP cell the instance evaluated (cells_computed)",
-           "passes": {"FETCH_SIZE": {"dispatches": nf, "cells_computed": cf},
-                      "WRITE_SIZE": {"dispatches": nw, "cells_computed": cw}}},
-          open(f"{out}/pmc_instance.json", "w"), indent=1)
-print(json.dumps(per_row))
+sq_all, pmc_all = [], []
+for wpj in (4, 8, 16):
+    sq, per_row, meta = {}, {}, {}
+    for p in ("sq1", "sq2"):
+        s, nd = counters(p, wpj)
+        c, nl = cells(p, wpj)
+        meta[p] = {"dispatches": nd, "launches_in_trace": nl, "cells_computed": c}
+        sq.update(s)
+        for k, v in s.items():
+            if k.startswith("SQ_INSTS") and c:
+                per_row[k] = v / (c / 64)
+        if sq.get("SQ_WAVE_CYCLES"):
+            per_row["wait_any_over_wave_cycles"] = sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]
+            per_row["active_valu_over_wave_cycles"] = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
+    if not meta["sq1"]["dispatches"]:
+        continue
+    sq_all.append({"kernel": name(wpj), "workload": work, "per": "64-cell strip row the instance evaluated",
+                   "per_strip_row": per_row, "counter_sums": sq, "passes": meta})
+    f, nf = counters("fetch", wpj)
+    w, nw = counters("write", wpj)
+    cf, _ = cells("fetch", wpj)
+    cw, _ = cells("write", wpj)
+    if not (cf and cw):
+        continue
+    fb = f.get("FETCH_SIZE", 0.0) * 1024 * 2
+    wb = w.get("WRITE_SIZE", 0.0) * 1024
+    pmc_all.append({"kernel": name(wpj), "workload": work,
+                    "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; kB x 1024; FETCH_SIZE "
+                              "doubled (gfx950 under-count, MI355X_MICROARCH.md HBM section); this instance's dispatches only",
+                    "fetch_bytes_per_cell": fb / cf, "fetch_bytes_per_cell_raw": fb / 2 / cf,
+                    "write_bytes_per_cell": wb / cw, "hbm_bytes_per_cell": fb / cf + wb / cw,
+                    "per": "DP cell the instance evaluated (cells_computed)",
+                    "cells_computed": cf,
+                    "passes": {"FETCH_SIZE": {"dispatches": nf, "cells_computed": cf},
+                               "WRITE_SIZE": {"dispatches": nw, "cells_computed": cw}}})
+sq_all.sort(key=lambda e: -e["counter_sums"].get("SQ_WAVE_CYCLES", 0))
+pmc_all.sort(key=lambda e: -e["cells_computed"])
+json.dump(sq_all, open(f"{out}/sq_instance.json", "w"), indent=1)
+json.dump(pmc_all, open(f"{out}/pmc_instance.json", "w"), indent=1)
+# every DP dispatch of the run (the kernel bench.py's roofline times): the
+# traffic figure profiles/pmc_poa_traffic.json carries
+f, nf = counters("fetch", None)
+w, nw = counters("write", None)
+cf, lf = cells("fetch", None)
+cw, lw = cells("write", None)
+fb, wb = f.get("FETCH_SIZE", 0.0) * 1024 * 2, w.get("WRITE_SIZE", 0.0) * 1024
+json.dump({"kernel": "poa_strip_kernel (every instance)", "workload": work,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; kB x 1024; FETCH_SIZE doubled "
+                     "(gfx950 under-count, MI355X_MICROARCH.md HBM section); every DP dispatch of the run",
+           "fetch_bytes_per_cell": fb / cf, "fetch_bytes_per_cell_raw": fb / 2 / cf, "write_bytes_per_cell": wb / cw,
+           "hbm_bytes_per_cell": fb / cf + wb / cw, "per": "DP cell evaluated by the kernel (cells_computed)",
+           "passes": {"FETCH_SIZE": {"kB": f.get("FETCH_SIZE", 0.0), "dispatches": nf, "cells_computed": cf, "launches": lf},
+                      "WRITE_SIZE": {"kB": w.get("WRITE_SIZE", 0.0), "dispatches": nw, "cells_computed": cw,
+                                     "launches": lw}}},
+          open(f"{out}/pmc_dp_all.json", "w"), indent=1)
+print("every DP instance: HBM B/cell", round(fb / cf + wb / cw, 3))
+for e in sq_all:
+    print(e["kernel"], json.dumps(e["per_strip_row"]))
+for e in pmc_all:
+    print(e["kernel"], "HBM B/cell", round(e["hbm_bytes_per_cell"], 3))
 PY
