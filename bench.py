@@ -354,6 +354,8 @@ def main():
                           "poa_table_exports": poa.get("prep_jobs", 0),
                           "poa_kernel_ms": round(kms, 2), "poa_launches": launches,
                           "poa_dual_launches": poa.get("dual_launches", 0),
+                          "dgraph_peak_gb": round(poa.get("dgraph_peak_bytes", 0) / 2**30, 2),
+                          "dgraph_reserved_gb": round(poa.get("dgraph_reserved_bytes", 0) / 2**30, 2),
                           "gcups": round(cells_done / (kms * 1e-3) / 1e9, 3) if kms else None,
                           "gcups_full_matrix_equivalent": round(cells / (kms * 1e-3) / 1e9, 3) if kms else None,
                           "host_graph_ms": round(poa["host_graph_ms"], 1),

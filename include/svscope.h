@@ -72,6 +72,10 @@ typedef struct svs_poa_stats {
      poa_dgraph_prep_kernel */
   double fold_update_ms, fold_sort_ms, fold_final_ms, fold_prep_ms;
   uint64_t dual_launches;   /* DP launches sweeping strips in pairs */
+  /* device-resident POA graphs (the context's graph arena): the most bytes of
+     task blocks live at once, and the HBM the arena holds (hipMalloc'ed chunks;
+     never returned before svs_release) */
+  uint64_t dgraph_peak_bytes, dgraph_reserved_bytes;
 } svs_poa_stats;
 
 /* One context per host thread; owns a HIP stream and device arenas. */

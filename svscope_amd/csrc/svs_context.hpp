@@ -190,6 +190,7 @@ struct svs_context {
   hipEvent_t ev_mid = nullptr, ev_rerun = nullptr;
   svs::ThreadPool* pool = nullptr;
   size_t device_budget = 0;  // bytes usable for traceback + row pool per launch
+  size_t dgraph_budget = 0;  // limit of dgraph_arena (the device-resident POA graphs)
   // POA arenas, one per concurrently in-flight task group
   std::vector<std::unique_ptr<svs::PoaArena>> poa_arenas;
   // blocks of the device-resident POA graphs (svs_devarena.hpp)

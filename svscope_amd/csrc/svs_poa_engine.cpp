@@ -796,7 +796,7 @@ struct PoaScheduler::Impl {
       if (v > 0 && static_cast<uint64_t>(v) < kSortLdsWordsMax) sort_lds_max = static_cast<uint64_t>(v);
     }
     if (dev) {
-      if (!ctx->dgraph_arena) ctx->dgraph_arena.reset(new DevArena());
+      if (!ctx->dgraph_arena) ctx->dgraph_arena.reset(new DevArena(ctx->dgraph_budget));
       darena = ctx->dgraph_arena.get();
     }
     // Both groups' DP kernels alternate on the context's one stream (a stream
@@ -1439,6 +1439,8 @@ struct PoaScheduler::Impl {
       SVS_HIP(hipEventElapsedTime(&ms, A.evf0, A.evf1));
       SVS_HIP(hipEventElapsedTime(&pms, A.evp, A.evp1));
       st.fold_ms += ms + pms;
+      st.dgraph_peak_bytes = std::max<uint64_t>(st.dgraph_peak_bytes, darena->peak());
+      st.dgraph_reserved_bytes = darena->reserved();
       // per fold kernel: update, sort, final, then the table completion
       auto phases = [&](hipEvent_t e0, const hipEvent_t* k, hipEvent_t e1) {
         float t[4] = {0.f, 0.f, 0.f, 0.f};

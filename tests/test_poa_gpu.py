@@ -174,6 +174,8 @@ def test_pruning_stats_and_exactness(slack, retries):
         assert st["cells_computed"] < 0.6 * st["dp_cells"], st
     assert st["prep_jobs"] > 0, st  # the device completed the row tables
     assert st["fold_jobs"] > 0, st  # and folded the alignments into its graphs
+    # the graph arena's footprint is reported (DevArena accounting)
+    assert 0 < st["dgraph_peak_bytes"] <= st["dgraph_reserved_bytes"], st
 
 
 def test_wide_slot_jobs_share_pruned_launches():
