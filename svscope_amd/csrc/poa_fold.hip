@@ -992,8 +992,19 @@ __device__ __forceinline__ uint32_t seq_code(uint32_t ch) {
 // worked out on the host from the flanks, only which columns row 0 occupies
 // is known here), then FindNonSameSite (:167-179) over rows 1 .. R-1 (R0
 // MSA rows and `extra` all-gap rows), then the kept columns of rows 1 .. R-1
-// as seqdatamx.  Lane per column; the kept column indices go through `keep`
-// (task block scratch).  Returns n_feat.
+// as seqdatamx.  The kept column indices go through `keep` (task block
+// scratch).  Returns n_feat.
+//
+// The counts: a lane takes four adjacent columns (one 32-bit word per row;
+// rows are 64-B aligned) and counts A, T, C, G in packed byte counters, eight
+// rows' words loaded before any is counted so that the loads overlap (one wave
+// per window: a load per row and column chunk in turn was a chain of ~7,000
+// dependent L2 round trips per window).  Everything else is a gap for
+// FindNonSameSite (SeqEncoder's 4), so n4 = extra + (R0 - 1) - (nA+nT+nC+nG).
+__device__ __forceinline__ uint32_t zero_bytes_hi(uint32_t t) {
+  // bit 7 of each byte set iff that byte of t is zero (exact, no borrow between bytes)
+  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+}
 __device__ uint32_t msa_features(const FoldJob& J, const gu32* __restrict__ col, uint32_t ncol,
                                  const gch* __restrict__ msa, gu32* __restrict__ keep) {
   const uint32_t lane = lanei();
@@ -1018,70 +1029,140 @@ __device__ uint32_t msa_features(const FoldJob& J, const gu32* __restrict__ col,
   // row-0 columns <= lo or >= hi are in the flank pool
   const int64_t lo = m5 ? static_cast<int64_t>(uni(col[uni(paths[a0 + m5 - 1])])) : -1;
   const int64_t hi = m3 ? static_cast<int64_t>(uni(col[uni(paths[a0 + L0 - m3])])) : static_cast<int64_t>(ncol);
+  const gu32* __restrict__ m32 = reinterpret_cast<const gu32*>(msa);
+  const uint32_t sw = stride >> 2;  // words per row
   uint32_t n_feat = 0;
-  for (uint32_t c0 = 0; c0 < ncol; c0 += 64) {
-    const uint32_t c = c0 + lane;
-    bool kept = false;
-    if (c < ncol) {
-      const bool in_pool = msa[c] != '-' && (static_cast<int64_t>(c) <= lo || static_cast<int64_t>(c) >= hi);
-      if (!in_pool) {
-        // (counters in named registers: no dynamically indexed array)
-        uint32_t n0 = 0, n1 = 0, n2 = 0, n3c = 0, n4 = J.extra;
-        for (uint32_t r = 1; r < R0; ++r) {
-          const uint32_t x = seq_code(static_cast<uint8_t>(msa[static_cast<uint64_t>(r) * stride + c]));
-          n0 += x == 0u;
-          n1 += x == 1u;
-          n2 += x == 2u;
-          n3c += x == 3u;
-          n4 += x == 4u;
+  for (uint32_t c0 = 0; c0 < ncol; c0 += 256) {
+    const uint32_t cw = (c0 >> 2) + lane;  // this lane's word: columns 4 cw .. 4 cw + 3
+    const bool live = 4u * cw < ncol;
+    uint32_t nA = 0, nT = 0, nC = 0, nG = 0;  // packed byte counters (<= 255 rows between flushes)
+    uint32_t tA = 0, tT = 0, tC = 0, tG = 0;  // the same, 16-bit fields: bytes 0, 2
+    uint32_t uA = 0, uT = 0, uC = 0, uG = 0;  // bytes 1, 3
+    auto count = [&](uint32_t x) {
+      const uint32_t u = x & 0xDFDFDFDFu;  // upper case
+      nA += zero_bytes_hi(u ^ 0x41414141u) >> 7;
+      nT += zero_bytes_hi(u ^ 0x54545454u) >> 7;
+      nC += zero_bytes_hi(u ^ 0x43434343u) >> 7;
+      nG += zero_bytes_hi(u ^ 0x47474747u) >> 7;
+    };
+    auto flush = [&]() {
+      tA += nA & 0x00FF00FFu; uA += (nA >> 8) & 0x00FF00FFu; nA = 0;
+      tT += nT & 0x00FF00FFu; uT += (nT >> 8) & 0x00FF00FFu; nT = 0;
+      tC += nC & 0x00FF00FFu; uC += (nC >> 8) & 0x00FF00FFu; nC = 0;
+      tG += nG & 0x00FF00FFu; uG += (nG >> 8) & 0x00FF00FFu; nG = 0;
+    };
+    uint32_t x0 = 0;
+    if (live) {
+      x0 = m32[cw];
+      uint32_t r = 1, blk = 0;
+      for (; r + 8 <= R0; r += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = m32[static_cast<uint64_t>(r + i) * sw + cw];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) count(x[i]);
+        if ((blk += 8) >= 248u) {
+          flush();
+          blk = 0;
         }
-        // second-largest count (sorted(counts)[3])
-        uint32_t m1 = 0, m2 = 0;
-        for (const uint32_t v : {n0, n1, n2, n3c, n4}) {
-          m2 = v > m1 ? m1 : max(m2, v);
-          m1 = max(m1, v);
-        }
-        kept = m2 >= J.cut;
       }
+      for (; r < R0; ++r) count(m32[static_cast<uint64_t>(r) * sw + cw]);
+      flush();
     }
-    const uint64_t km = ballot(kept);
-    if (kept) keep[n_feat + popc64(km & below())] = c;
-    n_feat += popc64(km);
+    // 16-bit fields: rows < 65536 (the host keeps windows far below that)
+    uint32_t kbits = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b) {
+      const uint32_t c = 4u * cw + b;
+      if (c >= ncol) continue;
+      const bool in_pool = ((x0 >> (8 * b)) & 0xFFu) != '-' &&
+                           (static_cast<int64_t>(c) <= lo || static_cast<int64_t>(c) >= hi);
+      if (in_pool) continue;
+      const uint32_t sh = 16 * (b >> 1);
+      auto field = [&](uint32_t even, uint32_t odd) { return (((b & 1u) ? odd : even) >> sh) & 0xFFFFu; };
+      const uint32_t n0 = field(tA, uA), n1 = field(tT, uT), n2 = field(tC, uC), n3c = field(tG, uG);
+      const uint32_t n4 = J.extra + (R0 - 1) - (n0 + n1 + n2 + n3c);
+      // second-largest count (sorted(counts)[3])
+      uint32_t m1 = 0, m2 = 0;
+      for (const uint32_t v : {n0, n1, n2, n3c, n4}) {
+        m2 = v > m1 ? m1 : max(m2, v);
+        m1 = max(m1, v);
+      }
+      if (m2 >= J.cut) kbits |= 1u << b;
+    }
+    // kept columns in column order: lane-major, then within the lane's word
+    const uint32_t kc = __builtin_popcount(kbits);
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (uint32_t bit = 0; bit < 3; ++bit) {
+      const uint64_t m = ballot((kc >> bit) & 1u);
+      off += popc64(m & below()) << bit;
+      tot += popc64(m) << bit;
+    }
+    uint32_t o = n_feat + off;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b)
+      if ((kbits >> b) & 1u) keep[o++] = 4u * cw + b;
+    n_feat += tot;
   }
   wave_sync_mem();
-  // seqdatamx: rows 1 .. R0-1 of the MSA, then `extra` all-gap rows
+  // seqdatamx: rows 1 .. R0-1 of the MSA, then `extra` all-gap rows; eight
+  // rows' gathers in flight at a time
   gu8* out = glb(J.feat_out);
   const uint32_t rows = R0 - 1 + J.extra;
   for (uint32_t k0 = 0; k0 < n_feat; k0 += 64) {
     const uint32_t k = k0 + lane;
-    const uint32_t c = k < n_feat ? keep[k] : 0u;
-    for (uint32_t r = 1; r < R0; ++r) {
-      if (k < n_feat)
+    if (k < n_feat) {
+      const uint32_t c = keep[k];
+      uint32_t r = 1;
+      for (; r + 8 <= R0; r += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = static_cast<uint8_t>(msa[static_cast<uint64_t>(r + i) * stride + c]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) out[static_cast<uint64_t>(r + i - 1) * n_feat + k] = static_cast<uint8_t>(seq_code(x[i]));
+      }
+      for (; r < R0; ++r)
         out[static_cast<uint64_t>(r - 1) * n_feat + k] =
             static_cast<uint8_t>(seq_code(static_cast<uint8_t>(msa[static_cast<uint64_t>(r) * stride + c])));
+      for (r = R0 - 1; r < rows; ++r) out[static_cast<uint64_t>(r) * n_feat + k] = 4u;
     }
-    for (uint32_t r = R0 - 1; r < rows; ++r)
-      if (k < n_feat) out[static_cast<uint64_t>(r) * n_feat + k] = 4u;
   }
   return n_feat;
 }
 
-// MSA rows: every sequence's path nodes at their columns, '-' elsewhere.
+// MSA rows: every sequence's path nodes at their columns, '-' elsewhere.  The
+// rows (stride and start 64-B aligned, stride >= ncol rounded up to 16) are
+// filled with 16-B stores, then each path's nodes are placed eight 64-node
+// chunks at a time (their node, column and letter loads all in flight before
+// the stores).
 __device__ void msa_rows(uint32_t n_paths, const gu32* __restrict__ paths, const gu32* __restrict__ path_off,
                          const gu32* __restrict__ colv, const gu8* __restrict__ base, uint32_t ncol,
                          gch* __restrict__ out, uint32_t stride) {
   const uint32_t lane = lanei();
+  const uint32_t w16 = (ncol + 15u) >> 4;
+  const u32x4 dash = {0x2D2D2D2Du, 0x2D2D2D2Du, 0x2D2D2D2Du, 0x2D2D2D2Du};
   for (uint32_t s = 0; s < n_paths; ++s) {
-    gch* row = out + static_cast<uint64_t>(s) * stride;
-    for (uint32_t c = lane; c < ncol; c += 64) row[c] = '-';
+    GLB u32x4* row = reinterpret_cast<GLB u32x4*>(out + static_cast<uint64_t>(s) * stride);
+    for (uint32_t c = lane; c < w16; c += 64) row[c] = dash;
   }
   wave_sync_mem();
+  constexpr uint32_t kU = 8;
   for (uint32_t s = 0; s < n_paths; ++s) {
     gch* row = out + static_cast<uint64_t>(s) * stride;
     const uint32_t a = path_off[s], b = path_off[s + 1];
-    for (uint32_t k = a + lane; k < b; k += 64) {
-      const uint32_t node = paths[k];
-      row[colv[node]] = static_cast<char>(base[node]);
+    for (uint32_t k = a + lane; k < b; k += 64 * kU) {
+      uint32_t nd[kU], cc[kU], bb[kU];
+#pragma unroll
+      for (uint32_t i = 0; i < kU; ++i) nd[i] = k + 64 * i < b ? paths[k + 64 * i] : 0u;
+#pragma unroll
+      for (uint32_t i = 0; i < kU; ++i) {
+        cc[i] = colv[nd[i]];
+        bb[i] = base[nd[i]];
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < kU; ++i)
+        if (k + 64 * i < b) row[cc[i]] = static_cast<char>(bb[i]);
     }
   }
 }

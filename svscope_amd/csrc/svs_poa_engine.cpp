@@ -1452,6 +1452,12 @@ struct PoaScheduler::Impl {
         st.fold_sort_ms += t[1];
         st.fold_final_ms += t[2];
         st.fold_prep_ms += t[3];
+        if (g_trace.f) {
+          size_t n_final = 0;
+          for (const FoldJob& F : D.folds) n_final += (F.flags & kFoldFinal) ? 1 : 0;
+          std::fprintf(g_trace.f, "fph %d %.3f %.3f %.3f %.3f %zu\n", (e0 == A.evf0 ? 10 : 20) + gid(g), t[0], t[1], t[2],
+                       t[3], n_final);
+        }
       };
       if (nj) phases(A.evf0, A.evk, A.evf1);
       if (D.n_pre) phases(A.evp, A.evpk, A.evp1);
