@@ -101,9 +101,12 @@ int svs_init(int device_ordinal, svs_context** out) {
       if (gb > 0) budget = static_cast<size_t>(gb * (1ull << 30));
     }
     ctx->device_budget = std::max<size_t>(budget, 64ull << 20);
-    // the device-resident POA graphs get what the launch budget leaves of the
-    // free HBM, less 4 GiB for the EM and MisScore buffers and HIP itself
-    const size_t rest = free_b > ctx->device_budget + (4ull << 30) ? free_b - ctx->device_budget - (4ull << 30) : 0;
+    // the device-resident POA graphs get what the launch buffers leave of the
+    // free HBM (the traceback budget, and the carry buffers sized at an eighth
+    // of it, svs_poa_engine.cpp), less 4 GiB for the EM and MisScore buffers
+    // and HIP itself
+    const size_t used = ctx->device_budget + ctx->device_budget / 8 + (4ull << 30);
+    const size_t rest = free_b > used ? free_b - used : 0;
     ctx->dgraph_budget = std::max<size_t>(rest, 1ull << 30);
     ctx->pool = new svs::ThreadPool(host_threads());
   });

@@ -31,15 +31,19 @@ struct SvsError : std::runtime_error {
 
 // Growable device buffer (never shrinks; contents not preserved on growth).
 // Growth is geometric (at least doubling), and `hint` (e.g. the launch budget)
-// is tried first: a regrow frees the old buffer, and hipFree waits for the whole
-// device, so a buffer that regrows during a run stalls the pipeline (a 4-s stall
-// in a traced bench run, profiles/r02_v11).
+// is tried first.  hipFree waits for the whole device, so a buffer that
+// regrows during a run would stall the pipeline (a 4-s stall in a traced bench
+// run, profiles/r02_v11; host pack phases of 20-60 ms behind the other group's
+// DP kernel in round 4, profiles/r04_g8): the old buffer is retired instead
+// and freed with the buffer (release), when the device is idle anyway.
+// Retired buffers of geometric growth add at most the final size again.
 struct DeviceBuf {
   void* ptr = nullptr;
   size_t cap = 0;
+  std::vector<void*> retired;
   void ensure(size_t bytes, size_t hint = 0) {
     if (bytes <= cap) return;
-    if (ptr) SVS_HIP(hipFree(ptr));
+    if (ptr) retired.push_back(ptr);
     ptr = nullptr;
     const size_t grown = std::max(bytes + bytes / 4 + 4096, 2 * cap);
     cap = 0;
@@ -63,19 +67,23 @@ struct DeviceBuf {
   template <class T> T* as() const { return static_cast<T*>(ptr); }
   void release() {
     if (ptr) (void)hipFree(ptr);
+    for (void* r : retired) (void)hipFree(r);
+    retired.clear();
     ptr = nullptr;
     cap = 0;
   }
 };
 
-// Growable pinned host buffer.
+// Growable pinned host buffer; a regrow retires the old buffer like DeviceBuf
+// (hipHostFree synchronises too).
 struct PinnedBuf {
   void* ptr = nullptr;
   size_t cap = 0;
   unsigned flags = hipHostMallocDefault;  // hipHostMallocMapped: kernels write it (hipHostGetDevicePointer)
+  std::vector<void*> retired;
   void ensure(size_t bytes) {
     if (bytes <= cap) return;
-    if (ptr) SVS_HIP(hipHostFree(ptr));
+    if (ptr) retired.push_back(ptr);
     ptr = nullptr;
     const size_t want = std::max(bytes + bytes / 4 + 4096, 2 * cap);  // geometric: few regrows
     cap = 0;
@@ -90,13 +98,15 @@ struct PinnedBuf {
     void* p = nullptr;
     SVS_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
     if (old && keep) std::memcpy(p, old, std::min(keep, cap));
-    if (old) SVS_HIP(hipHostFree(old));
+    if (old) retired.push_back(old);
     ptr = p;
     cap = want;
   }
   template <class T> T* as() const { return static_cast<T*>(ptr); }
   void release() {
     if (ptr) (void)hipHostFree(ptr);
+    for (void* r : retired) (void)hipHostFree(r);
+    retired.clear();
     ptr = nullptr;
     cap = 0;
   }

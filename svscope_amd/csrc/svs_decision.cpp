@@ -176,12 +176,16 @@ class Pipeline {
     b.cons_left.assign(b.n, 0);
     b.left = b.n;
     const uint32_t prio = static_cast<uint32_t>(b.ticket);
-    for (int32_t w = 0; w < b.n; ++w) {
+    // the windows' tasks are built on the pool (a batch's reads are ~100 MB of
+    // copies and letter checks: 30-60 ms on this thread, which also drives the
+    // POA launches, profiles/r04_g8), then queued in window order
+    std::vector<PoaTask> built(static_cast<size_t>(b.n));
+    ctx->pool->parallel_for(static_cast<size_t>(b.n), [&](size_t wi) {
+      const int32_t w = static_cast<int32_t>(wi);
       const svs_decision_window& W = b.wins[w];
-      PoaTask t;
+      PoaTask& t = built[wi];
       t.genmsa = true;
       t.prio = prio;
-      t.tag = new_ref(TaskRef{&b, w, -1});
       for (int32_t k = 0; k < W.n_seqs; ++k) {
         const int64_t x = b.seq_byte_start[W.seq_start + k], y = b.seq_byte_start[W.seq_start + k + 1];
         // (ranges checked on submit, check_decision_windows)
@@ -199,7 +203,10 @@ class Pipeline {
       } catch (const SvsError&) {
         t.feat_params.ok = false;
       }
-      sched.add(std::move(t));
+    });
+    for (int32_t w = 0; w < b.n; ++w) {
+      built[w].tag = new_ref(TaskRef{&b, w, -1});
+      sched.add(std::move(built[w]));
     }
     st.msa_tasks += b.n;
     msa_outstanding += static_cast<size_t>(b.n);
@@ -259,10 +266,10 @@ class Pipeline {
       st.em_flops += 410.0 * f.rows * f.n_feat * kk * (kk + 1) / 2;
     }
     std::vector<uint8_t> X(static_cast<size_t>(std::max<int64_t>(1, xoff)));
-    for (size_t i = 0; i < e->windows.size(); ++i) {
+    ctx->pool->parallel_for(e->windows.size(), [&](size_t i) {
       const WindowFeatures& f = e->windows[i].b->feats[e->windows[i].w];
       if (!f.feat.empty()) std::memcpy(X.data() + ew[i].x_off, f.feat.data(), f.feat.size());
-    }
+    });
     svs_context* c = ctx;
     svs_decision_session* s = S;
     const svs_em_config ec = ecfg;

@@ -1163,9 +1163,12 @@ struct PoaScheduler::Impl {
     D.wide = wide;
     st.wide_launches += wide ? 1 : 0;
     st.dual_launches += (dual && nj) ? 1 : 0;
+    // (hints: the carries are 16 B per 64 traceback codes, the pairs 8 B per
+    // row and read base; sized once for the group's budget instead of growing
+    // with the graphs)
     A.d_tb.ensure(n_tb * (wide ? 4 : 2) + 4096, ctx->device_budget / 2);
-    A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096);
-    A.d_aln.ensure(n_aln * 8 + 64);
+    A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096, ctx->device_budget / 16);
+    A.d_aln.ensure(n_aln * 8 + 64, 256ull << 20);
     A.d_alen.ensure(nj * 12 + 64);
     // fold jobs, growing blocks that could not hold this fold
     D.folds.assign(nf, FoldJob{});

@@ -8,7 +8,10 @@ the new tasks' chains (kern 20+g).  For each DP launch this script takes the
 latest of those ends as what the launch waited for, and sums the DP stream's
 idle time by cause.  Also prints the mean length of each stage of the loop.
 
-  python tools/dp_gaps.py trace.txt
+  python tools/dp_gaps.py trace.txt [TAIL_MS]
+
+TAIL_MS: only the DP launches of the trace's last TAIL_MS (bench.py's timed
+steps come after its warm-up batches in the same session).
 """
 import collections
 import json
@@ -34,15 +37,17 @@ def runs(path):
         yield cur
 
 
-def analyse(r):
+def analyse(r, tail_ms=None):
     dp = sorted([k for k in r["kern"] if k[0] < 10], key=lambda k: k[1])
+    if tail_ms:
+        dp = [k for k in dp if k[1] >= dp[-1][2] - tail_ms]
     if len(dp) < 3:
         return None
     by = collections.defaultdict(list)  # (kind, group) -> [(t0, t1)], kinds: fold chain, pre chain, host phases
     for g, a, b in r["kern"]:
         if 10 <= g < 20:
             by[("chain", g - 10)].append((a, b))
-        elif g >= 20:
+        elif 20 <= g < 30:
             by[("pre", g - 20)].append((a, b))
     for name, g, a, b in r["host"]:
         by[(name, g)].append((a, b))
@@ -80,14 +85,22 @@ def analyse(r):
                 if ph:
                     stage[kind + "_ms"].append(sum(b - a for a, b in ph))
         prev_end_g[g] = e
+    # host phases of the scheduler thread (a long one holds up both groups)
+    host = {}
+    for name in sorted({h[0] for h in r["host"]}):
+        d = [b - a for n, _, a, b in r["host"] if n == name]
+        host[name] = {"n": len(d), "total_ms": round(sum(d), 1), "over_10ms": sum(1 for x in d if x > 10),
+                      "over_10ms_total_ms": round(sum(x for x in d if x > 10), 1)}
     span = dp[-1][2] - dp[0][1]
     busy = sum(e - s for _, s, e in dp)
     return {"dp_launches": len(dp), "span_ms": round(span, 1), "dp_busy_frac": round(busy / span, 4),
             "dp_idle_ms_by_cause": {k: round(v, 1) for k, v in idle.most_common()},
             "mean_dp_ms": round(busy / len(dp), 2),
-            "loop_stage_means_ms": {k: round(sum(v) / len(v), 2) for k, v in stage.items() if v}}
+            "loop_stage_means_ms": {k: round(sum(v) / len(v), 2) for k, v in stage.items() if v},
+            "host_phases": host}
 
 
 if __name__ == "__main__":
-    out = [a for a in (analyse(r) for r in runs(sys.argv[1])) if a]
+    tail = float(sys.argv[2]) if len(sys.argv) > 2 else None
+    out = [a for a in (analyse(r, tail) for r in runs(sys.argv[1])) if a]
     print(json.dumps(out[-1] if len(out) == 1 else out, indent=1))
