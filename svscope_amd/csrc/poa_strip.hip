@@ -46,6 +46,18 @@ namespace {
 // prefetched for a later row as well.
 #define GLB __attribute__((address_space(1)))
 template <class T> __device__ __forceinline__ const GLB T* glb(const T* p) { return (const GLB T*)(p); }
+// The job's row tables (records, in-edges, column 0) are written by earlier
+// kernels and only read here: through the constant address space, a load at a
+// wave-uniform address is a scalar load straight into SGPRs (no vector load,
+// no v_readfirstlane per word), which the compiler cannot prove for pointers
+// it reads from the job descriptor.  SVS_TABLES_GLOBAL=1 (development builds)
+// keeps them global.
+#ifndef SVS_TABLES_GLOBAL
+#define TBL __attribute__((address_space(4)))
+#else
+#define TBL GLB
+#endif
+template <class T> __device__ __forceinline__ const TBL T* tbl(const T* p) { return (const TBL T*)(p); }
 
 // One pool slot: 65 int32 Hx = H at columns j0-1 .. j0+63 (so a successor
 // reads H[j] at Hx[l+1] and its diagonal H[j-1] at Hx[l], with no lane shift),
@@ -154,7 +166,7 @@ struct RowIn {
   int32_t b0, b1, b2, b3;
 };
 
-__device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, const GLB uint32_t* __restrict__ spill) {
+__device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, const TBL uint32_t* __restrict__ spill) {
   if (k >= kInlinePreds) return spill[k];
   return (d.w1 >> (16 * k)) & 0xFFFFu;
 }
@@ -270,11 +282,11 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * kStride;
   else pool = gpool + J.pool_off + static_cast<uint64_t>(wave) * ((nslot * kSlotInts + 63) / 64 * 64);
   CodeT* __restrict__ tbj = tb + J.tb_off;
-  const GLB uint32_t* __restrict__ rec = glb(J.rec);
-  const GLB uint32_t* __restrict__ rps = glb(J.pstart);
-  const GLB uint32_t* __restrict__ prow = glb(J.pred);
-  const GLB uint32_t* __restrict__ pslot = glb(J.pslot);
-  const GLB int32_t* __restrict__ rc0 = glb(J.col0);
+  const TBL uint32_t* __restrict__ rec = tbl(J.rec);
+  const TBL uint32_t* __restrict__ rps = tbl(J.pstart);
+  const TBL uint32_t* __restrict__ prow = tbl(J.pred);
+  const TBL uint32_t* __restrict__ pslot = tbl(J.pslot);
+  const TBL int32_t* __restrict__ rc0 = tbl(J.col0);
   const GLB uint8_t* __restrict__ seq = glb(J.seq);
   int32_t* __restrict__ bnd = bnd_all + J.bnd_off;
   // The same carry buffer, read-only: loads through it are uniform and never
@@ -381,7 +393,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     auto fetch = [&](RowIn& d, uint32_t r) {
       const uint32_t rr = r < V ? r : V - 1;
       // 32-bit byte offsets off the job's bases (a job has < 2^28 rows)
-      const GLB uint32_t* w = rec + (rr << 2);
+      const TBL uint32_t* w = rec + (rr << 2);
       d.w0 = w[0];
       d.w1 = w[1];
       if constexpr (PRUNE) {
@@ -447,7 +459,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
           const uint32_t wp = __builtin_amdgcn_readfirstlane(d.w1);
           live = slot_alive(wp & 0xFFFFu) || (np >= 2 && slot_alive(wp >> 16));
           if (!live && np > kInlinePreds) {
-            const GLB uint32_t* __restrict__ spill = pslot + rps[r];
+            const TBL uint32_t* __restrict__ spill = pslot + rps[r];
             for (uint32_t k = kInlinePreds; k < np && !live; ++k)
               live = slot_alive(__builtin_amdgcn_readfirstlane(spill[k]));
           }
@@ -590,7 +602,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         code |= lbit ? 1u << TF::kLBit : 0u;
         code |= ((va || (!vb && vc)) ? 1u << TF::kStop : 0u) | (ch0 ? 0u : (1u << TF::kUc));
       } else {
-        const GLB uint32_t* __restrict__ spill = pslot + rps[r];
+        const TBL uint32_t* __restrict__ spill = pslot + rps[r];
         F = SVS_VNEG;
         O = SVS_VNEG;
         int32_t Hd = SVS_VNEG;
@@ -832,7 +844,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
 
     auto fetch = [&](RowIn& d, uint32_t r) {
       const uint32_t rr = r < V ? r : V - 1;
-      const GLB uint32_t* w = rec + (rr << 2);
+      const TBL uint32_t* w = rec + (rr << 2);
       d.w0 = w[0];
       d.w1 = w[1];
       if constexpr (PRUNE) {
@@ -877,7 +889,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         bool la = cH_in > SVS_VNEG / 2 || sa(alive_a, s0) || (np >= 2 && sa(alive_a, s1));
         bool lbv = sa(alive_b, s0) || (np >= 2 && sa(alive_b, s1));
         if (np > kInlinePreds && !(la && lbv)) {
-          const GLB uint32_t* __restrict__ spill = pslot + rps[r];
+          const TBL uint32_t* __restrict__ spill = pslot + rps[r];
           for (uint32_t k = kInlinePreds; k < np && !(la && lbv); ++k) {
             const uint32_t ps = __builtin_amdgcn_readfirstlane(spill[k]);
             la = la || sa(alive_a, ps);
@@ -1034,7 +1046,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         code_a = code2(ga, Fa, Oa, a0h, a0f, a0o, a0m, a1h, a1f, a1o, a1m, mca);
         code_b = code2(gb, Fb, Ob, b0h, b0f, b0o, b0m, b1h, b1f, b1o, b1m, mcb);
       } else {
-        const GLB uint32_t* __restrict__ spill = pslot + rps[r];
+        const TBL uint32_t* __restrict__ spill = pslot + rps[r];
         Fa = Oa = Fb = Ob = SVS_VNEG;
         int32_t Hda = SVS_VNEG, Hdb = SVS_VNEG;
         for (uint32_t k = 0; k < np; ++k) {
