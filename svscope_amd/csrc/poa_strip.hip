@@ -726,6 +726,30 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     };
     auto dead_strip = [&]() { return (alive & ~1u) == 0; };
 
+#ifndef SVS_TWO_SETS
+    // One prefetch set, refilled for the next row as soon as a row is done.
+    // The row tables and carries are scalar loads, and a scalar load is only
+    // waited for with lgkmcnt(0), which waits for every scalar load (they
+    // return out of order) and LDS operation in flight: a second set loaded a
+    // row further ahead was waited for at the next row's start all the same,
+    // and its 8 SGPRs pushed more live values into spill lanes.
+    RowIn A;
+    uint32_t r = 0;
+    if (prune) SVS_SP(1, r = fast_forward(0));
+    pub_left = 8u - (r & 7u);
+    fetch(A, r);
+    while (r < V) {
+      step(r, A);
+      if (prune && dead_strip()) {
+        SVS_SP(1, r = fast_forward(r + 1));
+        pub_left = 8u - (r & 7u);
+        fetch(A, r);
+        continue;
+      }
+      ++r;
+      fetch(A, r);
+    }
+#else
     // rows in pairs with two statically named prefetch sets (no waits on
     // loads still in flight when a set is refilled)
     RowIn A, B;
@@ -756,6 +780,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       fetch(B, r + 3);
       r += 2;
     }
+#endif
     // the strip's last rows (V not a multiple of 8): every carry is stored
     if (WPJ > 1 && write_bnd && lane == 0)
       __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(V), __ATOMIC_RELEASE,
