@@ -95,7 +95,13 @@ int svs_init(int device_ordinal, svs_context** out) {
     SVS_HIP(hipEventCreate(&ctx->ev_rerun));
     size_t free_b = 0, total_b = 0;
     SVS_HIP(hipMemGetInfo(&free_b, &total_b));
-    size_t budget = free_b / 2;
+    // the launches' traceback codes and carries: 5/8 of the free HBM (180 GB
+    // of an MI355X), so that a group's launch holds 2048 config-3 alignments
+    // (about 40 MB of codes each at the end of a window MSA); the graph arena
+    // gets the rest less the carries and 4 GiB (below).  Driver-shape A/B,
+    // profiles/r04_h9: 352.5 / 350.9 windows/s at 180 GB and 2048 tasks per
+    // group against 334 at half the free HBM and 1792
+    size_t budget = free_b / 8 * 5;
     if (const char* s = std::getenv("SVS_DEVICE_BUDGET_GB")) {
       const double gb = std::atof(s);
       if (gb > 0) budget = static_cast<size_t>(gb * (1ull << 30));

@@ -36,14 +36,20 @@ struct SvsError : std::runtime_error {
 // run, profiles/r02_v11; host pack phases of 20-60 ms behind the other group's
 // DP kernel in round 4, profiles/r04_g8): the old buffer is retired instead
 // and freed with the buffer (release), when the device is idle anyway.
-// Retired buffers of geometric growth add at most the final size again.
+// Retired buffers of geometric growth add at most the final size again; a
+// buffer of 1 GiB or more (the traceback and carry buffers, sized once from
+// the budget) is freed at once instead, so that its rare regrow cannot hold
+// twice its size.
 struct DeviceBuf {
   void* ptr = nullptr;
   size_t cap = 0;
   std::vector<void*> retired;
   void ensure(size_t bytes, size_t hint = 0) {
     if (bytes <= cap) return;
-    if (ptr) retired.push_back(ptr);
+    if (ptr) {
+      if (cap >= (size_t(1) << 30)) SVS_HIP(hipFree(ptr));
+      else retired.push_back(ptr);
+    }
     ptr = nullptr;
     const size_t grown = std::max(bytes + bytes / 4 + 4096, 2 * cap);
     cap = 0;
@@ -83,7 +89,10 @@ struct PinnedBuf {
   std::vector<void*> retired;
   void ensure(size_t bytes) {
     if (bytes <= cap) return;
-    if (ptr) retired.push_back(ptr);
+    if (ptr) {
+      if (cap >= (size_t(256) << 20)) SVS_HIP(hipHostFree(ptr));
+      else retired.push_back(ptr);
+    }
     ptr = nullptr;
     const size_t want = std::max(bytes + bytes / 4 + 4096, 2 * cap);  // geometric: few regrows
     cap = 0;

@@ -748,15 +748,20 @@ size_t active_jobs_per_group() {
     const long v = std::atol(e);
     if (v > 0) return static_cast<size_t>(v);
   }
-  // 1792 tasks per group: with choose_wpj's 4 waves per job a launch holds
-  // 7168 waves, 7 per SIMD (the pruning kernel's 72-VGPR cap).  Fewer waves
-  // per job shorten each job's strip pipeline: at 8 waves per job a wave
-  // spends about 30 % of its life waiting for the wave sweeping the strip
-  // before it (at 4, 6 %; SVS_STRIP_PROF, profiles/r04_sp1), but a launch
-  // then needs more jobs to fill the CUs.  Driver-shape A/B with 10 batches in
-  // flight (profiles/r04_ab5, r04_ab6): 1536 tasks 296.8 / 297.1, 1792 tasks
-  // 301.4 / 310.2 / 311.1 windows/s; DP kernel 30.1-30.9 vs 31.7-31.9 s.
-  return 1792;
+  // 2048 tasks per group: with choose_wpj's 4 waves per job a launch holds
+  // 8192 waves, more than the 7168 resident at 7 per SIMD (the pruning
+  // kernel's 72-VGPR cap), so jobs that end early make room for the rest.
+  // Fewer waves per job shorten each job's strip pipeline: at 8 waves per job
+  // a wave spends about 30 % of its life waiting for the wave sweeping the
+  // strip before it (at 4, 6 %; SVS_STRIP_PROF, profiles/r04_sp1), but a
+  // launch then needs more jobs to fill the CUs.  Driver-shape A/B with 10
+  // batches in flight: 1536 tasks 296.8 / 297.1, 1792 tasks 301.4 / 310.2 /
+  // 311.1 windows/s (profiles/r04_ab5, r04_ab6); after the round-4 DP kernel
+  // changes and with the traceback budget at 5/8 of HBM (svs_abi.cpp), 1920
+  // 345.1, 2048 352.5 / 350.9, 2176 348.7 (profiles/r04_h9); at half of HBM,
+  // 2048 tasks overran the budget and launched in smaller pieces half the
+  // time (331.7 / 343.3, r04_h6).
+  return 2048;
 }
 
 }  // namespace
