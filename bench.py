@@ -211,11 +211,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("SVS_BENCH_BATCH", "512")))
-    # 10 batches in flight, as localGraph_npz streams (local_graph.iter_batches):
-    # 5120 windows keep both task groups near their 1792 active POA tasks
+    # 14 batches in flight, as localGraph_npz streams (local_graph.iter_batches):
+    # 7168 windows keep both task groups at their 2048 active POA tasks
     # (driver-shape A/B, profiles/r04_ab4..r04_ab6: 4 batches / 1024 tasks 273.7,
-    # 8 / 1536 302.5-304.6, 10 / 1792 301.4-311.1 windows/s)
-    ap.add_argument("--depth", type=int, default=int(os.environ.get("SVS_BENCH_DEPTH", "10")),
+    # 8 / 1536 302.5-304.6, 10 / 1792 301.4-311.1 windows/s; with 2048 tasks,
+    # profiles/r04_i2, r04_i3: 10 batches 351.2, 12 354.5-357.2, 14
+    # 359.2-360.6, 16 358.6, 20 358.4)
+    ap.add_argument("--depth", type=int, default=int(os.environ.get("SVS_BENCH_DEPTH", "14")),
                     help="batches in flight in the streaming session")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="CPU baseline: -1 both modes, 0 off")
     ap.add_argument("--gen-procs", type=int, default=0, help="window generator processes (0: all host cores)")

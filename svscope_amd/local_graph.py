@@ -81,10 +81,11 @@ def _window(r):
     return (r[4], list(r[0]), np.asarray(r[1]), r[2], r[3])
 
 
-def iter_batches(rows, batch_size=512, context=None, depth=10):
+def iter_batches(rows, batch_size=512, context=None, depth=14):
     """Yields the records of each batch of ``rows``, in order, streamed through
     one DecisionSession with up to ``depth`` batches in flight (the engine's
-    scheduler never drains between batches).  A window past an engine limit
+    scheduler never drains between batches; 14 x 512 windows keep both task
+    groups at their 2048 active POA tasks, bench.py --depth).  A window past an engine limit
     (decision_maker.WindowFailed) yields None in its place; the others run on,
     and once every batch is done a WindowFailed names all such windows (row
     indices into ``rows``)."""
