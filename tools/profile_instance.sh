@@ -16,6 +16,11 @@ N=${1:?name}; STEPS=${2:-4}
 OUT=gpurun_out/$N
 mkdir -p $OUT
 export TMPDIR=/tmp
+# a counter pass serialises the kernels and prints nothing until it ends: a
+# heartbeat under gpurun_out/ keeps the box from taking it for a hang
+(while sleep 50; do date >> $OUT/heartbeat; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 run() {  # pass name, counters...
   local p=$1; shift
   rm -f $OUT/$p.trace
