@@ -173,6 +173,23 @@ __device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, con
 
 }  // namespace
 
+// Publishing a wave's carry progress.  The consumer reads the carries with
+// scalar loads (bndr below), and those reach L2 beside the vector path: the
+// workgroup-scope release of the progress store orders this wave's carry
+// stores only for vector loads of the same CU (it emits no vmcnt wait), so a
+// scalar load issued right after the consumer sees the progress could reach
+// L2 before the store and cache a stale line (seen as a rare misalignment on
+// a one-row graph, where the consumer spins on the strip's only line).
+// Every publication therefore waits for this wave's vector memory
+// operations first (tests/test_poa_gpu.py::test_short_graph_strip_handoff:
+// 2-19 of 1500 one-row-graph alignments per kernel instance moved without
+// it, profiles/r04_j4).  It costs nothing measurable (MSA probe kernel time
+// 2714 vs 2728 ms without it); deferring the publication by a row or more so
+// that the wait finds the stores landed costs 3 %: consumers wait on the
+// line boundary.  gfx9 s_waitcnt field layout: vmcnt [3:0] and [15:14],
+// expcnt [6:4], lgkmcnt [11:8]; this is vmcnt(0) with the others at maximum.
+__device__ __forceinline__ void wait_vm_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 
 // Bounded LDS-flag wait (workgroup scope); sets *err after kStripSpinLimit polls.
 // Nap schedule of the progress polls: the first SVS_POLL_N polls sleep
@@ -294,7 +311,8 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   // scalar-cache loads.  Safe because every carry line is written once per
   // launch, by whole 128-B lines (strip blocks padded to 8 rows), and read only
   // after its producer has finished the line (progress is published at
-  // multiples of 8 rows after a release) and drained its stores.
+  // multiples of 8 rows) and waited for its stores to land (wait_vm_stores:
+  // the release alone does not order them for scalar loads).
   const GLB int32_t* __restrict__ bndr = glb(bnd_rd) + J.bnd_off;
 
   int32_t best = SVS_NEG_INF;  // meaningful on the lane owning column L
@@ -441,6 +459,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
           pub_left = 8;
           // every lane stores the same value: no exec-mask branch, and the
           // countdown stays a scalar
+          wait_vm_stores();
           __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(r) + 1,
                              __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -717,10 +736,13 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       }
       pH = pF = pO = pHm = SVS_VNEG;
       // carries of every row before r are stored: publish whole 8-row lines
-      if (WPJ > 1 && write_bnd && lane == 0) {
-        const uint32_t done = r >= V ? V : (r & ~7u);
-        __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(done),
-                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (WPJ > 1 && write_bnd) {
+        wait_vm_stores();
+        if (lane == 0) {
+          const uint32_t done = r >= V ? V : (r & ~7u);
+          __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(done),
+                             __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
       return r;
     };
@@ -781,12 +803,13 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       r += 2;
     }
 #endif
-    // the strip's last rows (V not a multiple of 8): every carry is stored
+    // this strip's boundary stores must land before the next strip reads
+    // them; then the strip's last rows (V not a multiple of 8) are published:
+    // every carry is stored
+    __builtin_amdgcn_s_waitcnt(0);
     if (WPJ > 1 && write_bnd && lane == 0)
       __hip_atomic_store(&prog[wave], s * static_cast<int32_t>(V + 1) + static_cast<int32_t>(V), __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_WORKGROUP);
-    // this strip's boundary stores must land before the next strip reads them
-    __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
   };
 
@@ -898,6 +921,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       auto publish = [&]() {
         if (WPJ > 1 && write_bnd && --pub_left == 0) {
           pub_left = 8;
+          wait_vm_stores();
           __hip_atomic_store(&prog[wave], pub_base + static_cast<int32_t>(r) + 1, __ATOMIC_RELEASE,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -1182,10 +1206,13 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         reinterpret_cast<uint16_t*>(q + kSlotInts + 65)[lane] = 0;
       }
       aH = aF = aO = aHm = bH = bF = bO = bHm = SVS_VNEG;
-      if (WPJ > 1 && write_bnd && lane == 0) {
-        const uint32_t done = r >= V ? V : (r & ~7u);
-        __hip_atomic_store(&prog[wave], pub_base + static_cast<int32_t>(done), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (WPJ > 1 && write_bnd) {
+        wait_vm_stores();
+        if (lane == 0) {
+          const uint32_t done = r >= V ? V : (r & ~7u);
+          __hip_atomic_store(&prog[wave], pub_base + static_cast<int32_t>(done), __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
       return r;
     };
@@ -1219,10 +1246,10 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       fetch(B, r + 3);
       r += 2;
     }
+    __builtin_amdgcn_s_waitcnt(0);
     if (WPJ > 1 && write_bnd && lane == 0)
       __hip_atomic_store(&prog[wave], pub_base + static_cast<int32_t>(V), __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_WORKGROUP);
-    __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
   };
 

@@ -148,6 +148,45 @@ def test_kernel_variants_match_oracle(env):
         assert g == oracle_poa(seqs, 1)
 
 
+@pytest.mark.parametrize("env", [
+    {"SVS_POA_WPJ": "2"},
+    {"SVS_POA_WPJ": "4"},
+    {"SVS_POA_WPJ": "8"},
+    {"SVS_POA_DUAL": "1", "SVS_POA_WPJ": "2"},
+    {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "4"},
+])
+def test_short_graph_strip_handoff(env):
+    """Many reads aligned to graphs of 1-7 rows (a first read of 1-7 bases):
+    each strip's carries are one partial 8-row line, published at the strip's
+    end, and the next strip's wave is already spinning on it.  The consumer
+    reads carries with scalar loads, which are not ordered behind the
+    producer's vector stores by the workgroup-scope release alone; a stale
+    carry moved the single base of the first read to another column of the
+    MSA (profiles/r04_i4/pytest_gpu.log, env19).  Several thousand such
+    handoffs per kernel instance, every one against the oracle."""
+    import os
+    import random
+    from svscope_amd.poa import poa_batch
+    rnd = random.Random(44)
+    cases = []
+    for _ in range(1500):
+        first = "".join(rnd.choice("ACGT") for _ in range(rnd.randint(1, 7)))
+        second = "".join(rnd.choice("ACGT") for _ in range(rnd.randint(130, 640)))
+        cases.append([first, second])
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        got = poa_batch(cases)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    bad = [i for i, (seqs, g) in enumerate(zip(cases, got)) if g != oracle_poa(seqs, 1)]
+    assert not bad, (len(bad), cases[bad[0]])
+
+
 @pytest.mark.parametrize("slack,retries", [("0.05", None), ("-0.3", True)])
 def test_pruning_stats_and_exactness(slack, retries):
     """The strip kernel's exact pruning on config-3-like windows: the oracle's
