@@ -185,9 +185,10 @@ __device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, con
 // 2-19 of 1500 one-row-graph alignments per kernel instance moved without
 // it, profiles/r04_j4).  It costs nothing measurable (MSA probe kernel time
 // 2714 vs 2728 ms without it); deferring the publication by a row or more so
-// that the wait finds the stores landed costs 3 %: consumers wait on the
-// line boundary.  gfx9 s_waitcnt field layout: vmcnt [3:0] and [15:14],
-// expcnt [6:4], lgkmcnt [11:8]; this is vmcnt(0) with the others at maximum.
+// that the wait finds the stores landed costs 3 % (with or without the
+// wait: the lag or the extra scalar state in the row loop).  gfx9 s_waitcnt
+// field layout: vmcnt [3:0] and [15:14], expcnt [6:4], lgkmcnt [11:8]; this
+// is vmcnt(0) with the others at maximum.
 __device__ __forceinline__ void wait_vm_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 
