@@ -1378,6 +1378,8 @@ struct PoaScheduler::Impl {
       pl.wide = wide;
       pl.dual = dual;
       pl.waves_per_job = wpj;
+      // the pool slots per wave the launch's LDS is sized for (its occupancy)
+      g_trace.host("slots", gid(g), Clock::now(), pl.lds_slots);
       SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
       SVS_HIP(hipEventRecord(A.ev0, A.stream));
       SVS_HIP(launch_poa_strip(pl, A.stream));
