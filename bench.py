@@ -64,8 +64,14 @@ def generate(ids, procs):
     if procs <= 1 or len(ids) < 2:
         return _gen(ids)
     chunks = [ids[i::procs] for i in range(procs)]
-    with mp.get_context("fork").Pool(procs) as pool:
+    # close + join, not the context manager: its exit terminates the workers
+    # (SIGTERM), which a profiler's signal handler reports as an abort
+    pool = mp.get_context("fork").Pool(procs)
+    try:
         parts = pool.map(_gen, chunks)
+    finally:
+        pool.close()
+        pool.join()
     by_id = {}
     for chunk, part in zip(chunks, parts):
         for w, row in zip(chunk, part):
@@ -99,8 +105,12 @@ def _oracle_window(row):
 
 def _time_pool(rows, workers):
     t = time.time()
-    with mp.get_context("fork").Pool(workers, initializer=_baseline_init) as pool:
+    pool = mp.get_context("fork").Pool(workers, initializer=_baseline_init)
+    try:
         pool.map(_oracle_window, rows, chunksize=1)
+    finally:
+        pool.close()
+        pool.join()
     return time.time() - t
 
 
@@ -294,10 +304,18 @@ def main():
     session.close()
     n_em = sum(1 for r in recs if str(r[-1]).endswith("|EMOutput"))
     assert len(recs) == K * B, (len(recs), K * B)
+    ranks = None
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        # every rank's own elapsed time and windows (SCALE shows LPT / box
+        # imbalance), then time = the max over ranks
+        mine = torch.tensor([elapsed, float(len(recs))], dtype=torch.float64, device=f"cuda:{local}")
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        per = [x.tolist() for x in every]
+        elapsed = max(p[0] for p in per)
+        mean = sum(p[0] for p in per) / len(per)
+        ranks = {"elapsed_s": [round(p[0], 3) for p in per], "windows": [int(p[1]) for p in per],
+                 "max_over_mean": round(elapsed / mean, 4) if mean > 0 else None}
 
     poa = st["poa"]
     cells, cells_done = poa["dp_cells"], poa["cells_computed"]
@@ -348,6 +366,7 @@ def main():
                                                   "pruning skips most cells, so not an HBM-traffic figure"}},
             "cpu_baseline": cpu,
             "oracle_check": digests,
+            "ranks": ranks,
             "breakdown": {"poa_cells": cells, "poa_cells_computed": cells_done,
                           "prune_retries": poa["prune_retries"],
                           # HIP events between the kernels on each group's fold stream
@@ -359,7 +378,6 @@ def main():
                                              "poa_dgraph_prep_kernel": round(poa["fold_prep_ms"], 1)},
                           "poa_table_exports": poa.get("prep_jobs", 0),
                           "poa_kernel_ms": round(kms, 2), "poa_launches": launches,
-                          "poa_dual_launches": poa.get("dual_launches", 0),
                           "dgraph_peak_gb": round(poa.get("dgraph_peak_bytes", 0) / 2**30, 2),
                           "dgraph_reserved_gb": round(poa.get("dgraph_reserved_bytes", 0) / 2**30, 2),
                           "gcups": round(cells_done / (kms * 1e-3) / 1e9, 3) if kms else None,

@@ -71,7 +71,6 @@ typedef struct svs_poa_stats {
      poa_fold_update_kernel, poa_fold_sort_kernel, poa_fold_final_kernel,
      poa_dgraph_prep_kernel */
   double fold_update_ms, fold_sort_ms, fold_final_ms, fold_prep_ms;
-  uint64_t dual_launches;   /* DP launches sweeping strips in pairs */
   /* device-resident POA graphs (the context's graph arena): the most bytes of
      task blocks live at once, and the HBM the arena holds (hipMalloc'ed chunks;
      never returned before svs_release) */

@@ -45,7 +45,6 @@ class PoaStats(ctypes.Structure):
                 ("fold_ms", ctypes.c_double), ("fold_jobs", ctypes.c_uint64), ("wide_launches", ctypes.c_uint64),
                 ("fold_update_ms", ctypes.c_double), ("fold_sort_ms", ctypes.c_double),
                 ("fold_final_ms", ctypes.c_double), ("fold_prep_ms", ctypes.c_double),
-                ("dual_launches", ctypes.c_uint64),
                 ("dgraph_peak_bytes", ctypes.c_uint64), ("dgraph_reserved_bytes", ctypes.c_uint64)]
 
     def as_dict(self):

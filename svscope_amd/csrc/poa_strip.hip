@@ -125,9 +125,7 @@ struct GapOut {
 // max is its last value.  The scans of A (P1's input) and B are therefore
 // independent and run interleaved (wave_prefix_max2).
 //
-// strip_gaps_tail is everything after the two scans (p1, u scanned); the dual
-// sweep runs the scans of two strips interleaved and the tails one after the
-// other (the second strip's carries come from the first's tail).
+// strip_gaps_tail is everything after the two scans (p1, u scanned).
 __device__ __forceinline__ void strip_gaps_tail(const PoaScore& P, int32_t j0, int32_t Hpre, const StripConst& K,
                                                 int32_t p1, int32_t u, StripCarry& cr, GapOut& o);
 __device__ __forceinline__ void strip_gaps_nf(const PoaScore& P, int32_t j0, int32_t Hpre, const StripConst& K,
@@ -187,9 +185,22 @@ __device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, con
 // 2714 vs 2728 ms without it); deferring the publication by a row or more so
 // that the wait finds the stores landed costs 3 % (with or without the
 // wait: the lag or the extra scalar state in the row loop).  gfx9 s_waitcnt
-// field layout: vmcnt [3:0] and [15:14], expcnt [6:4], lgkmcnt [11:8]; this
-// is vmcnt(0) with the others at maximum.
-__device__ __forceinline__ void wait_vm_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// field layout (gfx950 is a gfx9 target; gfx10+ encode the fields
+// differently and count stores apart): vmcnt [3:0] and [15:14], expcnt
+// [6:4], lgkmcnt [11:8]; kVmcnt0 is vmcnt(0) with the others at maximum.
+//
+// What the handoff relies on besides the wait: a published unit is whole
+// 128-B carry lines (8 rows x 16 B), so a consumer's scalar load never shares
+// a cache line with a carry its producer has not yet stored.  Strip blocks are
+// VP = round_up(V, 8) rows (a multiple of 128 B) and every job's carry region
+// starts 256-B aligned (bnd_off, svs_poa_engine.cpp, checked there).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "poa_strip.hip is written for gfx950 (the s_waitcnt encoding below is gfx9's)"
+#endif
+constexpr int kVmcnt0 = (0x7 << 4) | (0xF << 8);  // vmcnt 0, expcnt 7, lgkmcnt 15
+static_assert(kVmcnt0 == 0x0F70, "gfx9 s_waitcnt vmcnt(0) encoding");
+static_assert(kCarryLineRows * 16 == 128, "a carry publication unit is one 128-B line");
+__device__ __forceinline__ void wait_vm_stores() { __builtin_amdgcn_s_waitcnt(kVmcnt0); }
 
 
 // Bounded LDS-flag wait (workgroup scope); sets *err after kStripSpinLimit polls.
@@ -244,13 +255,9 @@ __device__ __forceinline__ int32_t strip_wait_ge(int32_t* flag, int32_t target, 
 // it publishes every 8 rows through an LDS progress counter (workgroup-scope
 // release / acquire), so the waves form a row-skewed pipeline over strips.
 //
-// DUAL: after strip 0, a wave sweeps strips in pairs (s, s+1) over the same
-// rows (sweep2 below): one row record decode, one carry fetch and one
-// progress publication serve two 64-cell strip rows, the four prefix scans
-// of the two strips interleave (no DPP wait states left to fill with s_nop),
-// and strip s's carries reach strip s+1 in registers instead of through HBM.
-// Each pool slot then holds both strips' rows (2 x kStripSlotBytes).
-template <bool LDSP, int WPJ, bool PRUNE, class CodeT, bool DUAL>
+// (A dual sweep, two strips per wave over the same rows, was measured slower
+// in round 4 and removed: DESIGN §4.1.)
+template <bool LDSP, int WPJ, bool PRUNE, class CodeT>
 // The pruning variant is held to 72 VGPRs (a few spills to scratch in cold
 // paths): its workgroups still fill a CU 6 waves per SIMD deep (LDS-bound),
 // and the 80 registers per SIMD left over take the one-wave fold kernels
@@ -261,12 +268,7 @@ template <bool LDSP, int WPJ, bool PRUNE, class CodeT, bool DUAL>
 #ifndef SVS_PRUNE_OCC
 #define SVS_PRUNE_OCC 7
 #endif
-// The dual sweep keeps two strips' rows in registers; its workgroups are
-// LDS-bound at about 3 waves per SIMD, so it is held to 128 VGPRs.
-#ifndef SVS_DUAL_OCC
-#define SVS_DUAL_OCC 4
-#endif
-#define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(DUAL ? SVS_DUAL_OCC : (PRUNE ? SVS_PRUNE_OCC : 1))))
+#define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? SVS_PRUNE_OCC : 1)))
 __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore Parg,
     CodeT* __restrict__ tb, int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
@@ -292,9 +294,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   const int32_t nstrips = static_cast<int32_t>(LS >> 6);
   auto strip_of = [](int32_t j) -> int32_t { return j >> 6; };
   auto lane_of = [](int32_t j) -> int32_t { return j & 63; };
-  // slot stride: a dual launch's slots hold strip s's row, then strip s+1's
-  constexpr int kStride = DUAL ? 2 * kSlotInts : kSlotInts;
-  static_assert(!DUAL || LDSP, "the dual sweep keeps its pools in LDS");
+  constexpr int kStride = kSlotInts;
   const uint32_t nslot = LDSP ? lds_slots : J.n_slots;
   int32_t* __restrict__ pool;  // this wave's pool: nslot x {H, F, O} x 64, then nslot boundary H
   if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * kStride;
@@ -814,445 +814,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     __builtin_amdgcn_wave_barrier();
   };
 
-  // Dual sweep of strips A = s and B = s + 1 (s >= 1, s + 1 < nstrips), both
-  // at row r in the same step.  A's carries come from strip s-1 (HBM, as in
-  // sweep); B's are A's carries out of the same row, so B's two prefix scans
-  // run without them (lane 0 of B's scan inputs is VNEG) and take them in
-  // afterwards: P1 and the u-scan are prefix maxima, so the lane-0 term is
-  // one scalar maximum over the scanned values.  A row is computed when
-  // either strip has an alive input; a strip computed without one yields only
-  // dead cells (every value stays at most its full-matrix value), so both
-  // strips keep spoa's exact values and codes on their alive cells.  Only
-  // alive strip rows count in rows_done.  Column L is in the last strip, so
-  // only B tracks the sink maximum.
-  auto sweep2 = [&](int32_t s) {
-    const int32_t j0 = s << 6, j0b = j0 + 64;
-    const int32_t ja = j0 + lane, jb = ja + 64;
-    const uint8_t rca = seq[ja - 1], rcb = seq[jb - 1];
-    CodeT* __restrict__ tbl = tbj + ja;  // A's column; B's is 64 codes further
-    const GLB int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s - 1) * VP * 4;
-    int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s + 1) * VP * 4;
-    const int32_t pw = (wave + WPJ - 1) % WPJ;
-    const int32_t need0 = (s - 1) * static_cast<int32_t>(V + 1);
-    const int32_t pub_base = (s + 1) * static_cast<int32_t>(V + 1);  // B's progress
-    int32_t avail = -1;
-    const bool write_bnd = s + 2 < nstrips;
-    const bool has_sink = s + 1 == strip_of(L);
-    uint32_t pub_left = 8;
-    constexpr uint32_t kRegBit = 1u << 31;
-    uint32_t alive_a = (!prune || row0_h(P, j0 - 1) + P.m * (L - j0 + 1) >= lb) ? 1u : 0u;
-    uint32_t alive_b = (!prune || row0_h(P, j0b - 1) + P.m * (L - j0b + 1) >= lb) ? 1u : 0u;
-    const int32_t rra = L - ja, rrb = L - jb;
-    const int32_t mrra = rra >= 0 ? P.m * rra : SVS_VNEG / 2, mrrb = rrb >= 0 ? P.m * rrb : SVS_VNEG / 2;
-    best = SVS_NEG_INF;
-    best_row = 0;
-    auto ub_of = [&](uint32_t w2, int32_t rr, int32_t mr) -> int32_t {
-      const int32_t dmin = static_cast<int32_t>(w2 & 0xFFFFu), dmax = static_cast<int32_t>(w2 >> 16);
-      const int32_t d = min(imax(rr, dmin), dmax) - rr;
-      return mr + __mul24(d, d >= 0 ? cg : P.m - cg);
-    };
-    StripConst KA, KB;
-    {
-      const int32_t ge = P.g - ja * P.e, c1 = (ja - 1) * P.c;
-      KA.qjc = P.q - ja * P.c;
-      KA.k1 = ge - KA.qjc;
-      KA.k2 = lane == 0 ? SVS_VNEG + c1 + ge : c1 + ge;
-      KA.t2b = lane == 0 ? SVS_VNEG : c1 + ge;
-      KA.jc = ja * P.c;
-      KA.je = ja * P.e;
-      KA.ve = P.e;
-      KA.vc = P.c;
-      const int32_t geb = P.g - jb * P.e, c1b = (jb - 1) * P.c, qjcb = P.q - jb * P.c;
-      KB.qjc = lane == 0 ? SVS_VNEG : qjcb;  // lane 0: no carry in the scan (taken in after it)
-      KB.k1 = geb - qjcb;
-      KB.k2 = lane == 0 ? SVS_VNEG + c1b + geb : c1b + geb;
-      KB.t2b = lane == 0 ? SVS_VNEG : c1b + geb;
-      KB.jc = jb * P.c;
-      KB.je = jb * P.e;
-      KB.ve = P.e;
-      KB.vc = P.c;
-    }
-    // B's lane-0 scan terms without the carry: q - j0b c and its u offset
-    const int32_t qb0 = P.q - j0b * P.c;
-    const int32_t k1b0 = (P.g - j0b * P.e) - qb0;
-    // virtual row 0 in slot 0, both strips
-    {
-      const int32_t ha = row0_h(P, ja), hb = row0_h(P, jb);
-      const int32_t foa = ja == 0 ? 0 : SVS_NEG_INF;
-      pool[lane + 1] = ha;
-      pool[kSlotInts + lane + 1] = hb;
-      if (lane == 0) {
-        pool[0] = row0_h(P, j0 - 1);
-        pool[kSlotInts] = row0_h(P, j0b - 1);
-      }
-      reinterpret_cast<uint16_t*>(pool + 65)[lane] = static_cast<uint16_t>(pack_fo(ha, foa, foa));
-      reinterpret_cast<uint16_t*>(pool + kSlotInts + 65)[lane] =
-          static_cast<uint16_t>(pack_fo(hb, SVS_NEG_INF, SVS_NEG_INF));
-    }
-    __builtin_amdgcn_wave_barrier();
-
-    auto fetch = [&](RowIn& d, uint32_t r) {
-      const uint32_t rr = r < V ? r : V - 1;
-      const TBL uint32_t* w = rec + (rr << 2);
-      d.w0 = w[0];
-      d.w1 = w[1];
-      if constexpr (PRUNE) {
-        d.w2 = w[2];
-        d.w3 = w[3];
-      }
-      if (WPJ > 1) {
-        const int32_t need = need0 + static_cast<int32_t>(rr) + 1;
-        if (avail < need) avail = strip_wait_ge(&prog[pw], need, &s_err);
-      }
-      const svs_i32x4 v = *reinterpret_cast<const GLB svs_i32x4*>(bin + (rr << 2));
-      d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
-    };
-
-    // rows just above, both strips (registers)
-    int32_t aH = 0, aF = 0, aO = 0, aHm = 0, bH = 0, bF = 0, bO = 0, bHm = 0;
-    auto step2 = [&](uint32_t r, const RowIn& d) {
-      const uint32_t w0 = __builtin_amdgcn_readfirstlane(d.w0);
-      const uint32_t nb = w0 & 0xFFu;
-      const bool sink = (w0 >> 8) & 1u;
-      const bool store = (w0 >> 9) & 1u;
-      const uint32_t np = sizeof(CodeT) == 4 ? rps[r + 1] - rps[r] : (w0 >> 10) & 63u;
-      const uint32_t own = w0 >> 16;
-      const uint32_t wp = __builtin_amdgcn_readfirstlane(d.w1);
-      const uint32_t own_bit = (store && own < 31u) ? 1u << own : 0u;
-      auto publish = [&]() {
-        if (WPJ > 1 && write_bnd && --pub_left == 0) {
-          pub_left = 8;
-          wait_vm_stores();
-          __hip_atomic_store(&prog[wave], pub_base + static_cast<int32_t>(r) + 1, __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      };
-      const int32_t cH_in = __builtin_amdgcn_readfirstlane(d.b3);
-      int32_t* __restrict__ qo = pool + own * kStride;  // this row's slot (A; B at + kSlotInts)
-      bool live_a = true, live_b_own = true;  // A has an alive input; B has one besides A's carry
-      if (prune) {
-        auto sa = [&](uint32_t al, uint32_t ps) -> bool {
-          if (ps == kNoSlot) return (al >> 31) != 0;
-          return ps >= 31u || ((al >> ps) & 1u) != 0;
-        };
-        const uint32_t s0 = wp & 0xFFFFu, s1 = wp >> 16;
-        bool la = cH_in > SVS_VNEG / 2 || sa(alive_a, s0) || (np >= 2 && sa(alive_a, s1));
-        bool lbv = sa(alive_b, s0) || (np >= 2 && sa(alive_b, s1));
-        if (np > kInlinePreds && !(la && lbv)) {
-          const TBL uint32_t* __restrict__ spill = pslot + rps[r];
-          for (uint32_t k = kInlinePreds; k < np && !(la && lbv); ++k) {
-            const uint32_t ps = __builtin_amdgcn_readfirstlane(spill[k]);
-            la = la || sa(alive_a, ps);
-            lbv = lbv || sa(alive_b, ps);
-          }
-        }
-        if (!la && !lbv) {
-          if (store) {
-            qo[lane + 1] = SVS_VNEG;
-            qo[lane] = SVS_VNEG;
-            reinterpret_cast<uint16_t*>(qo + 65)[lane] = 0;
-            qo[kSlotInts + lane + 1] = SVS_VNEG;
-            qo[kSlotInts + lane] = SVS_VNEG;
-            reinterpret_cast<uint16_t*>(qo + kSlotInts + 65)[lane] = 0;
-          }
-          const uint32_t clr = ~(__builtin_amdgcn_readfirstlane(d.w3) | own_bit | kRegBit);
-          alive_a &= clr;
-          alive_b &= clr;
-          aH = aF = aO = aHm = bH = bF = bO = bHm = SVS_VNEG;
-          if (write_bnd && lane == 0)
-            *reinterpret_cast<int4*>(reinterpret_cast<char*>(bout) + (r << 4)) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
-          publish();
-          return;
-        }
-        live_a = la;
-        live_b_own = lbv;
-      }
-      uint2 w2w3 = make_uint2(0, 0);
-      if constexpr (PRUNE)
-        w2w3 = make_uint2(__builtin_amdgcn_readfirstlane(d.w2), __builtin_amdgcn_readfirstlane(d.w3));
-      StripCarry cr;
-      {
-        const int32_t jl = j0 - 1;
-        cr.run1 = __builtin_amdgcn_readfirstlane(d.b0);
-        cr.run2 = __builtin_amdgcn_readfirstlane(d.b1);
-        cr.cHpre = __builtin_amdgcn_readfirstlane(d.b2);
-        cr.cH = cH_in;
-        cr.cQ = jl * P.c + cr.run1;
-        cr.cE = jl * P.e + cr.run2;
-      }
-      const int32_t mca = rca == nb ? P.m : P.n, mcb = rcb == nb ? P.m : P.n;
-      // in-edge values of strip X (0: A, 1: B) from slot ps or the registers
-      auto pv = [&](auto xtag, uint32_t ps, int32_t& hp, int32_t& fp, int32_t& op, int32_t& hpm) {
-        constexpr int X = decltype(xtag)::value;
-        if (ps == kNoSlot) {
-          if (X == 0) { hp = aH; fp = aF; op = aO; hpm = aHm; }
-          else { hp = bH; fp = bF; op = bO; hpm = bHm; }
-        } else {
-          const int32_t* q = pool + ps * kStride + X * kSlotInts;
-          hpm = __builtin_nontemporal_load(q + lane);
-          hp = __builtin_nontemporal_load(q + lane + 1);
-          const uint32_t dd = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(q + 65) + lane);
-          fp = hp - static_cast<int32_t>(dd & 0xFFu);
-          op = hp - static_cast<int32_t>((dd >> 8) & 0xFFu);
-        }
-      };
-      using XA = std::integral_constant<int, 0>;
-      using XB = std::integral_constant<int, 1>;
-      GapOut ga, gb;
-      bool any_a = true, any_b = true;
-      StripCarry cb;  // B's carries in, then out
-      // both strips' scans interleaved, A's tail, its liveness, B's tail
-      auto gaps2 = [&](int32_t hpa, int32_t hpb) {
-        int32_t p1a = shr1_add(cr.cHpre + KA.qjc, hpa, KA.qjc);
-        int32_t ua = p1a + KA.k1;
-        int32_t p1b = shr1_add_bc(hpb, KB.qjc);
-        int32_t ub = p1b + KB.k1;
-        wave_prefix_max4(p1a, ua, p1b, ub);
-        strip_gaps_tail(P, j0, hpa, KA, p1a, ua, cr, ga);
-        if (prune) any_a = __builtin_amdgcn_ballot_w64(ga.H + ub_of(w2w3.x, rra, mrra) >= lb) != 0;
-        // a row with no alive cell hands VNEG carries on (as through HBM)
-        cb.run1 = any_a ? cr.run1 : SVS_VNEG;
-        cb.run2 = any_a ? cr.run2 : SVS_VNEG;
-        cb.cHpre = any_a ? cr.cHpre : SVS_VNEG;
-        cb.cH = any_a ? cr.cH : SVS_VNEG;
-        cb.cQ = (j0b - 1) * P.c + cb.run1;
-        cb.cE = (j0b - 1) * P.e + cb.run2;
-        const int32_t c0 = cb.cHpre + qb0;
-        p1b = imax(p1b, c0);
-        ub = imax(ub, c0 + k1b0);
-        const int32_t cH_b = cb.cH;
-        strip_gaps_tail(P, j0b, hpb, KB, p1b, ub, cb, gb);
-        if (prune) any_b = __builtin_amdgcn_ballot_w64(gb.H + ub_of(w2w3.x, rrb, mrrb) >= lb) != 0;
-        return cH_b;
-      };
-      int32_t Fa, Oa, Fb, Ob, cHb_in;
-      uint32_t code_a, code_b;
-      // one in-edge: the codes of the single sweep's np <= 1 case
-      auto code1 = [&](const GapOut& o, int32_t F, int32_t O, int32_t hp, int32_t fp, int32_t op, int32_t hpm,
-                       int32_t mc) -> uint32_t {
-        const int32_t H = o.H;
-        const bool dg = H == hpm + mc;
-        const bool up = H == imax(F, O);
-        const bool ua = H == fp + P.e, ub = H == hp + P.g, uc = H == op + P.c;
-        const bool lf = H == imax(o.E, o.Q);
-        const bool la = H == o.prevEe, lb2 = H == o.prevH + P.g, lc = H == o.prevQc;
-        const bool lbit = o.prevH + P.g == o.E || o.prevH + P.q == o.Q;
-        const bool va = F == hp + P.g, vb = F == fp + P.e, vc = O == hp + P.q;
-        const uint32_t upc = (ua || (!ub && uc)) ? 5u : 1u;
-        const uint32_t lfc = (la || (!lb2 && lc)) ? 6u : 2u;
-        uint32_t code = dg ? 0u : (up ? upc : (lf ? lfc : 3u));
-        code |= lbit ? 1u << TF::kLBit : 0u;
-        if (np != 0) code |= (va || (!vb && vc)) ? 1u << TF::kStop : 0u;
-        else code |= TF::kMask << TF::kUc;
-        return code;
-      };
-      // two in-edges: the single sweep's np == 2 case
-      auto code2 = [&](const GapOut& o, int32_t F, int32_t O, int32_t hp0, int32_t fp0, int32_t op0, int32_t hm0,
-                       int32_t hp1, int32_t fp1, int32_t op1, int32_t hm1, int32_t mc) -> uint32_t {
-        const int32_t H = o.H;
-        const int32_t F0k = imax(hp0 + P.g, fp0 + P.e), O0k = imax(hp0 + P.q, op0 + P.c);
-        const int32_t F1k = imax(hp1 + P.g, fp1 + P.e), O1k = imax(hp1 + P.q, op1 + P.c);
-        const int32_t D0 = hm0 + mc, D1 = hm1 + mc;
-        const bool up0 = H == imax(F0k, O0k), up1 = H == imax(F1k, O1k);
-        const int32_t hpu = up0 ? hp0 : hp1, fpu = up0 ? fp0 : fp1, opu = up0 ? op0 : op1;
-        const bool ua = H == fpu + P.e, ub = H == hpu + P.g, uc = H == opu + P.c;
-        const bool ch0 = F == F0k || O == O0k;
-        const int32_t hpc = ch0 ? hp0 : hp1, fpc = ch0 ? fp0 : fp1;
-        const bool va = F == hpc + P.g, vb = F == fpc + P.e, vc = O == hpc + P.q;
-        const bool lf = H == imax(o.E, o.Q);
-        const bool la = H == o.prevEe, lb2 = H == o.prevH + P.g, lc = H == o.prevQc;
-        const bool lbit = o.prevH + P.g == o.E || o.prevH + P.q == o.Q;
-        const uint32_t upc = ((ua || (!ub && uc)) ? 5u : 1u) | (up0 ? 0u : 8u);
-        const uint32_t lfc = (la || (!lb2 && lc)) ? 6u : 2u;
-        uint32_t code = H == D0 ? 0u : (H == D1 ? 8u : (up0 || up1 ? upc : (lf ? lfc : 3u)));
-        code |= lbit ? 1u << TF::kLBit : 0u;
-        code |= ((va || (!vb && vc)) ? 1u << TF::kStop : 0u) | (ch0 ? 0u : (1u << TF::kUc));
-        return code;
-      };
-      if (np <= 1) {
-        const uint32_t ps = wp & 0xFFFFu;  // np == 0: slot 0 (virtual row)
-        int32_t hpa, fpa, opa, hma, hpb, fpb, opb, hmb;
-        pv(XA{}, ps, hpa, fpa, opa, hma);
-        pv(XB{}, ps, hpb, fpb, opb, hmb);
-        Fa = imax(hpa + P.g, fpa + P.e);
-        Oa = imax(hpa + P.q, opa + P.c);
-        Fb = imax(hpb + P.g, fpb + P.e);
-        Ob = imax(hpb + P.q, opb + P.c);
-        cHb_in = gaps2(imax(hma + mca, imax(Fa, Oa)), imax(hmb + mcb, imax(Fb, Ob)));
-        code_a = code1(ga, Fa, Oa, hpa, fpa, opa, hma, mca);
-        code_b = code1(gb, Fb, Ob, hpb, fpb, opb, hmb, mcb);
-      } else if (np == 2) {
-        int32_t a0h, a0f, a0o, a0m, a1h, a1f, a1o, a1m, b0h, b0f, b0o, b0m, b1h, b1f, b1o, b1m;
-        pv(XA{}, wp & 0xFFFFu, a0h, a0f, a0o, a0m);
-        pv(XA{}, wp >> 16, a1h, a1f, a1o, a1m);
-        pv(XB{}, wp & 0xFFFFu, b0h, b0f, b0o, b0m);
-        pv(XB{}, wp >> 16, b1h, b1f, b1o, b1m);
-        Fa = imax(imax(a0h + P.g, a0f + P.e), imax(a1h + P.g, a1f + P.e));
-        Oa = imax(imax(a0h + P.q, a0o + P.c), imax(a1h + P.q, a1o + P.c));
-        Fb = imax(imax(b0h + P.g, b0f + P.e), imax(b1h + P.g, b1f + P.e));
-        Ob = imax(imax(b0h + P.q, b0o + P.c), imax(b1h + P.q, b1o + P.c));
-        cHb_in = gaps2(imax(imax(a0m + mca, a1m + mca), imax(Fa, Oa)),
-                       imax(imax(b0m + mcb, b1m + mcb), imax(Fb, Ob)));
-        code_a = code2(ga, Fa, Oa, a0h, a0f, a0o, a0m, a1h, a1f, a1o, a1m, mca);
-        code_b = code2(gb, Fb, Ob, b0h, b0f, b0o, b0m, b1h, b1f, b1o, b1m, mcb);
-      } else {
-        const TBL uint32_t* __restrict__ spill = pslot + rps[r];
-        Fa = Oa = Fb = Ob = SVS_VNEG;
-        int32_t Hda = SVS_VNEG, Hdb = SVS_VNEG;
-        for (uint32_t k = 0; k < np; ++k) {
-          const uint32_t ps = __builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill));
-          int32_t hp, fp, op, hpm;
-          pv(XA{}, ps, hp, fp, op, hpm);
-          Fa = imax(Fa, imax(hp + P.g, fp + P.e));
-          Oa = imax(Oa, imax(hp + P.q, op + P.c));
-          Hda = imax(Hda, hpm + mca);
-          pv(XB{}, ps, hp, fp, op, hpm);
-          Fb = imax(Fb, imax(hp + P.g, fp + P.e));
-          Ob = imax(Ob, imax(hp + P.q, op + P.c));
-          Hdb = imax(Hdb, hpm + mcb);
-        }
-        cHb_in = gaps2(imax(Hda, imax(Fa, Oa)), imax(Hdb, imax(Fb, Ob)));
-        auto codeg = [&](auto xtag, const GapOut& o, int32_t F, int32_t O, int32_t mc) -> uint32_t {
-          const int32_t H = o.H;
-          uint32_t diag_k = TF::kMask, up_k = TF::kMask, up_ext = 0, uc_k = TF::kMask, uc_stop = 0;
-          for (uint32_t k = 0; k < np; ++k) {
-            int32_t hp, fp, op, hpm;
-            pv(xtag, __builtin_amdgcn_readfirstlane(pred_slot_of(d, k, spill)), hp, fp, op, hpm);
-            if (diag_k == TF::kMask && H == hpm + mc) diag_k = k;
-            if (up_k == TF::kMask) {
-              const bool a = H == fp + P.e, b = H == hp + P.g, c = H == op + P.c, dd = H == hp + P.q;
-              if (a || b || c || dd) { up_k = k; up_ext = (a || (!b && c)) ? 1u : 0u; }
-            }
-            if (uc_k == TF::kMask) {
-              const bool a = F == hp + P.g, b = F == fp + P.e, c = O == hp + P.q, dd = O == op + P.c;
-              if (a || b || c || dd) { uc_k = k; uc_stop = (a || (!b && c)) ? 1u : 0u; }
-            }
-          }
-          const bool la = H == o.prevEe, lb2 = H == o.prevH + P.g;
-          const bool lc = H == o.prevQc, ld = H == o.prevH + P.q;
-          const bool lbit = o.prevH + P.g == o.E || o.prevH + P.q == o.Q;
-          return assemble_code<TF>(diag_k, up_k, up_ext, la || lb2 || lc || ld, la || (!lb2 && lc), lbit, uc_k, uc_stop);
-        };
-        code_a = codeg(XA{}, ga, Fa, Oa, mca);
-        code_b = codeg(XB{}, gb, Fb, Ob, mcb);
-      }
-      tbl[r * LS] = static_cast<CodeT>(code_a);
-      tbl[r * LS + 64] = static_cast<CodeT>(code_b);
-      if (prune) {
-        // strip rows with an alive input (A: carry or in-edge; B: A's carry
-        // or an in-edge)
-        if constexpr (PRUNE)
-          rows_done += (live_a ? 1u : 0u) + ((live_b_own || any_a) ? 1u : 0u);
-        const uint32_t ob = own_bit | kRegBit;
-        const bool out_a = any_a || cH_in > SVS_VNEG / 2;
-        const bool out_b = any_b || cHb_in > SVS_VNEG / 2;
-        alive_a = ((alive_a & ~ob) | (out_a ? ob : 0u)) & ~w2w3.y;
-        alive_b = ((alive_b & ~ob) | (out_b ? ob : 0u)) & ~w2w3.y;
-      }
-      if (store) {
-        qo[lane + 1] = ga.H;
-        qo[lane] = ga.prevH;
-        reinterpret_cast<uint16_t*>(qo + 65)[lane] = static_cast<uint16_t>(pack_fo(ga.H, Fa, Oa));
-        qo[kSlotInts + lane + 1] = gb.H;
-        qo[kSlotInts + lane] = gb.prevH;
-        reinterpret_cast<uint16_t*>(qo + kSlotInts + 65)[lane] = static_cast<uint16_t>(pack_fo(gb.H, Fb, Ob));
-      }
-      aH = ga.H; aF = Fa; aO = Oa; aHm = ga.prevH;
-      bH = gb.H; bF = Fb; bO = Ob; bHm = gb.prevH;
-      if (write_bnd && lane == 0) {
-        *reinterpret_cast<int4*>(reinterpret_cast<char*>(bout) + (r << 4)) =
-            any_b ? make_int4(cb.run1, cb.run2, cb.cHpre, cb.cH) : make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
-      }
-      publish();
-      if (has_sink && sink) {
-        const bool u = gb.H > best;
-        best = u ? gb.H : best;
-        best_row = u ? static_cast<int32_t>(r) + 1 : best_row;
-      }
-    };
-
-    // fast_forward of the single sweep for the pair: the next row with an
-    // alive carry from strip s-1 (or a source row while a virtual row is
-    // alive); B's carries of the rows passed are VNEG, both pools reset
-    auto fast_forward2 = [&](uint32_t r) -> uint32_t {
-      const bool virt = ((alive_a | alive_b) & 1u) != 0;
-      while (r < V) {
-        uint32_t lim = min(64u, V - r);
-        if (WPJ > 1) {
-          const int32_t least = need0 + static_cast<int32_t>(min(V, r + 8));
-          if (avail < least) avail = strip_wait_ge(&prog[pw], least, &s_err);
-          lim = min(lim, static_cast<uint32_t>(min(static_cast<int32_t>(V), avail - need0)) - r);
-        }
-        const uint32_t rr = r + static_cast<uint32_t>(lane);
-        const bool in = static_cast<uint32_t>(lane) < lim;
-        bool cand = false;
-        if (in) cand = __builtin_nontemporal_load(bin + 4ull * rr + 3) > SVS_VNEG / 2;
-        if (virt && in) cand = cand || ((rec[static_cast<uint64_t>(rr) * kRecWords] >> 10) & 63u) == 0;
-        const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
-        const uint32_t n = m ? static_cast<uint32_t>(__builtin_ctzll(m)) : lim;
-        if (write_bnd && static_cast<uint32_t>(lane) < n)
-          *reinterpret_cast<int4*>(bout + 4ull * rr) = make_int4(SVS_VNEG, SVS_VNEG, SVS_VNEG, SVS_VNEG);
-        r += n;
-        if (m) break;
-      }
-      for (uint32_t p = 1; p < nslot; ++p) {
-        int32_t* q = pool + p * kStride;
-        q[lane + 1] = SVS_VNEG;
-        q[kSlotInts + lane + 1] = SVS_VNEG;
-        if (lane == 0) {
-          q[0] = SVS_VNEG;
-          q[kSlotInts] = SVS_VNEG;
-        }
-        reinterpret_cast<uint16_t*>(q + 65)[lane] = 0;
-        reinterpret_cast<uint16_t*>(q + kSlotInts + 65)[lane] = 0;
-      }
-      aH = aF = aO = aHm = bH = bF = bO = bHm = SVS_VNEG;
-      if (WPJ > 1 && write_bnd) {
-        wait_vm_stores();
-        if (lane == 0) {
-          const uint32_t done = r >= V ? V : (r & ~7u);
-          __hip_atomic_store(&prog[wave], pub_base + static_cast<int32_t>(done), __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-      return r;
-    };
-    auto dead_pair = [&]() { return ((alive_a | alive_b) & ~1u) == 0; };
-
-    RowIn A, B;
-    uint32_t r = 0;
-    if (prune) r = fast_forward2(0);
-    pub_left = 8u - (r & 7u);
-    fetch(A, r);
-    fetch(B, r + 1);
-    while (r < V) {
-      step2(r, A);
-      if (prune && dead_pair()) {
-        r = fast_forward2(r + 1);
-        pub_left = 8u - (r & 7u);
-        fetch(A, r);
-        fetch(B, r + 1);
-        continue;
-      }
-      fetch(A, r + 2);
-      if (r + 1 >= V) break;
-      step2(r + 1, B);
-      if (prune && dead_pair()) {
-        r = fast_forward2(r + 2);
-        pub_left = 8u - (r & 7u);
-        fetch(A, r);
-        fetch(B, r + 1);
-        continue;
-      }
-      fetch(B, r + 3);
-      r += 2;
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    if (WPJ > 1 && write_bnd && lane == 0)
-      __hip_atomic_store(&prog[wave], pub_base + static_cast<int32_t>(V), __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_WORKGROUP);
-    __builtin_amdgcn_wave_barrier();
-  };
 
   if (WPJ > 1) {
     if (lane == 0) {
@@ -1264,20 +825,9 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   if (V > 0) {
     using TrueT = std::integral_constant<bool, true>;
     using FalseT = std::integral_constant<bool, false>;
-    if constexpr (DUAL) {
-      // sweep t: strip 0 alone, then strips (2t-1, 2t); an unpaired last strip alone
-      const int32_t nsweeps = 1 + nstrips / 2;
-      for (int32_t t = wave; t < nsweeps; t += WPJ) {
-        const int32_t s = 2 * t - 1;
-        if (t == 0) SVS_SP(2, sweep(TrueT{}, 0));
-        else if (s + 1 < nstrips) SVS_SP(2, sweep2(s));
-        else SVS_SP(2, sweep(FalseT{}, s));
-      }
-    } else {
-      for (int32_t s = wave; s < nstrips; s += WPJ) {
-        if (s == 0) SVS_SP(2, sweep(TrueT{}, 0));
-        else SVS_SP(2, sweep(FalseT{}, s));
-      }
+    for (int32_t s = wave; s < nstrips; s += WPJ) {
+      if (s == 0) SVS_SP(2, sweep(TrueT{}, 0));
+      else SVS_SP(2, sweep(FalseT{}, s));
     }
   }
 
@@ -1285,8 +835,8 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   // traceback-code stores must be visible to wave 0's lane 0
   best_row = __shfl(best_row, lane_of(L), 64);
   best = __shfl(best, lane_of(L), 64);
-  // the sweep holding column L's strip, and its wave
-  const int32_t sink_wave = (DUAL ? (strip_of(L) + 1) / 2 : strip_of(L)) % WPJ;
+  // the wave that swept column L's strip
+  const int32_t sink_wave = strip_of(L) % WPJ;
   if (WPJ > 1) {
     if (lane == 0) {
       s_rows[wave] = rows_done;
@@ -1406,13 +956,11 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   if (a.n_jobs <= 0) return hipSuccess;
   const int w = a.waves_per_job;
   const bool lds_pool = a.lds_slots > 0;
-  const bool dual = lds_pool && a.dual;
-  const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * kStripSlotBytes * (dual ? 2 : 1) : 0;
-#define SVS_STRIP5(LP, W, PR, CT, DU)                                                                          \
-  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR, CT, DU>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, \
-                     a.n_jobs, a.score, static_cast<CT*>(a.tb), a.bnd, a.bnd, a.pool, a.aln, a.aln_len,            \
+  const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * kStripSlotBytes : 0;
+#define SVS_STRIP4(LP, W, PR, CT)                                                                          \
+  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR, CT>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, \
+                     a.n_jobs, a.score, static_cast<CT*>(a.tb), a.bnd, a.bnd, a.pool, a.aln, a.aln_len,     \
                      a.lds_slots)
-#define SVS_STRIP4(LP, W, PR, CT) SVS_STRIP5(LP, W, PR, CT, false)
 #define SVS_STRIP3(LP, W, PR)              \
   do {                                     \
     if (a.wide) {                          \
@@ -1429,33 +977,8 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
       SVS_STRIP3(LP, W, false);       \
     }                                 \
   } while (0)
-#define SVS_DUAL3(W, PR)                        \
-  do {                                          \
-    if (a.wide) {                               \
-      SVS_STRIP5(true, W, PR, uint32_t, true);  \
-    } else {                                    \
-      SVS_STRIP5(true, W, PR, uint16_t, true);  \
-    }                                           \
-  } while (0)
-#define SVS_DUAL(W)             \
-  do {                          \
-    if (a.prune) {              \
-      SVS_DUAL3(W, true);       \
-    } else {                    \
-      SVS_DUAL3(W, false);      \
-    }                           \
-  } while (0)
-  // the engine's choices: 1, 2, 4, 8 waves per job (16 with the pool in LDS;
-  // dual sweeps: 1, 2, 4, 8)
-  if (dual) {
-    switch (w) {
-      case 8: SVS_DUAL(8); break;
-      case 4: SVS_DUAL(4); break;
-      case 2: SVS_DUAL(2); break;
-      case 1: SVS_DUAL(1); break;
-      default: return hipErrorInvalidValue;
-    }
-  } else if (lds_pool) {
+  // the engine's choices: 1, 2, 4, 8 waves per job (16 with the pool in LDS)
+  if (lds_pool) {
     switch (w) {
       case 16: SVS_STRIP(true, 16); break;
       case 8: SVS_STRIP(true, 8); break;
@@ -1473,12 +996,9 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
       default: return hipErrorInvalidValue;
     }
   }
-#undef SVS_DUAL
-#undef SVS_DUAL3
 #undef SVS_STRIP
 #undef SVS_STRIP3
 #undef SVS_STRIP4
-#undef SVS_STRIP5
   return hipGetLastError();
 }
 

@@ -56,35 +56,6 @@ __device__ __forceinline__ void wave_prefix_max2(int32_t& a, int32_t& b) {
   b = dpp_max_step<0x143, 0xC>(b);
 }
 
-// Four independent scans (the two of each strip of a dual sweep): every DPP
-// read-after-write wait state is covered by another chain's step.
-__device__ __forceinline__ void wave_prefix_max4(int32_t& a, int32_t& b, int32_t& c, int32_t& d) {
-  a = dpp_max_step<0x111, 0xF>(a);
-  b = dpp_max_step<0x111, 0xF>(b);
-  c = dpp_max_step<0x111, 0xF>(c);
-  d = dpp_max_step<0x111, 0xF>(d);
-  a = dpp_max_step<0x112, 0xF>(a);
-  b = dpp_max_step<0x112, 0xF>(b);
-  c = dpp_max_step<0x112, 0xF>(c);
-  d = dpp_max_step<0x112, 0xF>(d);
-  a = dpp_max_step<0x114, 0xF>(a);
-  b = dpp_max_step<0x114, 0xF>(b);
-  c = dpp_max_step<0x114, 0xF>(c);
-  d = dpp_max_step<0x114, 0xF>(d);
-  a = dpp_max_step<0x118, 0xF>(a);
-  b = dpp_max_step<0x118, 0xF>(b);
-  c = dpp_max_step<0x118, 0xF>(c);
-  d = dpp_max_step<0x118, 0xF>(d);
-  a = dpp_max_step<0x142, 0xA>(a);
-  b = dpp_max_step<0x142, 0xA>(b);
-  c = dpp_max_step<0x142, 0xA>(c);
-  d = dpp_max_step<0x142, 0xA>(d);
-  a = dpp_max_step<0x143, 0xC>(a);
-  b = dpp_max_step<0x143, 0xC>(b);
-  c = dpp_max_step<0x143, 0xC>(c);
-  d = dpp_max_step<0x143, 0xC>(d);
-}
-
 // lane l <- x[l-1]; lane 0 <- fill (wave-uniform).  DPP wave_shr:1.
 __device__ __forceinline__ int32_t wave_shr1(int32_t x, int32_t fill, int /*lane*/) {
   return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xF, 0xF, false);

@@ -107,7 +107,12 @@ struct PinnedBuf {
     void* p = nullptr;
     SVS_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
     if (old && keep) std::memcpy(p, old, std::min(keep, cap));
-    if (old) retired.push_back(old);
+    // as in ensure(): a buffer of 256 MiB or more is freed at once (hipHostFree
+    // waits for the device), so that regrows never hold twice the peak
+    if (old) {
+      if (cap >= (size_t(256) << 20)) SVS_HIP(hipHostFree(old));
+      else retired.push_back(old);
+    }
     ptr = p;
     cap = want;
   }

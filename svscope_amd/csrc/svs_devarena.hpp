@@ -4,10 +4,13 @@
 // with a free list per class, so the thousands of task starts and ends of a
 // session never call hipMalloc / hipFree (both can stall the whole device).
 // The arena has a byte limit (svs_context::dgraph_budget: the HBM left after
-// the per-launch budget, svs_abi.cpp); a block that would take the chunks past
-// it fails loudly (SvsError -2) instead of running the device out of memory,
-// and chunks are sized from the limit.  Blocks go back to their class's free
-// list, never to HIP: reserved() only grows, peak() is the largest in_use().
+// the per-launch budget, svs_abi.cpp); chunks are sized from it.  Before a new
+// chunk is cut, a free block of a larger class is split in halves down to the
+// class asked for; when neither fits, try_alloc returns null (the engine fails
+// that task alone, svs_poa_engine.cpp reserve_blocks) and alloc throws
+// (SvsError -2) instead of running the device out of memory.  Blocks go back
+// to their class's free list, never to HIP: reserved() only grows, peak() is
+// the largest in_use().
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -38,8 +41,9 @@ class DevArena {
     while (c < bytes) c <<= 1;
     return c;
   }
-  // A block of at least `bytes` (its class size is what free() takes back).
-  void* alloc(size_t bytes) {
+  // A block of at least `bytes` (its class size is what free() takes back),
+  // or null when it would take the arena past its limit.
+  void* try_alloc(size_t bytes) {
     const size_t c = size_class(bytes);
     auto it = free_.find(c);
     if (it != free_.end() && !it->second.empty()) {
@@ -47,14 +51,40 @@ class DevArena {
       it->second.pop_back();
       return take(p, c);
     }
-    if (c > chunk_) return take(new_chunk(c), c);  // larger than a chunk: a chunk of its own
+    if (c > chunk_) {  // larger than a chunk: a chunk of its own
+      void* p = new_chunk(c);
+      return p ? take(p, c) : split_larger(c);
+    }
     if (!cur_ || used_ + c > chunk_) {
-      cur_ = static_cast<char*>(new_chunk(chunk_));
+      // the rest of the current chunk goes to the free lists, largest first
+      if (cur_) {
+        size_t left = chunk_ - used_;
+        for (size_t k = chunk_; k >= (size_t(64) << 10); k >>= 1)
+          while (left >= k) {
+            free_[k].push_back(cur_ + used_);
+            used_ += k;
+            left -= k;
+          }
+      }
+      void* n = new_chunk(chunk_);
+      if (!n) {
+        cur_ = nullptr;
+        used_ = 0;
+        return split_larger(c);
+      }
+      cur_ = static_cast<char*>(n);
       used_ = 0;
     }
     void* p = cur_ + used_;
     used_ += c;
     return take(p, c);
+  }
+  void* alloc(size_t bytes) {
+    void* p = try_alloc(bytes);
+    if (!p)
+      throw SvsError(-2, "device graph arena: a block of " + std::to_string(bytes) + " bytes would pass its limit of " +
+                             std::to_string(limit_) + " (SVS_DEVICE_BUDGET_GB, fewer tasks in flight)");
+    return p;
   }
   void free(void* p, size_t bytes) {
     if (!p) return;
@@ -73,10 +103,20 @@ class DevArena {
     peak_ = std::max(peak_, in_use_);
     return p;
   }
+  // a free block of the smallest larger class, halved down to class c (the
+  // upper halves go to their free lists); null when there is none
+  void* split_larger(size_t c) {
+    for (auto it = free_.upper_bound(c); it != free_.end(); ++it) {
+      if (it->second.empty()) continue;
+      char* p = static_cast<char*>(it->second.back());
+      it->second.pop_back();
+      for (size_t k = it->first; k > c; k >>= 1) free_[k >> 1].push_back(p + (k >> 1));
+      return take(p, c);
+    }
+    return nullptr;
+  }
   void* new_chunk(size_t bytes) {
-    if (reserved_ + bytes > limit_)
-      throw SvsError(-2, "device graph arena: " + std::to_string(reserved_ + bytes) + " bytes would pass its limit of " +
-                             std::to_string(limit_) + " (SVS_DEVICE_BUDGET_GB, fewer tasks in flight)");
+    if (reserved_ + bytes > limit_) return nullptr;
     void* p = nullptr;
     SVS_HIP(hipMalloc(&p, bytes));
     chunks_.push_back(p);

@@ -57,7 +57,6 @@ struct PoaLaunch {
   uint32_t lds_slots;    // pool slots per wave held in LDS (max n_slots of the launch)
   bool prune;            // some job has a pruning bound: the pruning kernel variant
   bool wide;             // some row has more than 31 in-edges: 32-bit codes (TbFmt, poa_wave.hpp)
-  bool dual;             // LDS pools: strips swept in pairs (poa_strip.hip, 2 x kStripSlotBytes per slot)
 };
 
 // One block copy of launch_scatter_copy (bytes a multiple of 64, both ends
@@ -83,6 +82,11 @@ constexpr uint32_t kStripMaxLdsSlots = 80;
 // LDS a strip workgroup's pools may take (160 KiB per CU on gfx950, less the
 // kernel's own few static words)
 constexpr uint64_t kStripLdsBytes = 160 * 1024 - 256;
+// Strip carries (16 B per row) are published to the next strip's wave in
+// whole lines of this many rows (poa_strip.hip wait_vm_stores); a job's carry
+// region starts at a multiple of kCarryAlignInts int32 (256 B).
+constexpr uint32_t kCarryLineRows = 8;
+constexpr uint64_t kCarryAlignInts = 64;
 
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream);
 // Device half of the strip row export (poa_prep.hip) for the jobs with

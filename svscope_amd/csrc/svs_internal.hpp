@@ -64,7 +64,14 @@ struct PoaTask {
   DGraphRef dg;
   uint8_t* d_static = nullptr;    // the task's reads (padded) + path offsets + node paths
   size_t static_bytes = 0;
+  size_t static_po = 0;           // path offsets' byte offset in d_static
+  bool static_up = false;         // d_static reserved, its image not yet uploaded
   size_t dg_bytes = 0;            // the graph block's allocation size
+  // a larger graph block reserved for this launch's fold (reserve_blocks),
+  // the current one moved into it by the launch
+  uint8_t* grow_blk = nullptr;
+  uint32_t grow_cv = 0, grow_ce = 0;
+  size_t grow_bytes = 0;
   std::vector<uint64_t> seq_at;   // byte offset of read k in d_static (its first base)
   uint32_t* d_path_off = nullptr; // non-empty reads + 1 offsets into d_paths
   uint32_t* d_paths = nullptr;

@@ -79,7 +79,13 @@ void run_misscore(svs_context* ctx, int32_t n_pairs, const int32_t* pair_a, cons
     }
   } guard{ev};
 
-  const uint64_t budget = std::max<uint64_t>(ctx->device_budget / 2, 256ull << 20);
+  // a launch's buffers: at most half the context's budget, and at most 3/4 of
+  // the HBM free now (the POA traceback and carry buffers, sized
+  // from the same budget, never shrink, so a MisScore call after a POA run
+  // must size itself from what they left)
+  size_t free_now = 0, total_now = 0;
+  SVS_HIP(hipMemGetInfo(&free_now, &total_now));
+  const uint64_t budget = std::max<uint64_t>(std::min<uint64_t>(ctx->device_budget / 2, free_now / 4 * 3), 256ull << 20);
   size_t i = 0;
   while (i < order.size()) {
     // one launch: the largest remaining pairs that fit the budget (at least one)

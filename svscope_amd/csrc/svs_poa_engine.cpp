@@ -93,17 +93,17 @@ struct PoaTrace {
   void host(const char* what, int g, Clock::time_point a, size_t n) {
     if (f) std::fprintf(f, "host %s %d %.3f %.3f %zu\n", what, g, at(a), at(Clock::now()), n);
   }
-  // DP launches also log their kernel instance (prune, dual, wide code flags)
+  // DP launches also log their kernel instance (prune, wide code flags)
   // and the cells the kernel evaluated (tools/profile_bench_*.sh: per-row
   // counter figures of one instance)
-  void kernel(int g, hipEvent_t k0, hipEvent_t k1, size_t n, int wpj, uint64_t cells, int prune = 0, int dual = 0,
-              int wide = 0, uint64_t computed = 0) {
+  void kernel(int g, hipEvent_t k0, hipEvent_t k1, size_t n, int wpj, uint64_t cells, int prune = 0, int wide = 0,
+              uint64_t computed = 0) {
     if (!f) return;
     float a = 0.f, b = 0.f;
     SVS_HIP(hipEventElapsedTime(&a, e0, k0));
     SVS_HIP(hipEventElapsedTime(&b, e0, k1));
-    std::fprintf(f, "kern %d %.3f %.3f %zu %d %llu %d %d %d %llu\n", g, a, b, n, wpj,
-                 static_cast<unsigned long long>(cells), prune, dual, wide, static_cast<unsigned long long>(computed));
+    std::fprintf(f, "kern %d %.3f %.3f %zu %d %llu %d %d %llu\n", g, a, b, n, wpj,
+                 static_cast<unsigned long long>(cells), prune, wide, static_cast<unsigned long long>(computed));
   }
   void close() {
     if (!f) return;
@@ -265,11 +265,11 @@ void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks);
 // Waves per job of a strip launch: enough strip-pipeline waves to fill the
 // CUs, only for reads wide enough to give every wave several strips, and only
 // as many as the per-wave LDS pools of one workgroup fit; SVS_POA_WPJ overrides.
-int choose_wpj(size_t nj, uint32_t max_slots, uint32_t min_strips, bool lds_pool, bool dual) {
+int choose_wpj(size_t nj, uint32_t max_slots, uint32_t min_strips, bool lds_pool) {
   int wpj = 1;
   const char* we = std::getenv("SVS_POA_WPJ");
   const int wenv = we ? std::atoi(we) : 0;
-  if ((wenv == 1 || wenv == 2 || wenv == 4 || wenv == 8) || (wenv == 16 && lds_pool && !dual)) {
+  if ((wenv == 1 || wenv == 2 || wenv == 4 || wenv == 8) || (wenv == 16 && lds_pool)) {
     wpj = wenv;
   } else {
     // ~6 waves per SIMD (1024 SIMDs); each wave keeps >= 6 strips.  Measured
@@ -279,23 +279,9 @@ int choose_wpj(size_t nj, uint32_t max_slots, uint32_t min_strips, bool lds_pool
     // the small launches at the end of a batch: 16 waves per job (>= 2 strips
     // each), or the few remaining jobs leave most SIMDs idle
     if (lds_pool && wpj == 8 && nj < 512 && min_strips >= 32u) wpj = 16;
-    // a dual wave sweeps two strips at a time: half the waves for the same
-    // strip pipeline
-    if (dual && wpj > 1) wpj /= 2;
   }
-  const uint64_t slot_bytes = static_cast<uint64_t>(kStripSlotBytes) * (dual ? 2 : 1);
-  while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * slot_bytes > kStripLdsBytes) wpj /= 2;
+  while (lds_pool && wpj > 1 && static_cast<uint64_t>(wpj) * max_slots * kStripSlotBytes > kStripLdsBytes) wpj /= 2;
   return wpj;
-}
-
-// Strips swept in pairs (poa_strip.hip DUAL) for launches whose pools sit in
-// LDS with SVS_POA_DUAL=1.  Measured slower (profiles/r04_d2, r04_ab1: MSA
-// probe kernel 3668 vs 2903 ms, bench 205.8 vs 252.0 windows/s): a dual wave
-// does about 1.6x the cells of a single one at half the waves per CU (LDS and
-// 128 VGPRs with 81 SGPR spills), so it stays a development variant.
-bool dual_sweeps() {
-  const char* e = std::getenv("SVS_POA_DUAL");
-  return e && std::string(e) == "1";
 }
 
 void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, const PoaScore& score,
@@ -326,8 +312,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     const uint32_t ls = job_ls(tasks[la.ids[k]].seqs[tasks[la.ids[k]].next].size());
     min_strips = std::min(min_strips, ls / 64);
   }
-  const bool dual = lds_pool && dual_sweeps();
-  const int wpj = choose_wpj(nj, max_slots, min_strips, lds_pool, dual);
+  const int wpj = choose_wpj(nj, max_slots, min_strips, lds_pool);
   if (std::getenv("SVS_POA_DEBUG"))
     std::fprintf(stderr, "[svs] strip launch: %zu jobs, wpj %d, slots %u\n", nj, wpj, max_slots);
   const PruneEnv penv;
@@ -350,7 +335,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     if (J.n_slots > 31 || J.len > kPruneMaxReadLen) J.lb = kNoPrune;
     any_prune = any_prune || J.lb != kNoPrune;
     n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
-    n_bnd += round_up(round_up(J.n_rows, 8) * (J.ls / 64) * 4, 64);
+    n_bnd += round_up(round_up(J.n_rows, kCarryLineRows) * (J.ls / 64) * 4, kCarryAlignInts);
     if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 97, 64);
     n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
     max_preds = std::max(max_preds, tt.max_preds);
@@ -361,7 +346,6 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   const bool wide = max_preds > kMaxInEdgesNarrow || force_wide();
   la.code_bytes = wide ? 4 : 2;
   st.wide_launches += wide ? 1 : 0;
-  st.dual_launches += dual ? 1 : 0;
   // the pruning variant prunes every job of its launch: the others get no bound
   if (any_prune)
     for (PoaJob& J : la.jobs)
@@ -494,7 +478,6 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.lds_slots = lds_pool ? max_slots : 0;
   pl.prune = any_prune;
   pl.wide = la.code_bytes == 4;
-  pl.dual = dual;
   pl.waves_per_job = wpj;
   la.wpj = wpj;
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
@@ -661,7 +644,7 @@ struct DevLaunch {
   size_t fin_copy = 0;  // bytes of the fin buffer copied back (consensus first; MSA rows when wanted)
   int wpj = 0;
   bool timed_dp = false;
-  bool prune = false, dual = false, wide = false;  // the DP kernel instance
+  bool prune = false, wide = false;  // the DP kernel instance
 };
 
 // Task group: a disjoint subset of the active tasks with its own arena.
@@ -800,6 +783,10 @@ struct PoaScheduler::Impl {
       const long v = std::atol(e);
       if (v > 0 && static_cast<uint64_t>(v) < kSortLdsWordsMax) sort_lds_max = static_cast<uint64_t>(v);
     }
+    if (const char* e = std::getenv("SVS_POA_TEST_MAX_BLOCK_BYTES")) {
+      const long long v = std::atoll(e);
+      if (v > 0) test_block_cap = static_cast<size_t>(v);
+    }
     if (dev) {
       if (!ctx->dgraph_arena) ctx->dgraph_arena.reset(new DevArena(ctx->dgraph_budget));
       darena = ctx->dgraph_arena.get();
@@ -875,10 +862,10 @@ struct PoaScheduler::Impl {
   // A task's reads (each as the DP kernel reads it: a zero pad byte, the read,
   // zeros up to ls + 64), the path offsets of its non-empty reads and room for
   // their node paths: one block, uploaded once (through the launch's pinned
-  // staging), read by every DP and fold of the task.  plan_static lays the
-  // block out and allocates it; returns the bytes of its host image (reads +
-  // path offsets; the paths are written by the folds).
-  size_t plan_static(PoaTask& t) {
+  // staging), read by every DP and fold of the task.  layout_static lays the
+  // block out (reserve_blocks allocates it); returns the bytes of its host
+  // image (reads + path offsets; the paths are written by the folds).
+  size_t layout_static(PoaTask& t) {
     const size_t n = t.seqs.size();
     t.seq_at.assign(n, 0);
     size_t o = 64;
@@ -897,12 +884,10 @@ struct PoaScheduler::Impl {
     }
     const size_t po = round_up(o, 64), pa = round_up(po + 4ull * (n_ne + 1), 64);
     t.static_bytes = pa + 4 * path_total + 64;
-    t.d_static = static_cast<uint8_t*>(darena->alloc(t.static_bytes));
-    t.d_path_off = reinterpret_cast<uint32_t*>(t.d_static + po);
-    t.d_paths = reinterpret_cast<uint32_t*>(t.d_static + pa);
+    t.static_po = po;
     return pa;
   }
-  // The host image of plan_static's block (`bytes` of it) at h.
+  // The host image of layout_static's block (`bytes` of it) at h.
   static void write_static(const PoaTask& t, char* h, size_t bytes) {
     const size_t po = static_cast<size_t>(reinterpret_cast<const uint8_t*>(t.d_path_off) - t.d_static);
     std::memset(h, 0, bytes);
@@ -937,6 +922,9 @@ struct PoaScheduler::Impl {
   static constexpr uint64_t kSortLdsWordsMax = 160 * 1024 / 4 - 64;
   uint64_t sort_lds_max = kSortLdsWordsMax;
   uint64_t sort_lds_words(uint64_t n) const { return 2 * ((n + 31) / 32) + sort_stack; }
+  // SVS_POA_TEST_MAX_BLOCK_BYTES (tests): reserve_blocks treats a block larger
+  // than this as past the arena's limit, so that one window fails alone
+  size_t test_block_cap = ~size_t(0);
 
   // the row limit of the device table planner (SVS_POA_TEST_MAX_ROWS lowers it
   // in tests, to fail one window of a batch on purpose)
@@ -949,8 +937,92 @@ struct PoaScheduler::Impl {
   void release_dev(PoaTask& t) {
     if (t.d_static) darena->free(t.d_static, t.static_bytes);
     if (t.dg.blk) darena->free(t.dg.blk, t.dg_bytes);
+    if (t.grow_blk) darena->free(t.grow_blk, t.grow_bytes);
     t.d_static = nullptr;
     t.dg.blk = nullptr;
+    t.grow_blk = nullptr;
+    t.static_up = false;
+  }
+
+  // Device blocks this launch needs, reserved before it is packed: the reads
+  // block of each task that starts, the graph block of each first-read chain
+  // (sized for the chain and its next read's fold in the same launch), and a
+  // larger graph block wherever this launch's fold could overflow the current
+  // one.  A task whose block would take the graph arena past its limit fails
+  // alone (fail_task), and the launch goes on without it.
+  void reserve_blocks(Group& g, std::vector<uint32_t>& dp, std::vector<uint32_t>& chain,
+                      std::vector<uint32_t>& chain_seq) {
+    std::vector<uint8_t> bad(tasks.size(), 0);
+    size_t n_bad = 0;
+    auto reserve = [&](size_t bytes) -> uint8_t* {
+      if (bytes > test_block_cap) return nullptr;
+      return static_cast<uint8_t*>(darena->try_alloc(bytes));
+    };
+    std::vector<uint8_t> is_chain(tasks.size(), 0);
+    for (size_t i = 0; i < chain.size(); ++i) {
+      const uint32_t id = chain[i];
+      PoaTask& t = tasks[id];
+      is_chain[id] = 1;
+      if (!t.d_static) {
+        const size_t pa = layout_static(t);
+        t.d_static = reserve(t.static_bytes);
+        if (!t.d_static) {
+          bad[id] = 1;
+          ++n_bad;
+          continue;
+        }
+        t.d_path_off = reinterpret_cast<uint32_t*>(t.d_static + t.static_po);
+        t.d_paths = reinterpret_cast<uint32_t*>(t.d_static + pa);
+        t.static_up = true;
+      }
+      const uint32_t len = static_cast<uint32_t>(t.seqs[chain_seq[i]].size());
+      const uint32_t nxt = t.next < t.seqs.size() ? static_cast<uint32_t>(t.seqs[t.next].size()) : 0u;
+      const uint32_t cv1 = std::max(3 * len, len + 2 * nxt) + 4096;
+      const uint32_t ce1 = std::max(4 * len, len + 3 * nxt) + 4096;
+      t.dg_bytes = dgraph_layout(cv1, ce1).bytes;
+      t.dg.blk = reserve(t.dg_bytes);
+      t.dg.cv = cv1;
+      t.dg.ce = ce1;
+      if (!t.dg.blk) {
+        bad[id] = 1;
+        ++n_bad;
+      }
+    }
+    for (uint32_t id : dp) {
+      PoaTask& t = tasks[id];
+      if (is_chain[id] || bad[id]) continue;
+      const uint32_t len = static_cast<uint32_t>(t.seqs[t.next].size());
+      if (t.dg.V + len > t.dg.cv || t.dg.E + len + 1 > t.dg.ce) {
+        // a window MSA of 64 reads x 3 kb ends near 2.2 L nodes and 2.9 L
+        // edges: the first block holds that, larger graphs double
+        t.grow_cv = std::max<uint32_t>(2 * t.dg.cv, t.dg.V + 3 * len + 4096);
+        t.grow_ce = std::max<uint32_t>(2 * t.dg.ce, t.dg.E + 4 * len + 4096);
+        t.grow_bytes = dgraph_layout(t.grow_cv, t.grow_ce).bytes;
+        t.grow_blk = reserve(t.grow_bytes);
+        if (!t.grow_blk) {
+          bad[id] = 1;
+          ++n_bad;
+        }
+      }
+    }
+    if (!n_bad) return;
+    auto drop = [&](std::vector<uint32_t>& v, std::vector<uint32_t>* w) {
+      size_t o = 0;
+      for (size_t i = 0; i < v.size(); ++i)
+        if (!bad[v[i]]) {
+          if (w) (*w)[o] = (*w)[i];
+          v[o++] = v[i];
+        }
+      v.resize(o);
+      if (w) w->resize(o);
+    };
+    for (uint32_t id = 0; id < tasks.size(); ++id)
+      if (bad[id])
+        fail_task(g, id, "the device graph arena is full: this task's graph block would pass its limit of " +
+                             std::to_string(darena->limit()) + " bytes (SVS_DEVICE_BUDGET_GB, fewer tasks in flight)");
+    drop(dp, nullptr);
+    drop(chain, &chain_seq);
+    drop(g.active, nullptr);
   }
 
   // Prepares the group's next device launch, completing the tasks with nothing
@@ -1055,6 +1127,8 @@ struct PoaScheduler::Impl {
         total += b;
       }
       dp.resize(fit);
+      reserve_blocks(g, dp, chain, chain_seq);
+      if (dp.empty() && chain.empty()) continue;  // every task of the launch failed alone
       const auto tp0 = Clock::now();
       pack_and_launch_dev(g, dp, chain, chain_seq);
       g_trace.host("pack", gid(g), tp0, dp.size() + chain.size());
@@ -1088,26 +1162,17 @@ struct PoaScheduler::Impl {
     std::vector<std::pair<size_t, PoaTask*>> uploads;  // staging offset (from s_up), task
     std::vector<size_t> up_bytes;
     size_t up_total = 0;
+    // (the reads blocks and the chains' graph blocks were reserved by
+    // reserve_blocks)
     for (uint32_t id : D.fold_ids)
-      if (!tasks[id].d_static) {
-        const size_t b = plan_static(tasks[id]);
-        uploads.emplace_back(up_total, &tasks[id]);
+      if (tasks[id].static_up) {
+        PoaTask& t = tasks[id];
+        t.static_up = false;
+        const size_t b = static_cast<size_t>(reinterpret_cast<uint8_t*>(t.d_paths) - t.d_static);
+        uploads.emplace_back(up_total, &t);
         up_bytes.push_back(b);
         up_total += round_up(b, 64);
       }
-    // a fresh block for each chain, sized for the chain and its next read's
-    // fold in this same launch
-    for (size_t i = 0; i < npre; ++i) {
-      PoaTask& t = tasks[D.fold_ids[i]];
-      const uint32_t len = static_cast<uint32_t>(t.seqs[D.fold_seq[i]].size());
-      const uint32_t nxt = t.next < t.seqs.size() ? static_cast<uint32_t>(t.seqs[t.next].size()) : 0u;
-      const uint32_t cv1 = std::max(3 * len, len + 2 * nxt) + 4096;
-      const uint32_t ce1 = std::max(4 * len, len + 3 * nxt) + 4096;
-      t.dg_bytes = dgraph_layout(cv1, ce1).bytes;
-      t.dg.blk = static_cast<uint8_t*>(darena->alloc(t.dg_bytes));
-      t.dg.cv = cv1;
-      t.dg.ce = ce1;
-    }
     // DP jobs: the tables the last fold exported, in the task's block
     D.jobs.assign(nj, PoaJob{});
     uint64_t n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
@@ -1123,8 +1188,7 @@ struct PoaScheduler::Impl {
       min_strips = std::min(min_strips, strip_ls(static_cast<uint32_t>(t.seqs[t.next].size())) / 64);
     }
     const bool lds_pool = max_slots <= kStripMaxLdsSlots && !strip_pool_forced_global();
-    const bool dual = lds_pool && dual_sweeps();
-    const int wpj = nj ? choose_wpj(nj, max_slots, min_strips, lds_pool, dual) : 1;
+    const int wpj = nj ? choose_wpj(nj, max_slots, min_strips, lds_pool) : 1;
     const PruneEnv penv;
     for (size_t k = 0; k < nj; ++k) {
       const PoaTask& t = tasks[dp[k]];
@@ -1153,7 +1217,7 @@ struct PoaScheduler::Impl {
       if (J.n_slots > 31 || J.len > kPruneMaxReadLen) J.lb = kNoPrune;
       any_prune = any_prune || J.lb != kNoPrune;
       n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
-      n_bnd += round_up(round_up(J.n_rows, 8) * (J.ls / 64) * 4, 64);
+      n_bnd += round_up(round_up(J.n_rows, kCarryLineRows) * (J.ls / 64) * 4, kCarryAlignInts);
       if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 97, 64);
       n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
       st.dp_cells += static_cast<uint64_t>(J.n_rows + 1) * (J.len + 1);
@@ -1164,10 +1228,8 @@ struct PoaScheduler::Impl {
     D.n_aln = n_aln;
     D.wpj = wpj;
     D.prune = any_prune;
-    D.dual = dual;
     D.wide = wide;
     st.wide_launches += wide ? 1 : 0;
-    st.dual_launches += (dual && nj) ? 1 : 0;
     // (hints: the carries are 16 B per 64 traceback codes, the pairs 8 B per
     // row and read base; sized once for the group's budget instead of growing
     // with the graphs)
@@ -1229,23 +1291,19 @@ struct PoaScheduler::Impl {
         if (last) final_outputs(i, t, F, len, 1);
         continue;
       }
-      if (t.dg.V + len > t.dg.cv || t.dg.E + len + 1 > t.dg.ce) {
-        // a window MSA of 64 reads x 3 kb ends near 2.2 L nodes and 2.9 L
-        // edges: the first block holds that, larger graphs double
-        const uint32_t cv1 = std::max<uint32_t>(2 * t.dg.cv, t.dg.V + 3 * len + 4096);
-        const uint32_t ce1 = std::max<uint32_t>(2 * t.dg.ce, t.dg.E + 4 * len + 4096);
-        const size_t bytes = dgraph_layout(cv1, ce1).bytes;
-        uint8_t* nb = static_cast<uint8_t*>(darena->alloc(bytes));
-        if (t.dg.blk) {
-          moves.push_back({reinterpret_cast<uint64_t>(t.dg.blk), t.dg.cv, t.dg.ce, reinterpret_cast<uint64_t>(nb), cv1,
-                           ce1, t.dg.V, t.dg.E, t.dg.par});
-          D.old_blocks.emplace_back(t.dg.blk, t.dg_bytes);
-          D.moved[i] = 1;
-        }
+      if (t.grow_blk) {
+        // the larger block reserve_blocks took for this fold
+        uint8_t* nb = t.grow_blk;
+        const uint32_t cv1 = t.grow_cv, ce1 = t.grow_ce;
+        moves.push_back({reinterpret_cast<uint64_t>(t.dg.blk), t.dg.cv, t.dg.ce, reinterpret_cast<uint64_t>(nb), cv1,
+                         ce1, t.dg.V, t.dg.E, t.dg.par});
+        D.old_blocks.emplace_back(t.dg.blk, t.dg_bytes);
+        D.moved[i] = 1;
         t.dg.blk = nb;
         t.dg.cv = cv1;
         t.dg.ce = ce1;
-        t.dg_bytes = bytes;
+        t.dg_bytes = t.grow_bytes;
+        t.grow_blk = nullptr;
       }
       F.blk = t.dg.blk;
       F.cv = t.dg.cv;
@@ -1376,8 +1434,7 @@ struct PoaScheduler::Impl {
       pl.lds_slots = lds_pool ? max_slots : 0;
       pl.prune = any_prune;
       pl.wide = wide;
-      pl.dual = dual;
-      pl.waves_per_job = wpj;
+          pl.waves_per_job = wpj;
       // the pool slots per wave the launch's LDS is sized for (its occupancy)
       g_trace.host("slots", gid(g), Clock::now(), pl.lds_slots);
       SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
@@ -1479,7 +1536,7 @@ struct PoaScheduler::Impl {
       uint64_t computed = 0;
       const int32_t* al = A.h_alen.as<int32_t>();
       for (size_t k = 0; k < nj; ++k) computed += 64ull * static_cast<uint32_t>(al[2 * nj + k]);
-      if (D.timed_dp) g_trace.kernel(gid(g), A.ev0, A.ev1, nj, D.wpj, cells, D.prune, D.dual, D.wide, computed);
+      if (D.timed_dp) g_trace.kernel(gid(g), A.ev0, A.ev1, nj, D.wpj, cells, D.prune, D.wide, computed);
       g_trace.kernel(10 + gid(g), A.evf0, A.evf1, nj, 0, 0);  // the fold chain after the DP kernel
       if (D.n_pre) g_trace.kernel(20 + gid(g), A.evp, A.evp1, D.n_pre, 0, 0);  // the chains before it
     }

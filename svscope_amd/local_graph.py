@@ -263,12 +263,10 @@ def _dist_setup():
     import torch.distributed as dist
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = torch.cuda.is_available()
-    # SVS_DIST_BACKEND=gloo with SVS_DEVICE=d (tests on a one-GPU box): every
-    # rank's engine on GPU d, the record gather over gloo on the host
     backend = os.environ.get("SVS_DIST_BACKEND") or ("nccl" if gpu else "gloo")
     device = torch.device("cpu")
     if gpu:
-        ordinal = int(os.environ.get("SVS_DEVICE", local))
+        ordinal = rank_device(backend, local, os.environ)
         torch.cuda.set_device(ordinal)
         os.environ["SVS_DEVICE"] = str(ordinal)
         if backend == "nccl":
@@ -278,9 +276,25 @@ def _dist_setup():
     return world, rank, dist, device
 
 
+def rank_device(backend, local, env):
+    """The GPU of this rank's engine (and, under nccl, its communicator):
+    LOCAL_RANK.  Only with SVS_DIST_BACKEND=gloo (tests on a one-GPU box) does
+    SVS_DEVICE=d put every rank's engine on GPU d, the records gathered over
+    gloo on the host.  Under nccl a stale exported SVS_DEVICE would put every
+    rank on one GPU, which RCCL rejects: it is ignored there, with
+    a warning when it names another GPU."""
+    dev = env.get("SVS_DEVICE")
+    if backend == "gloo" and dev is not None:
+        return int(dev)
+    if dev is not None and int(dev) != local:
+        log.warning("SVS_DEVICE=%s ignored under %s: rank with LOCAL_RANK %d uses GPU %d", dev, backend, local, local)
+    return local
+
+
 def _finish(path, lines_by_rank, rank, world, dist, device, finished, t0, what):
-    """Multi-rank: gather every rank's journalled lines to rank 0 (one RCCL
-    all_gather), then rank 0 sorts the output like sort -k1,1 -k2,2n."""
+    """Multi-rank: gather every rank's journalled lines to rank 0 (an 8-B
+    all_gather of the sizes, then one RCCL gather to rank 0), then rank 0
+    sorts the output like sort -k1,1 -k2,2n."""
     if dist is not None:
         lines = gather_lines(lines_by_rank, device)
         if rank == 0:

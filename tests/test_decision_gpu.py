@@ -291,6 +291,28 @@ def test_unbenched_paths_match_oracle_digests(name, batch):
         assert st["poa"]["prune_retries"] > 0, st["poa"]
 
 
+def test_session_reproduces_reference_records_at_baseline_sizes():
+    """the HIP session's records equal the reference's own
+    DecisionMaker.Decision records (tests/golden/reference_path_goldens.json,
+    gen_reference_path_goldens.py: the reference's code run in the build
+    container with the oracle POA standing in for pyspoa) for 16 config-3
+    windows (64 reads x 3 kb), 16 config-2 windows (32 x 2 kb) and 4 windows of
+    the harsh pruning profile, all in one streaming session."""
+    from svscope_amd import synth
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_path_goldens.json")))
+    rows, want = [], []
+    for w in ref["windows"]:
+        s = ref["sets"][w["set"]]
+        kw = {k: tuple(v) if isinstance(v, list) else v for k, v in s["make_window_kw"].items()}
+        rows.append(synth.make_window(w["window"], s["reads"], s["ref_len"], **kw))
+        want.append(w["digest"])
+    assert len(rows) == 36
+    digests, _ = _session_digests(rows, 12)
+    bad = [(ref["windows"][k]["set"], ref["windows"][k]["window"]) for k, (a, b) in enumerate(zip(digests, want))
+           if a != b]
+    assert not bad, f"windows differ from the reference's records: {bad}"
+
+
 def test_big_windows_mixed_into_config3_batch_match_oracle():
     """windows past the 64-read configs, a 600-read one
     (300 tumor + 300 normal, 1.2 kb) and a 320-read one (2 kb), mixed into a
@@ -322,15 +344,19 @@ def test_big_windows_mixed_into_config3_batch_match_oracle():
 
 
 @pytest.mark.parametrize("env,why", [({"SVS_POA_TEST_MAX_ROWS": "4000"}, "planner"),
-                                     ({"SVS_POA_TEST_SORT_LDS_WORDS": "1300"}, "sort kernel")])
+                                     ({"SVS_POA_TEST_SORT_LDS_WORDS": "1300"}, "sort kernel"),
+                                     ({"SVS_POA_TEST_MAX_BLOCK_BYTES": "2000000"}, "graph arena is full")])
 def test_window_past_an_engine_limit_fails_alone(env, why):
     """a window that goes past an engine limit fails alone
     (status SVS_DEC_FAILED, decision_maker.WindowFailed naming it) while the
     other windows of its batch and of the session get the oracle's records.
     The device planner's row limit (SVS_POA_TEST_MAX_ROWS), or the LDS the
     sort kernel's node flags may take (SVS_POA_TEST_SORT_LDS_WORDS, ADVICE
-    r03: a graph past it used to fail the whole launch), is lowered for the
-    test so that one 64-read x 3 kb window crosses it."""
+    r03: a graph past it used to fail the whole launch), or the largest graph
+    block the device arena hands out (SVS_POA_TEST_MAX_BLOCK_BYTES: the path a
+    block past the arena's byte limit takes, ADVICE r04: it used to abort the
+    session), is lowered for the test so that one 64-read x 3 kb window
+    crosses it."""
     from svscope_amd import synth
     from svscope_amd.decision_maker import DecisionSession, WindowFailed
     from svscope_amd.local_graph import _window, record_line

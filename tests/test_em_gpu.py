@@ -49,6 +49,26 @@ def test_em_matches_reference_goldens(em_mode):
         np.testing.assert_allclose(r["theta"].sum(axis=(1, 2)), gold[p + "theta_sum"], rtol=1e-9)
 
 
+def test_em_matches_reference_emcluster_at_config3_size(em_mode):
+    """the GPU EM on the seqdatamx the reference's own
+    MSAFeatureSelection produced for 16 config-3 windows (64 reads,
+    1375-2052 features) gives the reference EMCluster's K and labels exactly
+    and its BICList within 1e-5 (reference_path_goldens.json,
+    gen_reference_path_goldens.py; ReadsCluster.py:221-277)."""
+    import json
+    from svscope_amd.reads_cluster import em_cluster_batch
+    gdir = os.path.dirname(GOLD)
+    ref = json.load(open(os.path.join(gdir, "reference_path_goldens.json")))
+    z = np.load(os.path.join(gdir, "reference_em_inputs.npz"))
+    wins = [w for w in ref["windows"] if w["set"] == "config3" and "K" in w]
+    assert len(wins) == 16
+    got = em_cluster_batch([z[f"config3_{w['window']}"].astype(np.int64) for w in wins])
+    for w, r in zip(wins, got):
+        assert r["K"] == w["K"], w["window"]
+        np.testing.assert_array_equal(r["Rclust"], w["Rclust"])
+        np.testing.assert_allclose(r["BICList"], w["BICList"], rtol=1e-9, atol=1e-5)
+
+
 def test_em_matches_oracle_random_and_reinit_heavy(em_mode):
     """Random and re-initialisation-heavy windows against the oracle.  Four
     of them re-initialise at two or more K values (windows 0, 8, 9 and 12),

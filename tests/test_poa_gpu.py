@@ -92,11 +92,7 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_WPJ": "2"},
     {"SVS_POA_WPJ": "4"},
     {"SVS_POA_WPJ": "8"},
-    {"SVS_POA_DUAL": "1"},
-    {"SVS_POA_DUAL": "1", "SVS_POA_WPJ": "1"},
-    {"SVS_POA_DUAL": "1", "SVS_POA_WPJ": "2"},
-    {"SVS_POA_DUAL": "1", "SVS_POA_PRUNE_SLACK": "0", "SVS_POA_WPJ": "8"},
-    {"SVS_POA_DUAL": "1", "SVS_POA_PRUNE": "0"},
+    {"SVS_POA_WPJ": "16"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "1"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "4"},
     {"SVS_POA_PRUNE": "0"},
@@ -112,12 +108,10 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_HOST_GRAPH": "1"},
     {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_VERIFY_PREP": "1"},
     {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_VERIFY_PREP": "1", "SVS_POA_PRUNE_SLACK": "-0.3"},
-    {"SVS_POA_HOST_GRAPH": "1", "SVS_POA_DUAL": "1", "SVS_POA_PRUNE_SLACK": "-0.3"},
 ])
 def test_kernel_variants_match_oracle(env):
     """Every POA kernel instance the engine selects gives the oracle's result:
-    strips swept one at a time (the default) and in pairs (SVS_POA_DUAL=1),
-    1/2/4/8/16 (pairs: 1/2/4/8) pipelined waves per job, the
+    1/2/4/8/16 pipelined waves per job, the
     pool in global memory, and the exact pruning off, at its tightest slack,
     and with a bound above the optimum (every pruned job retried: with the
     looser retry slack, unpruned, or twice, the second time unpruned; with
@@ -152,7 +146,6 @@ def test_kernel_variants_match_oracle(env):
     {"SVS_POA_WPJ": "2"},
     {"SVS_POA_WPJ": "4"},
     {"SVS_POA_WPJ": "8"},
-    {"SVS_POA_DUAL": "1", "SVS_POA_WPJ": "2"},
     {"SVS_POA_STRIP_GLOBAL_POOL": "1", "SVS_POA_WPJ": "4"},
 ])
 def test_short_graph_strip_handoff(env):

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Counters of the DP kernel instances of the driver's timed region,
-# poa_strip_kernel<true, WPJ, true, unsigned short, false> (LDS pools, WPJ waves
+# poa_strip_kernel<true, WPJ, true, unsigned short> (LDS pools, WPJ waves
 # per job, pruning, 16-bit codes, single sweep) for WPJ 4, 8 and 16, on the
 # driver's shape: bench.py
 # with 512-window steps (--steps 4 --warmup 1).  Two SQ passes (8 counters
@@ -38,17 +38,17 @@ out, steps = sys.argv[1], int(sys.argv[2])
 
 def name(wpj):
     """an instance, or (wpj None) every DP kernel instance"""
-    return "poa_strip_kernel<" if wpj is None else f"poa_strip_kernel<true, {wpj}, true, unsigned short, false>"
+    return "poa_strip_kernel<" if wpj is None else f"poa_strip_kernel<true, {wpj}, true, unsigned short>"
 
 
 def cells(p, wpj):
-    """cells computed and launches of an instance (trace: kern g a b n wpj cells prune dual wide computed)"""
+    """cells computed and launches of an instance (trace: kern g a b n wpj cells prune wide computed)"""
     c = n = 0
     for line in open(f"{out}/{p}.trace"):
         f = line.split()
-        if f and f[0] == "kern" and len(f) >= 11 and int(f[1]) < 10 and (
-                wpj is None or (f[5] == str(wpj) and f[7] == "1" and f[8] == "0" and f[9] == "0")):
-            c += int(f[10])
+        if f and f[0] == "kern" and len(f) >= 10 and int(f[1]) < 10 and (
+                wpj is None or (f[5] == str(wpj) and f[7] == "1" and f[8] == "0")):
+            c += int(f[9])
             n += 1
     return c, n
 
