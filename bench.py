@@ -369,10 +369,6 @@ def main():
             "ranks": ranks,
             "breakdown": {"poa_cells": cells, "poa_cells_computed": cells_done,
                           "prune_retries": poa["prune_retries"],
-                          # traceback code pages the DP launches took (poa_strip.hip paging),
-                          # and jobs re-run because a launch's page pool ran out
-                          "tb_pages_gb": round(poa.get("tb_bytes", 0) / 1e9, 2),
-                          "tb_retries": poa.get("tb_retries", 0),
                           # HIP events between the kernels on each group's fold stream
                           # (device-resident graphs), timed steps only; they run beside
                           # the other group's DP kernel

@@ -50,7 +50,7 @@ typedef struct svs_poa_stats {
   uint64_t dp_cells;        /* sum over alignments of (|V|+1)*(L+1) */
   uint64_t alignments;      /* read-vs-graph DP jobs executed on the GPU */
   uint64_t launches;        /* kernel launches */
-  uint64_t tb_bytes;        /* traceback-code pages taken (bytes, HBM; poa_strip.hip paging) */
+  uint64_t tb_bytes;        /* traceback-code bytes written (HBM) */
   uint64_t pool_bytes;      /* row-pool bytes written (H,F,O planes) */
   uint64_t h2d_bytes, d2h_bytes;
   double kernel_ms;         /* sum of per-launch durations (HIP events) */
@@ -75,7 +75,6 @@ typedef struct svs_poa_stats {
      task blocks live at once, and the HBM the arena holds (hipMalloc'ed chunks;
      never returned before svs_release) */
   uint64_t dgraph_peak_bytes, dgraph_reserved_bytes;
-  uint64_t tb_retries;      /* DP jobs re-run because the launch's traceback page pool ran out */
 } svs_poa_stats;
 
 /* One context per host thread; owns a HIP stream and device arenas. */

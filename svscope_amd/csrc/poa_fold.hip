@@ -215,7 +215,7 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
   int32_t n = 0;
   if (!(J.flags & kFoldChain)) {
     n = *glb(J.aln_status);
-    if (n == kPruneRetry || n == kTbRetry) {
+    if (n == kPruneRetry) {
       if (lane == 0) res->status = kFoldSkipped;
       return;
     }

@@ -271,8 +271,7 @@ template <bool LDSP, int WPJ, bool PRUNE, class CodeT>
 #define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? SVS_PRUNE_OCC : 1)))
 __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore Parg,
-    CodeT* __restrict__ tb, uint32_t* __restrict__ pt_all, uint32_t pg_cap,
-    int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
+    CodeT* __restrict__ tb, int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
     int32_t* __restrict__ gpool, int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
   extern __shared__ int32_t lds[];
   using TF = TbFmt<CodeT>;
@@ -280,7 +279,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   SVS_SP_DECL;
   __shared__ int32_t prog[WPJ];  // per wave: strip * (V + 1) + rows done, carries published
   __shared__ int32_t s_err;
-  __shared__ int32_t s_tbov;  // some wave ran out of traceback pages (the job returns kTbRetry)
   __shared__ int32_t s_brow[WPJ], s_best[WPJ];
   __shared__ uint32_t s_rows[WPJ];
   const int lane = threadIdx.x & 63;
@@ -301,20 +299,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   int32_t* __restrict__ pool;  // this wave's pool: nslot x {H, F, O} x 64, then nslot boundary H
   if constexpr (LDSP) pool = lds + static_cast<uint32_t>(wave) * nslot * kStride;
   else pool = gpool + J.pool_off + static_cast<uint64_t>(wave) * ((nslot * kSlotInts + 63) / 64 * 64);
-  // Traceback codes in pages (kTbPageRows rows x 64 columns of one strip,
-  // rows contiguous) from the launch's page pool: only row groups a sweep
-  // computes get a page, so a launch's codes take the pruned band's bytes,
-  // not the full matrix's.  pt: the job's page table, NP entries per strip
-  // (kNoPage: never computed).  Pages come from the pool's counter in chunks
-  // of kTbChunkPages per wave (the counter is the word after the launch's
-  // aln_len triples); a wave that finds the pool empty writes into the spare
-  // page at pg_cap instead and the job returns kTbRetry (the host runs it
-  // again with its full matrix reserved).
-  uint32_t* __restrict__ pt = pt_all + J.pt_off;
-  const uint32_t NP = (V + kTbPageRows - 1) / kTbPageRows;
-  // the wave's next page; chunks start at multiples of kTbChunkPages, so a
-  // multiple means the chunk is used up (0: none yet)
-  uint32_t ch_next = 0;
+  CodeT* __restrict__ tbj = tb + J.tb_off;
   const TBL uint32_t* __restrict__ rec = tbl(J.rec);
   const TBL uint32_t* __restrict__ rps = tbl(J.pstart);
   const TBL uint32_t* __restrict__ prow = tbl(J.pred);
@@ -364,30 +349,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const int32_t j0 = s << 6;
     const int32_t j = j0 + lane;
     const uint8_t rc = seq[j - 1];  // seq[-1] is a zero pad byte (column 0)
-    // this strip's page table column: no page until a row of the group is
-    // computed (the stores land before any lane 0 entry below)
-    for (uint32_t p = static_cast<uint32_t>(lane); p < NP; p += 64) pt[static_cast<uint32_t>(s) * NP + p] = kNoPage;
-    wait_vm_stores();
-    uint32_t cur_pg = kNoPage;       // row group of the current page
-    CodeT* __restrict__ pgc = tb;    // its first code (scalar)
-    auto page_of = [&](uint32_t g) {
-      if (ch_next % kTbChunkPages == 0) {
-        uint32_t old = 0;
-        if (lane == 0)
-          old = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(aln_len + 3 * n_jobs), kTbChunkPages,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ch_next = __builtin_amdgcn_readfirstlane(old);
-      }
-      uint32_t pg = ch_next++;
-      if (pg >= pg_cap) {
-        pg = pg_cap;  // the spare page: this job's codes are incomplete
-        if (lane == 0) __hip_atomic_store(&s_tbov, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else if (lane == 0) {
-        pt[static_cast<uint32_t>(s) * NP + g] = pg;
-      }
-      cur_pg = g;
-      pgc = tb + static_cast<uint64_t>(pg) * (kTbPageRows * 64);
-    };
+    CodeT* __restrict__ tbl = tbj + j;  // this lane's column of the traceback codes
     const GLB int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
     int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;
     const int32_t pw = (wave + WPJ - 1) % WPJ;          // producer of strip s-1
@@ -695,8 +657,9 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
         const bool lbit = inner && (prevH + P.g == E || prevH + P.q == Q);
         code = assemble_code<TF>(diag_k, up_k, up_ext, la || lb || lc || ld, la || (!lb && lc), lbit, uc_k, uc_stop);
       }
-      if (r / kTbPageRows != cur_pg) page_of(r / kTbPageRows);
-      pgc[(r % kTbPageRows) * 64 + static_cast<uint32_t>(lane)] = static_cast<CodeT>(code);
+      // 32-bit row offset off this lane's column: the host keeps n_rows x ls
+      // below 2^31 per job
+      tbl[r * LS] = static_cast<CodeT>(code);
       bool any_alive = true;
       if (prune) {
         const int32_t ub = ub_of(w2w3.x, rrem, mrr);
@@ -855,15 +818,9 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
   if (WPJ > 1) {
     if (lane == 0) {
       prog[wave] = -1;
-      if (wave == 0) {
-        s_err = 0;
-        s_tbov = 0;
-      }
+      if (wave == 0) s_err = 0;
     }
     __syncthreads();
-  } else {
-    if (lane == 0) s_tbov = 0;
-    __builtin_amdgcn_wave_barrier();
   }
   if (V > 0) {
     using TrueT = std::integral_constant<bool, true>;
@@ -932,10 +889,6 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     if (lane == 0) aln_len[job_id] = kPruneRetry;
     return;
   }
-  if (__hip_atomic_load(&s_tbov, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-    if (lane == 0) aln_len[job_id] = kTbRetry;
-    return;
-  }
   int32_t t_r = INT32_MIN / 2, t_c = INT32_MIN / 2, p_r = INT32_MIN / 2;
   uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;  // element e = 64 v + lane: (t_r - e / 16, t_c - e % 16)
   int32_t pn = 0, p0 = 0, p1 = 0;           // lane l: in-edge count and in-edges 0, 1 of row p_r - l
@@ -945,22 +898,13 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
       t_r = row;
       t_c = col;
       const int32_t cc = col - (lane & 15), r0 = row - (lane >> 4);
-      // a cell's page from the strip's page table, then its code (cells in
-      // row groups never computed read as 0: off the path by construction)
-      auto pg = [&](int32_t rr) -> uint32_t {
-        return (rr >= 1 && cc >= 0) ? pt[static_cast<uint32_t>(cc >> 6) * NP + static_cast<uint32_t>(rr - 1) / kTbPageRows]
-                                    : kNoPage;
+      auto ld = [&](int32_t rr) -> uint32_t {
+        return (rr >= 1 && cc >= 0) ? tbj[static_cast<uint64_t>(rr - 1) * LS + cc] : 0u;
       };
-      auto ld = [&](int32_t rr, uint32_t p) -> uint32_t {
-        return p < pg_cap ? tb[static_cast<uint64_t>(p) * (kTbPageRows * 64) +
-                               (static_cast<uint32_t>(rr - 1) % kTbPageRows) * 64 + static_cast<uint32_t>(cc & 63)]
-                          : 0u;
-      };
-      const uint32_t q0 = pg(r0), q1 = pg(r0 - 4), q2 = pg(r0 - 8), q3 = pg(r0 - 12);
-      t0 = ld(r0, q0);
-      t1 = ld(r0 - 4, q1);
-      t2 = ld(r0 - 8, q2);
-      t3 = ld(r0 - 12, q3);
+      t0 = ld(r0);
+      t1 = ld(r0 - 4);
+      t2 = ld(r0 - 8);
+      t3 = ld(r0 - 12);
       return __builtin_amdgcn_readfirstlane(t0);
     }
     const uint32_t e = dr * 16 + dc, l = e & 63u, v = e >> 6;
@@ -1013,10 +957,10 @@ hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   const int w = a.waves_per_job;
   const bool lds_pool = a.lds_slots > 0;
   const size_t lds = lds_pool ? static_cast<size_t>(w) * a.lds_slots * kStripSlotBytes : 0;
-#define SVS_STRIP4(LP, W, PR, CT)                                                                              \
-  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR, CT>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs,     \
-                     a.n_jobs, a.score, static_cast<CT*>(a.tb), a.pt, a.pg_cap, a.bnd, a.bnd, a.pool,           \
-                     a.aln, a.aln_len, a.lds_slots)
+#define SVS_STRIP4(LP, W, PR, CT)                                                                          \
+  hipLaunchKernelGGL((poa_strip_kernel<LP, W, PR, CT>), dim3(a.n_jobs), dim3(64 * W), lds, stream, a.jobs, \
+                     a.n_jobs, a.score, static_cast<CT*>(a.tb), a.bnd, a.bnd, a.pool, a.aln, a.aln_len,     \
+                     a.lds_slots)
 #define SVS_STRIP3(LP, W, PR)              \
   do {                                     \
     if (a.wide) {                          \

@@ -95,24 +95,23 @@ int svs_init(int device_ordinal, svs_context** out) {
     SVS_HIP(hipEventCreate(&ctx->ev_rerun));
     size_t free_b = 0, total_b = 0;
     SVS_HIP(hipMemGetInfo(&free_b, &total_b));
-    // the launches' traceback pages and strip carries: 3/8 of the free HBM
-    // (about 100 GB of an MI355X; per task group two thirds pages, a third
-    // carries).  Since the codes are paged (round 5: only row groups a strip
-    // computes take a page, about 8 MB for a config-3 alignment at the end of
-    // a window MSA instead of its full 40 MB matrix), a group's launch of
-    // several thousand alignments fits, and the device-resident graphs get the
-    // rest of the HBM less 4 GiB (below).  Round 4 gave the full-matrix codes
-    // 5/8 (profiles/r04_h9)
-    size_t budget = free_b / 8 * 3;
+    // the launches' traceback codes and carries: 5/8 of the free HBM (180 GB
+    // of an MI355X), so that a group's launch holds 2048 config-3 alignments
+    // (about 40 MB of codes each at the end of a window MSA); the graph arena
+    // gets the rest less the carries and 4 GiB (below).  Driver-shape A/B,
+    // profiles/r04_h9: 352.5 / 350.9 windows/s at 180 GB and 2048 tasks per
+    // group against 334 at half the free HBM and 1792
+    size_t budget = free_b / 8 * 5;
     if (const char* s = std::getenv("SVS_DEVICE_BUDGET_GB")) {
       const double gb = std::atof(s);
       if (gb > 0) budget = static_cast<size_t>(gb * (1ull << 30));
     }
     ctx->device_budget = std::max<size_t>(budget, 64ull << 20);
     // the device-resident POA graphs get what the launch buffers leave of the
-    // free HBM (the traceback pages and carries, svs_poa_engine.cpp), less
-    // 4 GiB for the EM and MisScore buffers and HIP itself
-    const size_t used = ctx->device_budget + (4ull << 30);
+    // free HBM (the traceback budget, and the carry buffers sized at an eighth
+    // of it, svs_poa_engine.cpp), less 4 GiB for the EM and MisScore buffers
+    // and HIP itself
+    const size_t used = ctx->device_budget + ctx->device_budget / 8 + (4ull << 30);
     const size_t rest = free_b > used ? free_b - used : 0;
     ctx->dgraph_budget = std::max<size_t>(rest, 1ull << 30);
     ctx->pool = new svs::ThreadPool(host_threads());

@@ -131,7 +131,7 @@ struct PinnedBuf {
 // the group's own copy stream carries its H2D tables and D2H alignments, so
 // they overlap the other group's kernel.
 struct PoaArena {
-  DeviceBuf d_in, d_tb, d_pt, d_pool, d_aln, d_alen;  // d_tb: traceback pages, d_pt: their tables
+  DeviceBuf d_in, d_tb, d_pool, d_aln, d_alen;
   PinnedBuf h_in, h_aln, h_alen;
   // device-resident graphs: the launch's job / fold descriptors and fold
   // results, and the finished tasks' consensus + MSA rows
@@ -180,7 +180,7 @@ struct PoaArena {
   ~PoaArena() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
-    for (DeviceBuf* b : {&d_in, &d_tb, &d_pt, &d_pool, &d_aln, &d_alen, &d_desc, &d_fin}) b->release();
+    for (DeviceBuf* b : {&d_in, &d_tb, &d_pool, &d_aln, &d_alen, &d_desc, &d_fin}) b->release();
     for (PinnedBuf* b : {&h_in, &h_aln, &h_alen, &h_desc, &h_fin, &h_feat}) b->release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);

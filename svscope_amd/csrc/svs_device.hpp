@@ -21,7 +21,7 @@ struct PoaJob {
   const int32_t* col0;    // H, F, O of DP column 0 per row
   const uint8_t* seq;     // the read; seq[-1] is a zero pad byte, region ls + 64 bytes
   const uint32_t* info;   // prep jobs: per-row words (export_strip_lite)
-  uint64_t pt_off;        // the job's traceback page table (uint32 entries, NP per strip)
+  uint64_t tb_off;        // uint16 traceback codes, rows 1..n_rows, stride ls
   uint64_t bnd_off;       // int32 strip-boundary carries
   uint64_t pool_off;      // int32 global row pool (pools that do not fit LDS)
   uint64_t aln_off;       // output pairs (2 x int32), capacity n_rows + len + 1
@@ -42,31 +42,12 @@ constexpr int32_t kPruneAll = INT32_MIN / 4;
 // aln_len[job] for a pruned job whose best sink score fell below its bound
 // (the bound was not a lower bound of the optimum: run it again unpruned).
 constexpr int32_t kPruneRetry = -2;
-// aln_len[job] for a job that found the launch's traceback page pool empty:
-// run it again, with its full matrix of pages reserved.
-constexpr int32_t kTbRetry = -3;
-
-// Traceback code pages of the strip kernel (poa_strip.hip): kTbPageRows rows
-// x 64 columns of one strip each, taken from the launch's pool kTbChunkPages
-// at a time per wave; page-table entries of row groups never computed hold
-// kNoPage.
-constexpr uint32_t kTbPageRows = 16;
-constexpr uint32_t kTbChunkPages = 8;
-constexpr uint32_t kNoPage = 0xFFFFFFFFu;
-// Pages of a job: strips x row groups (the page-table size), all of them
-// when every row is computed.
-inline uint64_t tb_table_pages(uint32_t n_rows, uint32_t ls) {
-  return static_cast<uint64_t>(ls / 64) * ((n_rows + kTbPageRows - 1) / kTbPageRows);
-}
 
 struct PoaLaunch {
   const PoaJob* jobs;
   int n_jobs;
   PoaScore score;
-  void* tb;              // traceback code pages: pg_cap + 1 of them (the last one the overflow spare)
-  uint32_t* pt;          // page tables (PoaJob::pt_off)
-  uint32_t* pg_ctr;      // pages taken so far, zero at the launch's start: aln_len + 3 n_jobs
-  uint32_t pg_cap;       // pages in the pool
+  void* tb;              // traceback codes: uint16 (wide: uint32) per cell
   int32_t* bnd;          // strip-boundary carries
   int32_t* pool;         // global row pools
   int32_t* aln;

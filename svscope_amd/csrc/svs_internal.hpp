@@ -58,7 +58,6 @@ struct PoaTask {
   uint8_t n_retries = 0;     // retried alignments of this task
   uint8_t read_retries = 0;  // retries of the current sequence
   uint32_t last_rows = 0;    // strip rows (64 columns) the last alignment computed
-  bool tb_full = false;      // the last DP job ran out of traceback pages: reserve the whole matrix
 
   // device-resident graph (poa_dgraph.hpp, the default; SVS_POA_HOST_GRAPH=1
   // keeps the graph in `graph` on the host instead)

@@ -68,7 +68,6 @@ struct Launch {
   int wpj = 0;
   int gid = 0;
   int code_bytes = 2;    // traceback code width of the launch (4: a node with > 31 in-edges)
-  uint64_t page_bytes = 0;  // bytes of one traceback page (the pages taken are read back with aln_len)
   size_t prep_jobs = 0;  // jobs whose tables the device completed (poa_prep.hip)
   int32_t gaps[4] = {0, 0, 0, 0};  // g, e, q, c of the launch (SVS_POA_VERIFY_PREP)
 };
@@ -250,53 +249,15 @@ bool force_wide() {
   return e && std::atoi(e) != 0;
 }
 
-// Traceback code pages of one DP job (poa_strip.hip): a launch's page pool
-// is sized from the sum of these estimates plus the pages each wave may hold
-// unused at the end of its chunk; the kernel may use the whole buffer, and a
-// job that still finds it empty returns kTbRetry.  A pruned job is expected
-// to compute about the strip rows its task's previous alignment computed
-// (last_rows; +25 %), in kTbPageRows-row groups, plus two partly used groups
-// per strip.  A job with no such history (a task's first alignment, a retry,
-// an unpruned job, or one that ran out of pages before: `full`) gets its
-// whole matrix.
-uint64_t tb_pages_est(uint32_t last_rows, bool full, uint32_t V, uint32_t ls) {
-  const uint64_t all = tb_table_pages(V, ls);
-  if (full || last_rows == 0) return all;
-  const uint64_t est = (static_cast<uint64_t>(last_rows) * 5 / 4 + kTbPageRows - 1) / kTbPageRows + 2ull * (ls / 64);
-  return std::min(all, est);
-}
-uint64_t tb_page_bytes(uint64_t code_bytes) { return kTbPageRows * 64 * code_bytes; }
-
 // code_bytes: the launch's traceback code width (4 when some job of it has a
 // node with more than 31 in-edges)
-uint64_t job_bytes(const RowTables& tt, uint64_t L, const KernelEnv& ke, uint64_t code_bytes, uint64_t tb_pages) {
+uint64_t job_bytes(const RowTables& tt, uint64_t L, const KernelEnv& ke, uint64_t code_bytes) {
   const uint64_t ls = strip_ls(static_cast<uint32_t>(L)), V = tt.n_rows;
-  // traceback pages and their table + two strip-boundary carry buffers (+ a
-  // global pool when the graph needs more slots than the LDS pool holds)
+  // traceback codes + two strip-boundary carry buffers (+ a global pool when
+  // the graph needs more slots than the LDS pool holds)
   const uint64_t pool = (tt.n_slots > kStripMaxLdsSlots || ke.global_pool)
                             ? 8ull * round_up(static_cast<uint64_t>(tt.n_slots) * 97, 64) * 4 : 0;
-  return tb_pages * tb_page_bytes(code_bytes) + 4 * tb_table_pages(static_cast<uint32_t>(V), static_cast<uint32_t>(ls)) +
-         round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
-}
-
-// Sizes a launch's page pool and page tables (pages: the jobs' estimates,
-// tables: their page-table entries) and points the launch at them: the pool
-// holds at least the estimates plus every wave's unused chunk tail, and the
-// kernel may take every page of the buffer (pg_cap; the page after it is the
-// overflow spare).  The page counter is the word after the launch's aln_len
-// triples, zeroed on the kernel stream.
-void tb_launch_buffers(PoaArena& A, PoaLaunch& pl, uint64_t pages, uint64_t tables, size_t nj, int wpj,
-                       uint64_t code_bytes, uint64_t hint, hipStream_t s) {
-  const uint64_t pb = tb_page_bytes(code_bytes);
-  const uint64_t want = pages + static_cast<uint64_t>(nj) * wpj * kTbChunkPages + 1;
-  A.d_tb.ensure(want * pb, hint);
-  A.d_pt.ensure(tables * 4 + 256);
-  const uint64_t cap = std::min<uint64_t>(A.d_tb.cap / pb, 0xF0000000ull) - 1;
-  pl.tb = A.d_tb.as<char>();
-  pl.pt = A.d_pt.as<uint32_t>();
-  pl.pg_cap = static_cast<uint32_t>(cap);
-  pl.pg_ctr = reinterpret_cast<uint32_t*>(A.d_alen.as<int32_t>() + 3 * nj);
-  SVS_HIP(hipMemsetAsync(pl.pg_ctr, 0, 4, s));
+  return V * ls * code_bytes + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
 }
 
 void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks);
@@ -328,7 +289,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   auto th0 = Clock::now();
   const size_t nj = la.ids.size();
   la.jobs.assign(nj, PoaJob{});
-  uint64_t n_pages = 0, n_pt = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
+  uint64_t n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
   uint32_t max_preds = 0, max_slots = 1;
   bool any_prune = false;
   PoaArena& A = *la.arena;
@@ -365,17 +326,15 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     J.n_slots = tt.n_slots;
     if (static_cast<uint64_t>(J.n_rows) * J.ls > 0x7FFFFFFFull)  // the strip kernel's 32-bit code offsets
       throw SvsError(SVS_E_UNSUPPORTED, "a job's traceback matrix exceeds 2^31 cells");
-    J.pt_off = n_pt;
+    J.tb_off = n_tb;
     J.bnd_off = n_bnd;
     J.pool_off = n_pool;
     J.aln_off = n_aln;
-    const PoaTask& tk = tasks[la.ids[k]];
-    J.lb = prune_bound(tk, score, J.n_rows, J.len, penv);
+    J.lb = prune_bound(tasks[la.ids[k]], score, J.n_rows, J.len, penv);
     // the kernel tracks slot liveness in 31 bits; path lengths are 16-bit
     if (J.n_slots > 31 || J.len > kPruneMaxReadLen) J.lb = kNoPrune;
     any_prune = any_prune || J.lb != kNoPrune;
-    n_pt += tb_table_pages(J.n_rows, J.ls);
-    n_pages += tb_pages_est(tk.last_rows, tk.tb_full || tk.retry || J.lb == kNoPrune, J.n_rows, J.ls);
+    n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
     n_bnd += round_up(round_up(J.n_rows, kCarryLineRows) * (J.ls / 64) * 4, kCarryAlignInts);
     if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 97, 64);
     n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
@@ -471,11 +430,14 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   host_ms += ms_since(th0);
 
   A.d_in.ensure(dev_end);
+  // the traceback codes dominate a launch's footprint: sized to the group's
+  // budget at the first launch, so it never regrows (and syncs) mid-run
+  A.d_tb.ensure(n_tb * la.code_bytes + 4096, ctx->device_budget / 2);
   A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096);
   A.d_aln.ensure(n_aln * 8);
-  A.d_alen.ensure(nj * 12 + 64);
+  A.d_alen.ensure(nj * 12);
   A.h_aln.ensure(n_aln * 8);
-  A.h_alen.ensure(nj * 12 + 64);
+  A.h_alen.ensure(nj * 12);
   char* dg = A.d_in.as<char>();
   for (size_t k = 0; k < nj; ++k) {
     PoaJob& J = la.jobs[k];
@@ -508,6 +470,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.jobs = reinterpret_cast<const PoaJob*>(dg + s_jobs);
   pl.n_jobs = static_cast<int>(nj);
   pl.score = score;
+  pl.tb = A.d_tb.as<char>();
   pl.bnd = A.d_pool.as<int32_t>();
   pl.pool = A.d_pool.as<int32_t>() + n_bnd;
   pl.aln = A.d_aln.as<int32_t>();
@@ -517,22 +480,19 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.wide = la.code_bytes == 4;
   pl.waves_per_job = wpj;
   la.wpj = wpj;
-  // the traceback pages are sized to the group's budget at the first launch,
-  // so the pool never regrows (and syncs) mid-run
-  tb_launch_buffers(A, pl, n_pages, n_pt, nj, wpj, la.code_bytes, ctx->device_budget / 2 / 4 * 3, A.stream);
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
   SVS_HIP(launch_poa_strip(pl, A.stream));
   SVS_HIP(hipEventRecord(A.ev1, A.stream));
   SVS_HIP(hipStreamWaitEvent(A.copy_stream, A.ev1, 0));
-  SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 12 + 4, hipMemcpyDeviceToHost, A.copy_stream));
+  SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, pl.aln_len, nj * 12, hipMemcpyDeviceToHost, A.copy_stream));
   SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, pl.aln, n_aln * 8, hipMemcpyDeviceToHost, A.copy_stream));
   SVS_HIP(hipEventRecord(A.done, A.copy_stream));
-  la.page_bytes = tb_page_bytes(la.code_bytes);
   st.launches += 1;
   st.alignments += nj;
+  st.tb_bytes += n_tb * 2;
   st.pool_bytes += (n_bnd + n_pool) * 4;
   st.h2d_bytes += off;
-  st.d2h_bytes += n_aln * 8 + nj * 12 + 4;
+  st.d2h_bytes += n_aln * 8 + nj * 12;
 }
 
 // Readies a task's next step: sequences landing on an empty graph become a
@@ -627,20 +587,11 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
       st.cells_computed += 64ull * static_cast<uint32_t>(alen[2 * nj + k]);
       tasks[la.ids[k]].last_rows = static_cast<uint32_t>(alen[2 * nj + k]);
       if (alen[k] == kPruneRetry) st.prune_retries += 1;
-      if (alen[k] == kTbRetry) st.tb_retries += 1;
     }
-    st.tb_bytes += static_cast<uint64_t>(static_cast<uint32_t>(alen[3 * nj])) * la.page_bytes;
   }
   ctx->pool->parallel_for(nj, [&](size_t k) {
     const int32_t n = alen[k];
     auto& t = tasks[la.ids[k]];
-    if (n == kTbRetry) {
-      // the page pool ran out: the same step again, its whole matrix reserved
-      t.tb_full = true;
-      t.prepped = 1;
-      return;
-    }
-    t.tb_full = false;
     if (n == kPruneRetry) {
       // the bound was above the optimum: the same sequence again, unpruned
       // (its row tables are still those of this step)
@@ -694,7 +645,6 @@ struct DevLaunch {
   int wpj = 0;
   bool timed_dp = false;
   bool prune = false, wide = false;  // the DP kernel instance
-  uint64_t n_pages = 0, n_pt = 0, page_bytes = 0;  // traceback page estimate, page-table entries, page size
 };
 
 // Task group: a disjoint subset of the active tasks with its own arena.
@@ -1191,10 +1141,7 @@ struct PoaScheduler::Impl {
     const uint64_t L = t.seqs[t.next].size(), ls = strip_ls(static_cast<uint32_t>(L)), V = t.dg.V;
     const uint64_t pool = (t.n_slots_next > kStripMaxLdsSlots || ke.global_pool)
                               ? 8ull * round_up(static_cast<uint64_t>(t.n_slots_next) * 97, 64) * 4 : 0;
-    const uint64_t pages = tb_pages_est(t.last_rows, t.tb_full || t.retry || !t.have_rate, static_cast<uint32_t>(V),
-                                        static_cast<uint32_t>(ls));
-    return pages * tb_page_bytes(code_bytes) + 4 * tb_table_pages(static_cast<uint32_t>(V), static_cast<uint32_t>(ls)) +
-           round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
+    return V * ls * code_bytes + round_up(V, 8) * (ls / 64) * 16 + pool + 256 + (V + L + 1) * 8;
   }
 
   void pack_and_launch_dev(Group& g, const std::vector<uint32_t>& dp, const std::vector<uint32_t>& chain,
@@ -1228,7 +1175,7 @@ struct PoaScheduler::Impl {
       }
     // DP jobs: the tables the last fold exported, in the task's block
     D.jobs.assign(nj, PoaJob{});
-    uint64_t n_pages = 0, n_pt = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
+    uint64_t n_tb = 0, n_bnd = 0, n_pool = 0, n_aln = 0;
     uint32_t max_slots = 1, min_strips = 0xFFFFFFFFu;
     bool any_prune = false, wide = force_wide();
     for (uint32_t id : dp) {
@@ -1262,15 +1209,14 @@ struct PoaScheduler::Impl {
       J.n_slots = t.n_slots_next;
       if (static_cast<uint64_t>(J.n_rows) * J.ls > 0x7FFFFFFFull)
         throw SvsError(SVS_E_UNSUPPORTED, "a job's traceback matrix exceeds 2^31 cells");
-      J.pt_off = n_pt;
+      J.tb_off = n_tb;
       J.bnd_off = n_bnd;
       J.pool_off = n_pool;
       J.aln_off = n_aln;
       J.lb = prune_bound(t, score, J.n_rows, J.len, penv);
       if (J.n_slots > 31 || J.len > kPruneMaxReadLen) J.lb = kNoPrune;
       any_prune = any_prune || J.lb != kNoPrune;
-      n_pt += tb_table_pages(J.n_rows, J.ls);
-      n_pages += tb_pages_est(t.last_rows, t.tb_full || t.retry || J.lb == kNoPrune, J.n_rows, J.ls);
+      n_tb += static_cast<uint64_t>(J.n_rows) * J.ls;
       n_bnd += round_up(round_up(J.n_rows, kCarryLineRows) * (J.ls / 64) * 4, kCarryAlignInts);
       if (!lds_pool) n_pool += static_cast<uint64_t>(wpj) * round_up(static_cast<uint64_t>(J.n_slots) * 97, 64);
       n_aln += static_cast<uint64_t>(J.n_rows) + J.len + 1;
@@ -1284,12 +1230,11 @@ struct PoaScheduler::Impl {
     D.prune = any_prune;
     D.wide = wide;
     st.wide_launches += wide ? 1 : 0;
-    // (hints: the group's budget is two thirds traceback pages and a third
-    // strip carries, 16 B per strip row of the full matrix; the pairs 8 B per
-    // row and read base; sized once instead of growing with the graphs)
-    D.n_pages = n_pages;
-    D.n_pt = n_pt;
-    A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096, budget / 3);
+    // (hints: the carries are 16 B per 64 traceback codes, the pairs 8 B per
+    // row and read base; sized once for the group's budget instead of growing
+    // with the graphs)
+    A.d_tb.ensure(n_tb * (wide ? 4 : 2) + 4096, ctx->device_budget / 2);
+    A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096, ctx->device_budget / 16);
     A.d_aln.ensure(n_aln * 8 + 64, 256ull << 20);
     A.d_alen.ensure(nj * 12 + 64);
     // fold jobs, growing blocks that could not hold this fold
@@ -1481,6 +1426,7 @@ struct PoaScheduler::Impl {
       pl.jobs = reinterpret_cast<const PoaJob*>(dd);
       pl.n_jobs = static_cast<int>(nj);
       pl.score = score;
+      pl.tb = A.d_tb.as<char>();
       pl.bnd = A.d_pool.as<int32_t>();
       pl.pool = A.d_pool.as<int32_t>() + n_bnd;
       pl.aln = A.d_aln.as<int32_t>();
@@ -1488,12 +1434,10 @@ struct PoaScheduler::Impl {
       pl.lds_slots = lds_pool ? max_slots : 0;
       pl.prune = any_prune;
       pl.wide = wide;
-      pl.waves_per_job = wpj;
+          pl.waves_per_job = wpj;
       // the pool slots per wave the launch's LDS is sized for (its occupancy)
       g_trace.host("slots", gid(g), Clock::now(), pl.lds_slots);
       SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
-      tb_launch_buffers(A, pl, D.n_pages, D.n_pt, nj, wpj, wide ? 4 : 2, budget / 3 * 2, A.stream);
-      D.page_bytes = tb_page_bytes(wide ? 4 : 2);
       SVS_HIP(hipEventRecord(A.ev0, A.stream));
       SVS_HIP(launch_poa_strip(pl, A.stream));
       SVS_HIP(hipEventRecord(A.ev1, A.stream));
@@ -1507,7 +1451,7 @@ struct PoaScheduler::Impl {
     }
     SVS_HIP(hipEventRecord(A.evf1, side));
     A.h_alen.ensure(nj * 12 + 64);
-    if (nj) SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, A.d_alen.ptr, nj * 12 + 4, hipMemcpyDeviceToHost, side));
+    if (nj) SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, A.d_alen.ptr, nj * 12, hipMemcpyDeviceToHost, side));
     SVS_HIP(hipMemcpyAsync(hd + s_res, dd + s_res, nf * sizeof(FoldResult), hipMemcpyDeviceToHost, side));
     if (D.fin_copy) SVS_HIP(hipMemcpyAsync(A.h_fin.ptr, A.d_fin.ptr, D.fin_copy, hipMemcpyDeviceToHost, side));
     if (verify) {
@@ -1525,9 +1469,10 @@ struct PoaScheduler::Impl {
     }
     st.launches += nj ? 1 : 0;
     st.alignments += nj;
+    st.tb_bytes += n_tb * 2;
     st.pool_bytes += (n_bnd + n_pool) * 4;
     st.h2d_bytes += total;
-    st.d2h_bytes += (nj ? nj * 12 + 4 : 0) + nf * sizeof(FoldResult) + D.fin_copy;
+    st.d2h_bytes += nj * 12 + nf * sizeof(FoldResult) + D.fin_copy;
     st.fold_jobs += nf;
     for (const FoldJob& F : D.folds) st.prep_jobs += (F.flags & kFoldExport) ? 1 : 0;
   }
@@ -1598,20 +1543,11 @@ struct PoaScheduler::Impl {
     const auto th0 = Clock::now();
     const int32_t* alen = A.h_alen.as<int32_t>();
     const FoldResult* res = reinterpret_cast<const FoldResult*>(A.h_desc.as<char>() + D.s_res);
-    if (nj) st.tb_bytes += static_cast<uint64_t>(static_cast<uint32_t>(alen[3 * nj])) * D.page_bytes;
     for (size_t k = 0; k < nj; ++k) {
       PoaTask& t = tasks[D.dp_ids[k]];
       st.cells_computed += 64ull * static_cast<uint32_t>(alen[2 * nj + k]);
       t.last_rows = static_cast<uint32_t>(alen[2 * nj + k]);
       const int32_t n = alen[k];
-      if (n == kTbRetry) {
-        // the launch's page pool ran out: the same read again (its fold was
-        // skipped), with its whole matrix reserved
-        st.tb_retries += 1;
-        t.tb_full = true;
-        continue;
-      }
-      t.tb_full = false;
       if (n == kPruneRetry) {
         st.prune_retries += 1;
         t.retry = true;
@@ -1816,14 +1752,8 @@ struct PoaScheduler::Impl {
       const KernelEnv ke;
       for (uint32_t id : ids)
         if (tasks[id].rows.max_preds > kMaxInEdgesNarrow) code_bytes = 4;
-      auto host_job_bytes = [&](uint32_t id) {
-        const PoaTask& t = tasks[id];
-        const uint64_t L = t.seqs[t.next].size();
-        return job_bytes(t.rows, L, ke, code_bytes,
-                         tb_pages_est(t.last_rows, t.tb_full || t.retry || !t.have_rate, t.rows.n_rows,
-                                      strip_ls(static_cast<uint32_t>(L))));
-      };
-      for (uint32_t id : ids) total += host_job_bytes(id);
+      for (uint32_t id : ids)
+        total += job_bytes(tasks[id].rows, tasks[id].seqs[tasks[id].next].size(), ke, code_bytes);
       if (total <= budget) {
         order_by_cost(ids);
         g.la.ids = std::move(ids);
@@ -1841,7 +1771,8 @@ struct PoaScheduler::Impl {
         size_t last = first;
         uint64_t bytes = 0;
         while (last < ids.size()) {
-          const uint64_t b = host_job_bytes(ids[last]);
+          const uint64_t b =
+              job_bytes(tasks[ids[last]].rows, tasks[ids[last]].seqs[tasks[ids[last]].next].size(), ke, code_bytes);
           if (last > first && bytes + b > budget) break;
           bytes += b;
           ++last;
