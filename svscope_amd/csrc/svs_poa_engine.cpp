@@ -797,7 +797,25 @@ struct PoaScheduler::Impl {
     while (ctx->poa_arenas.size() < 2) ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
     for (int g = 0; g < 2; ++g) groups[g].arena = ctx->poa_arenas[g].get();
     split_cus();
+    // SVS_POA_DP_STREAMS=2 (development): each group's DP kernel on a stream
+    // of its own, so that one group's launch can start in the tail of the
+    // other's (the default alternates both on the context's stream)
+    if (const char* e = std::getenv("SVS_POA_DP_STREAMS"))
+      if (std::atoi(e) == 2 && !ctx->poa_fold_cus)
+        for (int g = 0; g < 2; ++g) {
+          SVS_HIP(hipStreamCreateWithFlags(&own_dp[g], hipStreamNonBlocking));
+          groups[g].arena->stream = own_dp[g];
+        }
   }
+  ~Impl() {
+    for (int g = 0; g < 2; ++g)
+      if (own_dp[g]) {
+        (void)hipStreamSynchronize(own_dp[g]);
+        groups[g].arena->stream = ctx->stream;
+        (void)hipStreamDestroy(own_dp[g]);
+      }
+  }
+  hipStream_t own_dp[2] = {nullptr, nullptr};
 
   // SVS_POA_FOLD_CUS=n (device-resident graphs, shared DP stream): n CUs,
   // spread evenly over the device, run the fold kernels (the groups' copy
