@@ -349,6 +349,13 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
     const int32_t j0 = s << 6;
     const int32_t j = j0 + lane;
     const uint8_t rc = seq[j - 1];  // seq[-1] is a zero pad byte (column 0)
+    // The read base is waited for here, once per strip.  Left to the compiler,
+    // the wait sat at its first use inside the row loop: a load from before the
+    // loop is still "pending" at the loop header (the waitcnt pass merges the
+    // preheader's state), and with the row's code and carry stores counted on
+    // the same vmcnt it became a vmcnt(0) on every computed row, each row
+    // waiting for the previous row's stores to be acknowledged.
+    wait_vm_stores();
     CodeT* __restrict__ tbl = tbj + j;  // this lane's column of the traceback codes
     const GLB int32_t* __restrict__ bin = bndr + static_cast<uint64_t>(s > 0 ? s - 1 : 0) * VP * 4;
     int32_t* __restrict__ bout = bnd + static_cast<uint64_t>(s) * VP * 4;

@@ -791,21 +791,25 @@ struct PoaScheduler::Impl {
       if (!ctx->dgraph_arena) ctx->dgraph_arena.reset(new DevArena(ctx->dgraph_budget));
       darena = ctx->dgraph_arena.get();
     }
-    // Both groups' DP kernels alternate on the context's one stream (a stream
-    // per group measured no faster: 196.9 vs 202.0 windows/s, r01_v40; 237.4
-    // vs 240.2 with device graphs, r03_s3c).
+    // (both arenas start on the context's stream; the DP streams below)
     while (ctx->poa_arenas.size() < 2) ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
     for (int g = 0; g < 2; ++g) groups[g].arena = ctx->poa_arenas[g].get();
     split_cus();
-    // SVS_POA_DP_STREAMS=2 (development): each group's DP kernel on a stream
-    // of its own, so that one group's launch can start in the tail of the
-    // other's (the default alternates both on the context's stream)
-    if (const char* e = std::getenv("SVS_POA_DP_STREAMS"))
-      if (std::atoi(e) == 2 && !ctx->poa_fold_cus)
-        for (int g = 0; g < 2; ++g) {
-          SVS_HIP(hipStreamCreateWithFlags(&own_dp[g], hipStreamNonBlocking));
-          groups[g].arena->stream = own_dp[g];
-        }
+    // Each group's DP kernel on a stream of its own (round 5), so that one
+    // group's launch starts in the tail of the other's: a launch ends with its
+    // longest jobs and leaves CUs idle that the other group's first
+    // workgroups now take.  Same-box driver-shape A/B 378.4 / 375.7 vs 362.3 /
+    // 361.7 windows/s (profiles/r05_a6), 382.1 vs 365.7 (r05_a8); the DP
+    // launches' mean event time grows by ~1 % where they overlap.  Round 3
+    // measured no gain (237.4 vs 240.2, r03_s3c) when the host fold still paced
+    // the launches.  SVS_POA_DP_STREAMS=1 alternates both groups on the
+    // context's stream.
+    const char* dse = std::getenv("SVS_POA_DP_STREAMS");
+    if (!(dse && std::atoi(dse) == 1) && !ctx->poa_fold_cus)
+      for (int g = 0; g < 2; ++g) {
+        SVS_HIP(hipStreamCreateWithFlags(&own_dp[g], hipStreamNonBlocking));
+        groups[g].arena->stream = own_dp[g];
+      }
   }
   ~Impl() {
     for (int g = 0; g < 2; ++g)
