@@ -89,6 +89,23 @@ int svs_init(int device_ordinal, svs_context** out) {
     ctx->device = device_ordinal;
     SVS_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     SVS_HIP(hipStreamCreateWithFlags(&ctx->em_stream, hipStreamNonBlocking));
+    // SVS_EM_CUS=n (measurement): the EM stream confined
+    // to n CUs spread over the device, so that its workgroups never share a
+    // CU with the DP kernel's on the others
+    if (const char* e = std::getenv("SVS_EM_CUS")) {
+      const int want = std::atoi(e);
+      hipDeviceProp_t prop;
+      SVS_HIP(hipGetDeviceProperties(&prop, device_ordinal));
+      const int n_cu = prop.multiProcessorCount;
+      if (want > 0 && want < n_cu) {
+        std::vector<uint32_t> mask((n_cu + 31) / 32, 0);
+        const int step = n_cu / want;
+        for (int i = 0; i < n_cu; ++i)
+          if (i % step == step - 1 && i / step < want) mask[i / 32] |= 1u << (i % 32);
+        SVS_HIP(hipStreamDestroy(ctx->em_stream));
+        SVS_HIP(hipExtStreamCreateWithCUMask(&ctx->em_stream, static_cast<uint32_t>(n_cu), mask.data()));
+      }
+    }
     SVS_HIP(hipEventCreate(&ctx->ev_start));
     SVS_HIP(hipEventCreate(&ctx->ev_stop));
     SVS_HIP(hipEventCreate(&ctx->ev_mid));
