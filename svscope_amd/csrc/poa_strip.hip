@@ -418,8 +418,10 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
 
     auto fetch = [&](RowIn& d, uint32_t r) {
       const uint32_t rr = r < V ? r : V - 1;
-      // 32-bit byte offsets off the job's bases (a job has < 2^28 rows)
-      const TBL uint32_t* w = rec + (rr << 2);
+      // 32-bit byte offsets off the job's bases (a job has < 2^28 rows), so
+      // that the scalar loads take them as their SGPR offset (an index scaled
+      // in 64 bits cost four more SALU per load)
+      const TBL uint32_t* w = reinterpret_cast<const TBL uint32_t*>(reinterpret_cast<const TBL char*>(rec) + (rr << 4));
       d.w0 = w[0];
       d.w1 = w[1];
       if constexpr (PRUNE) {
@@ -440,7 +442,7 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
             SVS_SP(0, avail = strip_wait_ge(&prog[pw], need, &s_err));
           }
         }
-        const svs_i32x4 v = *reinterpret_cast<const GLB svs_i32x4*>(bin + (rr << 2));
+        const svs_i32x4 v = *reinterpret_cast<const GLB svs_i32x4*>(reinterpret_cast<const GLB char*>(bin) + (rr << 4));
         d.b0 = v.x; d.b1 = v.y; d.b2 = v.z; d.b3 = v.w;
       }
     };
