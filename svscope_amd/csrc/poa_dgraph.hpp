@@ -31,6 +31,11 @@
 //   prep outputs (poa_prep.hip): col0 i32[3 cv], rec u32[4 cv],
 //            pslot u32[ce + 4] + scratch u32[3 (cv + 4)]
 //   stk      u32  [ce + 2 cv + 64]  the sort's DFS stack beyond its LDS part
+//   chg      u32  [2 ceil(cv / 64)]  bit plane by node id: the fold changed the
+//                            node's in-edge or aligned list (update kernel)
+//   seg      u32  [2][ceil(cv / 32) + 2]  bit plane by rank: a DFS root's
+//                            segment of the rank order starts here (the sort
+//                            of a fold reads seg[par] and writes seg[1 - par])
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -41,7 +46,7 @@ namespace svs {
 
 struct DGraphLayout {
   size_t base, al, in_off[2], in_nbr[2], in_eid[2], out_off[2], out_nbr[2], out_eid[2], ew, nin, nout;
-  size_t nrec, r2n, n2r, col, last, pstart, pred, info, col0, rec, pslot, stk, bytes;
+  size_t nrec, r2n, n2r, col, last, pstart, pred, info, col0, rec, pslot, stk, chg, seg[2], bytes;
 };
 
 __host__ __device__ inline DGraphLayout dgraph_layout(uint32_t cv, uint32_t ce) {
@@ -78,6 +83,8 @@ __host__ __device__ inline DGraphLayout dgraph_layout(uint32_t cv, uint32_t ce) 
   L.rec = take(16 * V);
   L.pslot = take(4 * (E + 4) + 12 * (V + 4));
   L.stk = take(4 * (E + 2 * V + 64));
+  L.chg = take(8 * ((V + 63) / 64));
+  for (int b = 0; b < 2; ++b) L.seg[b] = take(4 * ((V + 31) / 32 + 2));
   L.bytes = o;
   return L;
 }

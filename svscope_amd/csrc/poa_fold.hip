@@ -82,6 +82,10 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
   for (int o = 32; o >= 1; o >>= 1) x = max(x, static_cast<uint32_t>(__shfl_xor(x, o, 64)));
   return x;
 }
+__device__ __forceinline__ uint32_t wave_min(uint32_t x) {
+  for (int o = 32; o >= 1; o >>= 1) x = min(x, static_cast<uint32_t>(__shfl_xor(x, o, 64)));
+  return x;
+}
 __device__ __forceinline__ int32_t wave_min_i(int32_t x) {
   for (int o = 32; o >= 1; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
   return x;
@@ -108,6 +112,8 @@ struct GPtr {
   gu32 *in_off, *in_nbr, *in_eid, *out_off, *out_nbr, *out_eid;
   gu32* ew;
   gu32 *nin, *nout, *nrec, *r2n, *n2r, *col, *last, *pstart, *pred, *info, *stk;
+  gu32* chg;
+  gu32 *seg, *seg_other;  // segment-start plane of buffer b, of 1 - b
 };
 
 __device__ __forceinline__ GPtr gptr(uint8_t* blk, uint32_t cv, uint32_t ce, uint32_t b) {
@@ -136,16 +142,22 @@ __device__ __forceinline__ GPtr gptr(uint8_t* blk, uint32_t cv, uint32_t ce, uin
   g.pred = u(L.pred);
   g.info = u(L.info);
   g.stk = u(L.stk);
+  g.chg = u(L.chg);
+  g.seg = u(b ? L.seg[1] : L.seg[0]);
+  g.seg_other = u(b ? L.seg[0] : L.seg[1]);
   return g;
 }
 
 // One CSR list (in or out) rebuilt into buffer b1 from b0 for nodes
 // 0 .. V1-1, each node's new entry (nw[2v] = eid, nw[2v+1] = neighbour, eid
 // kNone = none) appended; the new-entry slots are reset.  For the in-list
-// (nrec given) also every node's sort record (poa_dgraph.hpp).  Returns the
-// number of new entries found.
+// (nrec given) also every node's sort record (poa_dgraph.hpp) and the changed
+// plane chg: a node of the old graph whose in-edge list gained an entry or
+// whose aligned list grew (the record's aligned count differs), and every new
+// node.  Returns the number of new entries found.
 __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, const gu32* nbr0, const gu32* eid0,
-                                gu32* off1, gu32* nbr1, gu32* eid1, gu32* nw, gu32* nrec, const gu32* al) {
+                                gu32* off1, gu32* nbr1, gu32* eid1, gu32* nw, gu32* nrec, const gu32* al,
+                                gu32* chg) {
   const uint32_t lane = lanei();
   uint32_t run = 0, found = 0;
   for (uint32_t v0 = 0; v0 < V1; v0 += 64) {
@@ -162,6 +174,7 @@ __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, cons
     const uint32_t has = ne != kNone ? 1u : 0u;
     uint32_t tot;
     const uint32_t o = run + wave_excl(d + has, &tot);
+    bool changed = true;
     if (v < V1) {
       off1[v] = o;
       for (uint32_t k = 0; k < d; ++k) {
@@ -177,9 +190,14 @@ __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, cons
         auto tail = [&](uint32_t k) -> uint32_t { return k < d ? nbr0[a + k] : (k == d && has ? nb : 0u); };
         const u32x4 alw = *reinterpret_cast<const GLB u32x4*>(al + 4 * v);
         GLB u32x4* nr = reinterpret_cast<GLB u32x4*>(nrec + 8 * v);
+        if (v < V0) changed = has || (nrec[8 * v + 1] >> 24) != alw.x;
         nr[0] = u32x4{o, (d + has) | (alw.x << 24), alw.y, alw.z};
         nr[1] = u32x4{alw.w, tail(0), tail(1), tail(2)};
       }
+    }
+    if (nrec) {
+      const uint64_t cm = ballot(v < V1 && changed);
+      if (lane < 2u) chg[(v0 >> 5) + lane] = static_cast<uint32_t>(lane ? cm >> 32 : cm);
     }
     found += wave_add(has);
     run += tot;
@@ -392,9 +410,10 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
   const uint32_t V1 = next;
   // both adjacency lists into the other buffer, the new edge of each node last
   const uint32_t fin =
-      rebuild_csr(V0, V1, g.in_off, g.in_nbr, g.in_eid, h.in_off, h.in_nbr, h.in_eid, g.nin, g.nrec, g.al);
+      rebuild_csr(V0, V1, g.in_off, g.in_nbr, g.in_eid, h.in_off, h.in_nbr, h.in_eid, g.nin, g.nrec, g.al, g.chg);
   const uint32_t fout =
-      rebuild_csr(V0, V1, g.out_off, g.out_nbr, g.out_eid, h.out_off, h.out_nbr, h.out_eid, g.nout, nullptr, nullptr);
+      rebuild_csr(V0, V1, g.out_off, g.out_nbr, g.out_eid, h.out_off, h.out_nbr, h.out_eid, g.nout, nullptr, nullptr,
+                  nullptr);
   // a node twice on the path would have lost one of its new edges
   if (fin != E1 - E0 || fout != E1 - E0) return fail(kFoldErrPath);
   if (lane == 0) {
@@ -415,11 +434,26 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
 //
 // Node flags live in LDS (two bit planes), the stack's top in LDS (the rest
 // spills to the block's stk array in blocks of half the LDS stack).
+//
+// Reuse of the previous sort.  Everything emitted between one root's start
+// and the next root's is that root's segment of the rank order, and the
+// segments tile it.  A root's DFS reads only the records of the nodes it
+// emits, and flags that, at a root's start, only ever grow from one fold to
+// the next (the done set is then the ancestor-and-aligned closure of every
+// smaller id, and a fold only adds edges and aligned members).  So, walking
+// the previous order segment by segment: a segment none of whose nodes the
+// fold changed (chg) and none of whose nodes is done yet is emitted again
+// unchanged; any other segment's root (its smallest id) runs the DFS unless
+// it is done; and the new ids follow as roots in id order.  The result is
+// spoa's order exactly; on the config-3 windows 91 % of the examinations are
+// skipped (a host replay of spoa's sort with this walk, profiles/r05_s1).
 namespace {
 
 struct SortState {
   uint32_t* done;  // LDS bit plane
   uint32_t* ign;   // LDS bit plane
+  const uint32_t* chg;  // LDS copy of the fold's changed plane (by node id)
+  uint32_t* nseg;  // LDS bit plane by rank: the new segment starts
   uint32_t* st;    // LDS stack
   uint32_t cap;    // LDS stack entries (even)
   gu32* spill;     // global spill area
@@ -428,6 +462,7 @@ struct SortState {
   uint32_t spill_cap;  // entries the spill area holds
   bool err;            // the stack outgrew its spill area
   uint32_t n_exam, n_roots;  // statistics
+  uint32_t n_emit;           // nodes emitted (V unless the sort failed)
   uint64_t prof[4];          // SVS_FOLD_PROF: fast roots, DFS runs, window loads, rest (clocks)
 };
 #include "poa_fold_prof.hpp"  // development profile builds only; no-ops otherwise
@@ -446,15 +481,18 @@ template <int L> __device__ __forceinline__ uint32_t write_lane_c(uint32_t x, ui
 // cache.
 // V0: the node count before this fold (nodes >= V0 are the fold's new ones);
 // r2n_old: the previous sort's rank order of nodes < V0 (a copy: r2n is
-// overwritten as nodes are emitted).
+// overwritten as nodes are emitted); seg_old: the previous sort's segment
+// starts (nullptr: no reuse, every root runs).
 __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nrec, const gu32* __restrict__ in_nbr,
                             gu32* __restrict__ r2n, gu32* __restrict__ n2r, const gu32* __restrict__ r2n_old,
-                            gu32* __restrict__ col, SortState& S, uint32_t* ncol_out) {
+                            gu32* __restrict__ col, const gu32* __restrict__ seg_old, SortState& S,
+                            uint32_t* ncol_out) {
   const uint32_t lane = lanei();
   const uint32_t W = (V + 31u) >> 5;
   for (uint32_t w = lane; w < W; w += 64) {
     S.done[w] = 0;
     S.ign[w] = 0;
+    S.nseg[w] = 0;
   }
   uint32_t cnt = 0, ncol = 0;
   // Uniform control throughout.  LDS operations of one wave complete in
@@ -546,7 +584,6 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
       eb_n = 0;
     }
   };
-  uint32_t root = 0;
   // every examination pops or pushes: a bound on them stops a corrupt graph
   uint32_t steps = 0;
   const uint32_t max_steps = 64u * (V + S.spill_cap) + 4096u;
@@ -601,25 +638,119 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
     off = lane_val(o0, l); w1 = lane_val(o1, l); m0 = lane_val(o2, l); m1 = lane_val(o3, l);
     m2 = lane_val(o4, l); t0 = lane_val(o5, l); t1 = lane_val(o6, l); t2 = lane_val(o7, l);
   };
+  // The previous order's segment starts at ranks p .. p + 63 (bit l: rank
+  // p + l); the end of the old order counts as a start.
+  auto seg_window = [&](uint32_t p) -> uint64_t {
+    const uint32_t a = p >> 5, s = p & 31u;
+    const uint64_t lo = uni(seg_old[a]) | (static_cast<uint64_t>(uni(seg_old[a + 1])) << 32);
+    const uint64_t hi = uni(seg_old[a + 2]);
+    uint64_t m = s ? (lo >> s) | (hi << (64u - s)) : lo;
+    const uint32_t left = V0 - p;
+    if (left < 64u) m = (m & ((1ull << left) - 1ull)) | (1ull << left);
+    return m;
+  };
+  auto next_start = [&](uint32_t q) -> uint32_t {  // the first segment start >= q
+    while (q < V0) {
+      const uint32_t w = uni(seg_old[q >> 5]) >> (q & 31u);
+      if (w) return min(q + static_cast<uint32_t>(__builtin_ctz(w)), V0);
+      q = (q | 31u) + 1u;
+    }
+    return V0;
+  };
+  // the fold changed node v, or it is emitted already
+  auto bad_of = [&](uint32_t v) -> uint32_t { return ((S.chg[v >> 5] | S.done[v >> 5]) >> (v & 31u)) & 1u; };
+  // a chunk of the previous order (lane: node nd, old column co; lanes < k)
+  // emitted again at cnt + lane, columns shifted by ncol - c0; st: the
+  // chunk's segment starts.  Returns the chunk's last old column.
+  auto copy_ranks = [&](uint32_t nd, uint32_t co, uint32_t k, uint32_t c0, uint64_t st) -> uint32_t {
+    if (lane < k) {
+      r2n[cnt + lane] = nd;
+      n2r[nd] = cnt + lane;
+      col[nd] = ncol + co - c0;
+      set_bit(S.done, nd);
+      if ((st >> lane) & 1u) set_bit(S.nseg, cnt + lane);
+    }
+    return lane_val(co, k - 1u);
+  };
   // Every node with an id below the current root is done (each root's DFS
   // finishes all it pushed), so flags are only read for larger ids and a root
   // whose tails and aligned nodes all have smaller ids is emitted at once,
   // with no stack and no flag access (its own done bit is then never read).
   // The root scan keeps its done word in a register while no DFS writes.
+  uint32_t p = 0;                          // the walk's next segment start
+  uint32_t scan = seg_old ? V0 : 0u;       // the root scan's next id
   uint32_t dwi = kNone, dwv = 0;
-  while (root < V && !S.err) {
-    if ((root >> 5) != dwi) {
-      dwi = root >> 5;
-      dwv = uni(S.done[dwi]);
+  while (!S.err) {
+    uint32_t root;
+    if (seg_old && p < V0) {
+      // the previous order, 64 ranks at a time: every whole segment before
+      // the first changed or done node is emitted again in one pass
+      const uint32_t q = p + lane;
+      const bool in = q < V0;
+      const uint32_t nd = in ? r2n_old[q] : 0u;
+      const uint64_t sm = seg_window(p);
+      const uint64_t bad = ballot(in && bad_of(nd) != 0u);
+      const uint64_t upto = bad ? (2ull << __builtin_ctzll(bad)) - 1ull : ~0ull;
+      const uint64_t ends = sm & upto & ~1ull;
+      if (ends) {
+        const uint32_t k = 63u - static_cast<uint32_t>(__builtin_clzll(ends));
+        flush_emit();
+        const uint32_t co = col[nd];
+        const uint32_t c0 = lane_val(co, 0);
+        const uint32_t cl = copy_ranks(nd, co, k, c0, sm);
+        cnt += k;
+        ncol += cl + 1u - c0;
+        p += k;
+        continue;
+      }
+      // the segment at p is longer than the window or holds a bad node:
+      // its end, its root, and whether it can still be copied
+      const uint64_t rest = sm & ~1ull;
+      const uint32_t e = rest ? p + static_cast<uint32_t>(__builtin_ctzll(rest)) : next_start(p + 64u);
+      const uint32_t n0 = min(e - p, 64u);
+      uint32_t r = uni(wave_min(lane < n0 ? nd : kNone));
+      bool clean = (bad & (n0 < 64u ? (1ull << n0) - 1ull : ~0ull)) == 0;
+      for (uint32_t c = p + 64u; c < e; c += 64u) {
+        const uint32_t cq = c + lane;
+        const uint32_t cn = cq < e ? r2n_old[cq] : kNone;
+        clean = clean && ballot(cq < e && bad_of(cn) != 0u) == 0;
+        r = min(r, uni(wave_min(cn)));
+      }
+      if (clean) {
+        flush_emit();
+        const uint32_t c0 = lane_val(col[nd], 0);
+        uint32_t cl = c0;
+        for (uint32_t c = p; c < e; c += 64u) {
+          const uint32_t cq = c + lane;
+          const uint32_t cn = cq < e ? r2n_old[cq] : 0u;
+          cl = copy_ranks(cn, col[cn], min(e - c, 64u), c0, c == p ? 1ull : 0ull);
+          cnt += min(e - c, 64u);
+        }
+        ncol += cl + 1u - c0;
+        p = e;
+        continue;
+      }
+      p = e;
+      if (done_of(r)) continue;  // emitted by an earlier root's DFS
+      root = r;
+    } else {
+      // the new ids (or, with no previous order, every id) in id order
+      if (scan >= V) break;
+      if ((scan >> 5) != dwi) {
+        dwi = scan >> 5;
+        dwv = uni(S.done[dwi]);
+      }
+      const uint32_t fw = ~dwv >> (scan & 31u);
+      if (fw == 0) {
+        scan = (scan | 31u) + 1u;
+        continue;
+      }
+      scan += static_cast<uint32_t>(__builtin_ctz(fw));
+      if (scan >= V) break;
+      root = scan++;
     }
-    const uint32_t fw = ~dwv >> (root & 31u);
-    if (fw == 0) {
-      root = (root | 31u) + 1u;
-      continue;
-    }
-    root += static_cast<uint32_t>(__builtin_ctz(fw));
-    if (root >= V) break;
     ++S.n_roots;
+    set_bit(S.nseg, cnt);  // root's segment starts here
     const uint64_t pf0 = SVS_PF_CLK();
     {
       uint32_t off, w1, m0, m1, m2, t0, t1, t2;
@@ -635,7 +766,6 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
           if (alc > 1u) emit(m1);
           if (alc > 2u) emit(m2);
           ++ncol;
-          ++root;
           SVS_PF_ADD(0, pf0);
           continue;
         }
@@ -726,11 +856,11 @@ __device__ int32_t dfs_sort(uint32_t V, uint32_t V0, const gu32* __restrict__ nr
       SVS_PF_EXAM(3, px3);
     }
     SVS_PF_ADD(1, pf0);
-    ++root;
   }
   flush_emit();
   *ncol_out = ncol;
   S.n_exam = static_cast<uint32_t>(steps);
+  S.n_emit = cnt;
   return (cnt == V && !S.err) ? kFoldOk : kFoldErrStack;
 }
 
@@ -1181,8 +1311,10 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
   SortState S;
   S.done = lds;
   S.ign = lds + W;
-  S.st = lds + 2 * W;
-  S.cap = ((lds_words - 2 * W) / 2) * 2;
+  S.chg = lds + 2 * W;
+  S.nseg = lds + 3 * W;
+  S.st = lds + 4 * W;
+  S.cap = ((lds_words - 4 * W) / 2) * 2;
   S.spill = g.stk;
   S.spilled = 0;
   S.sp = 0;
@@ -1190,6 +1322,7 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
   S.err = false;
   S.n_exam = 0;
   S.n_roots = 0;
+  S.n_emit = 0;
   S.prof[0] = S.prof[1] = S.prof[2] = S.prof[3] = 0;
   uint32_t ncol = 0;
   if (S.cap < 64) {
@@ -1205,17 +1338,28 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
       g.n2r[v] = v;
       g.col[v] = v;
     }
+    for (uint32_t w = lanei(); w < W; w += 64) g.seg[w] = ~0u;  // every node its own root
     ncol = V;
   } else {
     // the previous rank order, kept for the DFS's record windows (export
-    // reuses `last` after the sort)
+    // reuses `last` after the sort), and the fold's changed plane
     const uint32_t V0 = min(J.V, V);
     for (uint32_t r = lanei(); r < V0; r += 64) g.last[r] = g.r2n[r];
+    for (uint32_t w = lanei(); w < W; w += 64) lds[2 * W + w] = g.chg[w];
     wave_sync_mem();
-    st = dfs_sort(V, V0, g.nrec, g.in_nbr, g.r2n, g.n2r, g.last, g.col, S, &ncol);
+    st = dfs_sort(V, V0, g.nrec, g.in_nbr, g.r2n, g.n2r, g.last, g.col, V0 ? g.seg_other : nullptr, S, &ncol);
+    if (st == kFoldOk)
+      for (uint32_t w = lanei(); w < W; w += 64) g.seg[w] = S.nseg[w];
   }
   if (st != kFoldOk) {
-    if (lanei() == 0) res->status = st;
+    if (lanei() == 0) {
+      // for the host's message: nodes emitted, whether the stack overflowed
+      res->pad0 = S.n_emit;
+      res->pad1 = S.err ? 1u : 0u;
+      res->n_exam = S.n_exam;
+      res->n_roots = S.n_roots;
+      res->status = st;
+    }
     return;
   }
   wave_sync_mem();
@@ -1308,6 +1452,10 @@ __global__ __launch_bounds__(256) void poa_dgraph_move_kernel(const uint8_t* __r
   cp(A.col0, B.col0, 12ull * V);
   cp(A.rec, B.rec, 16ull * V);
   cp(A.pslot, B.pslot, 4ull * E);
+  // the last sort's segment starts (the next sort walks them), and the node
+  // records (the next update tells a changed aligned list by their counts)
+  cp(pick(A.seg), pick(B.seg), 4ull * ((V + 31) / 32 + 2));
+  cp(A.nrec, B.nrec, 32ull * V);
 }
 
 hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, uint32_t final_lds_words,

@@ -141,8 +141,10 @@ void PoaGraph::sort_ranks() {
   uint8_t* __restrict__ fl = flags.data();
   uint32_t* stk = stack.data();
   const uint32_t* __restrict__ etail = e_tail_.data();
+  seg_start_.assign(n, 0);
   for (uint32_t root = 0; root < n; ++root) {
     if (fl[root] != 0) continue;
+    if (cnt < n) seg_start_[cnt] = 1;
     size_t sp = 0;
     stk[sp++] = root;
     while (sp != 0) {

@@ -214,6 +214,8 @@ class PoaGraph {
   uint32_t num_edges() const { return static_cast<uint32_t>(e_tail_.size()); }
   uint32_t num_sequences() const { return static_cast<uint32_t>(paths_.size()); }
   bool empty() const { return base_.empty(); }
+  size_t in_degree(uint32_t v) const { return in_[v].size(); }
+  size_t aligned_count(uint32_t v) const { return aligned_[v].size(); }
 
   // pairs are (rank-row index 0-based or -1, sequence position or -1), in
   // forward order.  Node identity is resolved through the CURRENT rank order.
@@ -241,6 +243,9 @@ class PoaGraph {
   std::string consensus(int32_t min_coverage);
 
   const std::vector<uint32_t>& rank_to_node() const { return rank_to_node_; }
+  // by rank: 1 where a DFS root's segment of the order starts (the device
+  // sort's reuse plane, checked by SVS_POA_VERIFY_GRAPH)
+  const std::vector<uint8_t>& segment_starts() const { return seg_start_; }
 
  private:
   uint32_t new_node(char b);
@@ -258,6 +263,7 @@ class PoaGraph {
   std::vector<int64_t> e_w_;
   std::vector<std::vector<uint32_t>> paths_;
   std::vector<uint32_t> rank_to_node_, node_to_rank_;
+  std::vector<uint8_t> seg_start_;
 };
 
 }  // namespace svs

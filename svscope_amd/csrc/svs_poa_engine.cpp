@@ -943,7 +943,8 @@ struct PoaScheduler::Impl {
   // (SVS_POA_TEST_SORT_LDS_WORDS lowers the limit in tests)
   static constexpr uint64_t kSortLdsWordsMax = 160 * 1024 / 4 - 64;
   uint64_t sort_lds_max = kSortLdsWordsMax;
-  uint64_t sort_lds_words(uint64_t n) const { return 2 * ((n + 31) / 32) + sort_stack; }
+  // four bit planes (done, ignored, changed, segment starts) and the stack top
+  uint64_t sort_lds_words(uint64_t n) const { return 4 * ((n + 31) / 32) + sort_stack; }
   // SVS_POA_TEST_MAX_BLOCK_BYTES (tests): reserve_blocks treats a block larger
   // than this as past the arena's limit, so that one window fails alone
   size_t test_block_cap = ~size_t(0);
@@ -1101,7 +1102,7 @@ struct PoaScheduler::Impl {
         else if (len > 0 && rows * strip_ls(static_cast<uint32_t>(len)) > 0x7FFFFFFFull)
           why = "an alignment's traceback matrix exceeds 2^31 cells";
         else if (sort_lds_words(rows + len) > sort_lds_max)
-          why = "a POA graph too large for the sort kernel's LDS node flags (about 630,000 nodes)";
+          why = "a POA graph too large for the sort kernel's LDS node flags (about 315,000 nodes)";
         if (why) fail_task(g, id, why);
         else keep.push_back(id);
       }
@@ -1594,8 +1595,17 @@ struct PoaScheduler::Impl {
       const FoldJob& F = D.folds[i];
       if (r.status == kFoldSkipped) continue;  // a pruning retry: graph and tables unchanged
       if (!t.error.empty()) continue;          // the task failed at an earlier fold of this launch
-      if (r.status != kFoldOk)
-        throw SvsError(SVS_E_INTERNAL, "device POA graph fold failed (status " + std::to_string(r.status) + ")");
+      if (verify && r.status == kFoldErrStack) verify_fold(g, i, r);  // names the first table that differs
+      if (r.status != kFoldOk) {
+        std::string why = "device POA graph fold failed (status " + std::to_string(r.status) + "; fold of read " +
+                          std::to_string(F.n_paths) + ", graph " + std::to_string(F.V) + " nodes + read of " +
+                          std::to_string(F.len) + ", flags " + std::to_string(F.flags);
+        if (r.status == kFoldErrStack)
+          why += "; sort emitted " + std::to_string(r.pad0) + " of " + std::to_string(r.V) + " nodes, stack " +
+                 (r.pad1 ? "overflowed" : "ok") + ", " + std::to_string(r.n_exam) + " examinations, " +
+                 std::to_string(r.n_roots) + " roots";
+        throw SvsError(SVS_E_INTERNAL, why + ")");
+      }
       g_fold_times.add(r, F.flags);
       if (verify) verify_fold(g, i, r);
       if (i < D.n_pre) {
@@ -1669,6 +1679,12 @@ struct PoaScheduler::Impl {
     PoaTask& t = tasks[D.fold_ids[i]];
     const FoldJob& F = D.folds[i];
     const std::string& s = t.seqs[D.fold_seq[i]];
+    const uint32_t V0 = t.graph.num_nodes();
+    std::vector<size_t> deg0(V0), al0(V0);
+    for (uint32_t v = 0; v < V0; ++v) {
+      deg0[v] = t.graph.in_degree(v);
+      al0[v] = t.graph.aligned_count(v);
+    }
     if (F.flags & kFoldChain) {
       t.graph.add_alignment_nodes({}, s);
     } else {
@@ -1692,11 +1708,36 @@ struct PoaScheduler::Impl {
       throw SvsError(SVS_E_INTERNAL, "device graph differs from the host graph after fold (" + what + "), read " +
                                          std::to_string(D.fold_seq[i]) + ", V " + std::to_string(V));
     };
-    if (r.V != V || r.E != E) fail("node/edge counts " + std::to_string(r.V) + "/" + std::to_string(r.E));
     const DGraphLayout L = dgraph_layout(F.cv, F.ce);
+    if (!(F.flags & kFoldChain) && V0) {
+      // the update kernel's changed plane (the sort's reuse test)
+      std::vector<uint32_t> chg((V0 + 31) / 32);
+      SVS_HIP(hipMemcpy(chg.data(), F.blk + L.chg, 4 * chg.size(), hipMemcpyDeviceToHost));
+      uint32_t bad = 0, first = 0, dev1 = 0, host1 = 0;
+      for (uint32_t v = 0; v < V0; ++v) {
+        const bool c = t.graph.in_degree(v) != deg0[v] || t.graph.aligned_count(v) != al0[v];
+        const uint32_t d = (chg[v >> 5] >> (v & 31)) & 1u;
+        dev1 += d;
+        host1 += c ? 1u : 0u;
+        if (d != (c ? 1u : 0u) && bad++ == 0) first = v;
+      }
+      if (bad)
+        fail("changed flags: " + std::to_string(bad) + " differ, first node " + std::to_string(first) + "; device " +
+             std::to_string(dev1) + " set, host " + std::to_string(host1) + "; V0 " + std::to_string(V0) +
+             ", device V0 " + std::to_string(F.V) + ", par " + std::to_string(F.par) + ", cv " + std::to_string(F.cv));
+    }
+    if (r.V != V || r.E != E) fail("node/edge counts " + std::to_string(r.V) + "/" + std::to_string(r.E));
     std::vector<uint32_t> r2n(V);
     SVS_HIP(hipMemcpy(r2n.data(), F.blk + L.r2n, 4ull * V, hipMemcpyDeviceToHost));
     if (r2n != t.graph.rank_to_node()) fail("rank order");
+    {
+      // the segment starts the next sort walks (poa_fold.hip dfs_sort)
+      std::vector<uint32_t> seg((V + 31) / 32);
+      SVS_HIP(hipMemcpy(seg.data(), F.blk + L.seg[1 - F.par], 4 * seg.size(), hipMemcpyDeviceToHost));
+      const std::vector<uint8_t>& hs = t.graph.segment_starts();
+      for (uint32_t k = 0; k < V; ++k)
+        if (((seg[k >> 5] >> (k & 31)) & 1u) != hs[k]) fail("segment start at rank " + std::to_string(k));
+    }
     if (F.flags & kFoldExport) {
       RowTables h;
       std::vector<uint32_t> ps(V + 1), pr(E), inf(V);

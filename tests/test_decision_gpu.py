@@ -344,7 +344,7 @@ def test_big_windows_mixed_into_config3_batch_match_oracle():
 
 
 @pytest.mark.parametrize("env,why", [({"SVS_POA_TEST_MAX_ROWS": "4000"}, "planner"),
-                                     ({"SVS_POA_TEST_SORT_LDS_WORDS": "1300"}, "sort kernel"),
+                                     ({"SVS_POA_TEST_SORT_LDS_WORDS": "1800"}, "sort kernel"),
                                      ({"SVS_POA_TEST_MAX_BLOCK_BYTES": "2000000"}, "graph arena is full")])
 def test_window_past_an_engine_limit_fails_alone(env, why):
     """a window that goes past an engine limit fails alone
