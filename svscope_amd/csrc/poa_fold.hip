@@ -1472,6 +1472,12 @@ hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, 
   return hipGetLastError();
 }
 
+hipError_t launch_poa_final(const FoldJob* jobs, int n_jobs, uint32_t final_lds_words, hipStream_t stream) {
+  if (n_jobs <= 0 || final_lds_words == 0) return hipSuccess;
+  hipLaunchKernelGGL(poa_fold_final_kernel, dim3(n_jobs), dim3(64), final_lds_words * 4, stream, jobs, final_lds_words);
+  return hipGetLastError();
+}
+
 // The new tasks' read blocks from the launch's staging into their own blocks:
 // one workgroup per copy, 16-byte words.
 __global__ __launch_bounds__(256) void scatter_copy_kernel(const CopyDesc* __restrict__ d) {

@@ -146,6 +146,10 @@ struct PoaArena {
   // after the update, sort and final fold kernels: of the folds after the DP
   // kernel (evk) and of the new tasks' chains before it (evpk)
   hipEvent_t evk[3] = {nullptr, nullptr, nullptr}, evpk[3] = {nullptr, nullptr, nullptr};
+  // the final kernel on a stream of its own beside the table completion
+  // (SVS_POA_FINAL_STREAM): forked after the sort, joined before the copies
+  hipStream_t fin_stream = nullptr;
+  hipEvent_t ev_sorted = nullptr, ev_fin0 = nullptr, ev_fin1 = nullptr;
   // Staging of the next launch's strip tables in h_in: the fold exports each
   // job's tables straight into a block claimed with an atomic bump (st_cur), so
   // packing the launch copies nothing.  A new generation (st_gen) starts when
@@ -164,6 +168,10 @@ struct PoaArena {
     int least = 0, greatest = 0;
     SVS_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
     SVS_HIP(hipStreamCreateWithPriority(&copy_stream, hipStreamNonBlocking, greatest));
+    SVS_HIP(hipStreamCreateWithPriority(&fin_stream, hipStreamNonBlocking, greatest));
+    SVS_HIP(hipEventCreateWithFlags(&ev_sorted, hipEventDisableTiming));
+    SVS_HIP(hipEventCreate(&ev_fin0));
+    SVS_HIP(hipEventCreate(&ev_fin1));
     SVS_HIP(hipEventCreate(&ev0));
     SVS_HIP(hipEventCreate(&ev1));
     SVS_HIP(hipEventCreate(&evp));
@@ -180,6 +188,7 @@ struct PoaArena {
   ~PoaArena() {
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+    if (fin_stream) (void)hipStreamSynchronize(fin_stream);
     for (DeviceBuf* b : {&d_in, &d_tb, &d_pool, &d_aln, &d_alen, &d_desc, &d_fin}) b->release();
     for (PinnedBuf* b : {&h_in, &h_aln, &h_alen, &h_desc, &h_fin, &h_feat}) b->release();
     if (ev0) (void)hipEventDestroy(ev0);
@@ -194,6 +203,10 @@ struct PoaArena {
     }
     if (done) (void)hipEventDestroy(done);
     if (h2d) (void)hipEventDestroy(h2d);
+    if (ev_sorted) (void)hipEventDestroy(ev_sorted);
+    if (ev_fin0) (void)hipEventDestroy(ev_fin0);
+    if (ev_fin1) (void)hipEventDestroy(ev_fin1);
+    if (fin_stream) (void)hipStreamDestroy(fin_stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
   }
   PoaArena(const PoaArena&) = delete;

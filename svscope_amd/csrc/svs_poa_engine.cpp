@@ -645,6 +645,7 @@ struct DevLaunch {
   int wpj = 0;
   bool timed_dp = false;
   bool prune = false, wide = false;  // the DP kernel instance
+  bool split_final = false;          // the final kernel ran on the arena's fin_stream
 };
 
 // Task group: a disjoint subset of the active tasks with its own arena.
@@ -724,6 +725,18 @@ bool debug_launches() {
 bool sync_check() {
   const char* e = std::getenv("SVS_POA_SYNC_CHECK");
   return e && std::string(e) == "1";
+}
+// The final fold kernel on a stream of its own, beside the table completion
+// of the same launch (a finishing task needs no tables, a continuing one no
+// consensus), so the fold chain the group's next DP launch waits for is
+// update, sort, then the longer of the two: 427.3 / 429.9 vs 418.0 / 419.7
+// windows/s same box (profiles/r05_g1).  SVS_POA_FINAL_STREAM=0: in line.
+bool final_stream() {
+  static const bool on = [] {
+    const char* e = std::getenv("SVS_POA_FINAL_STREAM");
+    return !(e && std::string(e) == "0");
+  }();
+  return on;
 }
 
 size_t active_jobs_per_group() {
@@ -1468,11 +1481,23 @@ struct PoaScheduler::Impl {
     }
     // graph update, sort, export and table completion beside the other group's DP
     SVS_HIP(hipEventRecord(A.evf0, side));
+    const uint32_t fin_lds = nj ? final_lds(npre, npre + nj) : 0u;
+    D.split_final = fin_lds && final_stream();
     if (nj) {
-      SVS_HIP(launch_poa_fold(dfold + npre, static_cast<int>(nj), lds_words, final_lds(npre, npre + nj), side, A.evk));
+      SVS_HIP(launch_poa_fold(dfold + npre, static_cast<int>(nj), lds_words, D.split_final ? 0u : fin_lds, side, A.evk));
+      if (D.split_final) {
+        // a finishing task needs no tables and a continuing one no consensus:
+        // the final kernel runs beside the table completion
+        SVS_HIP(hipEventRecord(A.ev_sorted, side));
+        SVS_HIP(hipStreamWaitEvent(A.fin_stream, A.ev_sorted, 0));
+        SVS_HIP(hipEventRecord(A.ev_fin0, A.fin_stream));
+        SVS_HIP(launch_poa_final(dfold + npre, static_cast<int>(nj), fin_lds, A.fin_stream));
+        SVS_HIP(hipEventRecord(A.ev_fin1, A.fin_stream));
+      }
       SVS_HIP(launch_dgraph_prep(dfold + npre, static_cast<int>(nj), score, side));
     }
     SVS_HIP(hipEventRecord(A.evf1, side));
+    if (D.split_final) SVS_HIP(hipStreamWaitEvent(side, A.ev_fin1, 0));
     A.h_alen.ensure(nj * 12 + 64);
     if (nj) SVS_HIP(hipMemcpyAsync(A.h_alen.ptr, A.d_alen.ptr, nj * 12, hipMemcpyDeviceToHost, side));
     SVS_HIP(hipMemcpyAsync(hd + s_res, dd + s_res, nf * sizeof(FoldResult), hipMemcpyDeviceToHost, side));
@@ -1550,6 +1575,11 @@ struct PoaScheduler::Impl {
         }
       };
       if (nj) phases(A.evf0, A.evk, A.evf1);
+      if (nj && D.split_final) {
+        float t = 0.f;
+        SVS_HIP(hipEventElapsedTime(&t, A.ev_fin0, A.ev_fin1));
+        st.fold_final_ms += t;
+      }
       if (D.n_pre) phases(A.evp, A.evpk, A.evp1);
     }
     if (g_trace.f) {
