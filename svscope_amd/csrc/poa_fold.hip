@@ -1384,11 +1384,13 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
 // The last read's fold (kFoldFinal): consensus and MSA rows, after the sort.
 // lds_words: the LDS the launch gives each job (6 B per node for the scores
 // and predecessors; larger graphs score in global memory).
-__global__ __launch_bounds__(64) void poa_fold_final_kernel(const FoldJob* __restrict__ jobs, uint32_t lds_words) {
+// idx (optional): the final folds' indices into jobs, one per workgroup.
+__global__ __launch_bounds__(64) void poa_fold_final_kernel(const FoldJob* __restrict__ jobs, uint32_t lds_words,
+                                                            const uint32_t* __restrict__ idx) {
   SVS_FOLD_PRIO();
   extern __shared__ uint32_t lds[];
   const uint64_t T0 = __builtin_amdgcn_s_memrealtime();
-  const FoldJob J = jobs[blockIdx.x];
+  const FoldJob J = jobs[idx ? idx[blockIdx.x] : blockIdx.x];
   if (!(J.flags & kFoldFinal)) return;
   GLB FoldResult* res = glb(J.result);
   if (uni(static_cast<uint32_t>(res->status)) != static_cast<uint32_t>(kFoldOk)) return;
@@ -1467,14 +1469,16 @@ hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, 
   if (marks) (void)hipEventRecord(marks[1], stream);
   if (final_lds_words)
     hipLaunchKernelGGL(poa_fold_final_kernel, dim3(n_jobs), dim3(64), final_lds_words * 4, stream, jobs,
-                       final_lds_words);
+                       final_lds_words, static_cast<const uint32_t*>(nullptr));
   if (marks) (void)hipEventRecord(marks[2], stream);
   return hipGetLastError();
 }
 
-hipError_t launch_poa_final(const FoldJob* jobs, int n_jobs, uint32_t final_lds_words, hipStream_t stream) {
-  if (n_jobs <= 0 || final_lds_words == 0) return hipSuccess;
-  hipLaunchKernelGGL(poa_fold_final_kernel, dim3(n_jobs), dim3(64), final_lds_words * 4, stream, jobs, final_lds_words);
+hipError_t launch_poa_final(const FoldJob* jobs, const uint32_t* idx, int n_final, uint32_t final_lds_words,
+                            hipStream_t stream) {
+  if (n_final <= 0 || final_lds_words == 0) return hipSuccess;
+  hipLaunchKernelGGL(poa_fold_final_kernel, dim3(n_final), dim3(64), final_lds_words * 4, stream, jobs, final_lds_words,
+                     idx);
   return hipGetLastError();
 }
 

@@ -107,8 +107,10 @@ struct FoldJob;
 // update, the sort and the final kernel
 hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, uint32_t final_lds_words,
                            hipStream_t stream, const hipEvent_t* marks = nullptr);
-// the final kernel alone (after the sort, on a stream of its own)
-hipError_t launch_poa_final(const FoldJob* jobs, int n_jobs, uint32_t final_lds_words, hipStream_t stream);
+// the final kernel alone (after the sort, on a stream of its own), one
+// workgroup per final fold: jobs[idx[k]], k < n_final
+hipError_t launch_poa_final(const FoldJob* jobs, const uint32_t* idx, int n_final, uint32_t final_lds_words,
+                            hipStream_t stream);
 hipError_t launch_dgraph_prep(const FoldJob* jobs, int n_jobs, const PoaScore& score, hipStream_t stream);
 hipError_t launch_dgraph_move(const uint8_t* src, uint32_t cv0, uint32_t ce0, uint8_t* dst, uint32_t cv1, uint32_t ce1,
                               uint32_t V, uint32_t E, uint32_t par, hipStream_t stream);

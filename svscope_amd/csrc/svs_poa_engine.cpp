@@ -641,6 +641,7 @@ struct DevLaunch {
   std::vector<size_t> cons_off, msa_off;         // fold i's final outputs in the fin buffer
   std::vector<size_t> feat_off;                  // fold i's seqdatamx in the group's h_feat (kFoldFeat)
   size_t n_aln = 0, s_fold = 0, s_res = 0, fin_bytes = 0;
+  size_t s_fidx = 0, n_fin = 0;  // the post-DP final folds' indices (from the first post-DP fold)
   size_t fin_copy = 0;  // bytes of the fin buffer copied back (consensus first; MSA rows when wanted)
   int wpj = 0;
   bool timed_dp = false;
@@ -1367,7 +1368,17 @@ struct PoaScheduler::Impl {
     const size_t s_res = round_up(s_fold + nf * sizeof(FoldJob), 256);
     const size_t s_up = round_up(s_res + nf * sizeof(FoldResult), 256);
     const size_t s_cp = round_up(s_up + up_total, 256);
-    const size_t total = s_cp + uploads.size() * sizeof(CopyDesc);
+    // the final kernel's grid: the post-DP folds with kFoldFinal only (each
+    // workgroup of a launch gets the launch's LDS, up to 64 KiB: a grid over
+    // every fold made ~2,000 empty workgroups wait for that much LDS beside
+    // the other group's DP workgroups)
+    std::vector<uint32_t> fin_idx;
+    for (size_t i = npre; i < nf; ++i)
+      if (D.folds[i].flags & kFoldFinal) fin_idx.push_back(static_cast<uint32_t>(i - npre));
+    const size_t s_fidx = round_up(s_cp + uploads.size() * sizeof(CopyDesc), 256);
+    const size_t total = s_fidx + fin_idx.size() * sizeof(uint32_t);
+    D.s_fidx = s_fidx;
+    D.n_fin = fin_idx.size();
     D.s_fold = s_fold;
     D.s_res = s_res;
     A.h_desc.ensure(total);
@@ -1399,6 +1410,7 @@ struct PoaScheduler::Impl {
       r.status = kFoldNotRun;  // only the update kernel makes it kFoldOk
       std::memcpy(hd + s_res + i * sizeof(FoldResult), &r, sizeof(r));
     }
+    if (!fin_idx.empty()) std::memcpy(hd + s_fidx, fin_idx.data(), fin_idx.size() * sizeof(uint32_t));
     CopyDesc* cps = reinterpret_cast<CopyDesc*>(hd + s_cp);
     for (size_t u = 0; u < uploads.size(); ++u)
       cps[u] = CopyDesc{dd + s_up + uploads[u].first, uploads[u].second->d_static, round_up(up_bytes[u], 64)};
@@ -1491,7 +1503,8 @@ struct PoaScheduler::Impl {
         SVS_HIP(hipEventRecord(A.ev_sorted, side));
         SVS_HIP(hipStreamWaitEvent(A.fin_stream, A.ev_sorted, 0));
         SVS_HIP(hipEventRecord(A.ev_fin0, A.fin_stream));
-        SVS_HIP(launch_poa_final(dfold + npre, static_cast<int>(nj), fin_lds, A.fin_stream));
+        SVS_HIP(launch_poa_final(dfold + npre, reinterpret_cast<const uint32_t*>(dd + D.s_fidx),
+                                 static_cast<int>(D.n_fin), fin_lds, A.fin_stream));
         SVS_HIP(hipEventRecord(A.ev_fin1, A.fin_stream));
       }
       SVS_HIP(launch_dgraph_prep(dfold + npre, static_cast<int>(nj), score, side));
