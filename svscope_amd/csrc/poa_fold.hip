@@ -155,9 +155,17 @@ __device__ __forceinline__ GPtr gptr(uint8_t* blk, uint32_t cv, uint32_t ce, uin
 // plane chg: a node of the old graph whose in-edge list gained an entry or
 // whose aligned list grew (the record's aligned count differs), and every new
 // node.  Returns the number of new entries found.
-__device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, const gu32* nbr0, const gu32* eid0,
-                                gu32* off1, gu32* nbr1, gu32* eid1, gu32* nw, gu32* nrec, const gu32* al,
-                                gu32* chg) {
+//
+// Per 64-node chunk the old entries are moved edge-parallel, 64 per store:
+// an old entry x of node v moves by the chunk's running offset plus one for
+// every node u < v of the chunk that gains an entry (u's new entry goes at the
+// end of u's list), i.e. every such u whose old list ends at or before x (a
+// per-node loop over each node's entries had the lanes wait on one
+// dependent load after another: 68 % of the update kernel's clocks).
+__device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* __restrict__ off0,
+                                const gu32* __restrict__ nbr0, const gu32* __restrict__ eid0, gu32* __restrict__ off1,
+                                gu32* __restrict__ nbr1, gu32* __restrict__ eid1, gu32* __restrict__ nw,
+                                gu32* __restrict__ nrec, const gu32* __restrict__ al, gu32* __restrict__ chg) {
   const uint32_t lane = lanei();
   uint32_t run = 0, found = 0;
   for (uint32_t v0 = 0; v0 < V1; v0 += 64) {
@@ -174,13 +182,26 @@ __device__ uint32_t rebuild_csr(uint32_t V0, uint32_t V1, const gu32* off0, cons
     const uint32_t has = ne != kNone ? 1u : 0u;
     uint32_t tot;
     const uint32_t o = run + wave_excl(d + has, &tot);
+    if (v0 < V0) {
+      // the chunk's old entries [xa, xb), contiguous in both buffers but for
+      // the new entries that land between them
+      const uint32_t nold = min(64u, V0 - v0);
+      const uint32_t xa = lane_val(a, 0), xb = lane_val(a + d, nold - 1u);
+      const uint64_t hm = ballot(has != 0u && v < V0);
+      const uint32_t end = a + d;  // node v's old list ends here
+      for (uint32_t x0 = xa; x0 < xb; x0 += 64u) {
+        const uint32_t x = x0 + lane;
+        uint32_t s = run - xa;
+        for (uint64_t m = hm; m; m &= m - 1u) s += x >= lane_val(end, static_cast<uint32_t>(__builtin_ctzll(m))) ? 1u : 0u;
+        if (x < xb) {
+          nbr1[x + s] = nbr0[x];
+          eid1[x + s] = eid0[x];
+        }
+      }
+    }
     bool changed = true;
     if (v < V1) {
       off1[v] = o;
-      for (uint32_t k = 0; k < d; ++k) {
-        nbr1[o + k] = nbr0[a + k];
-        eid1[o + k] = eid0[a + k];
-      }
       if (has) {
         nbr1[o + d] = nb;
         eid1[o + d] = ne;
@@ -246,6 +267,19 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
   const uint32_t b0 = J.par, b1 = 1u - J.par;
   const GPtr g = gptr(J.blk, J.cv, J.ce, b0);
   const GPtr h = gptr(J.blk, J.cv, J.ce, b1);
+#ifdef SVS_FOLD_PROF_UPD
+  // development builds: clocks of the update's phases into prof[0..3] (middle,
+  // edges, in-list rebuild, out-list rebuild)
+  uint64_t pu = __builtin_readcyclecounter();
+  uint32_t pud[4] = {0, 0, 0, 0};
+  auto pmark = [&](int k) {
+    const uint64_t t = __builtin_readcyclecounter();
+    pud[k] = static_cast<uint32_t>((t - pu) >> 10);
+    pu = t;
+  };
+#else
+  auto pmark = [](int) {};
+#endif
   gu32* __restrict__ path = glb(J.paths) + glb(J.path_off)[J.n_paths];
   const gu8* __restrict__ seq = glb(J.seq);
   const gi32* __restrict__ aln = glb(J.aln);
@@ -372,6 +406,7 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
   }
   if (next > J.cv || next - V0 > len) return fail(kFoldErrCapacity);
   wave_sync_mem();
+  pmark(0);
 
   // edges along the path: existing ones gain weight, new ones are recorded at
   // their head (nin) and tail (nout) for the CSR rebuild
@@ -407,16 +442,22 @@ __global__ __launch_bounds__(64) void poa_fold_update_kernel(const FoldJob* __re
     E1 += popc64(nm);
   }
   wave_sync_mem();
+  pmark(1);
   const uint32_t V1 = next;
   // both adjacency lists into the other buffer, the new edge of each node last
   const uint32_t fin =
       rebuild_csr(V0, V1, g.in_off, g.in_nbr, g.in_eid, h.in_off, h.in_nbr, h.in_eid, g.nin, g.nrec, g.al, g.chg);
+  pmark(2);
   const uint32_t fout =
       rebuild_csr(V0, V1, g.out_off, g.out_nbr, g.out_eid, h.out_off, h.out_nbr, h.out_eid, g.nout, nullptr, nullptr,
                   nullptr);
+  pmark(3);
   // a node twice on the path would have lost one of its new edges
   if (fin != E1 - E0 || fout != E1 - E0) return fail(kFoldErrPath);
   if (lane == 0) {
+#ifdef SVS_FOLD_PROF_UPD
+    for (int k = 0; k < 4; ++k) res->prof[k] = pud[k];
+#endif
     res->status = kFoldOk;
     res->V = V1;
     res->E = E1;
@@ -1377,7 +1418,9 @@ __global__ __launch_bounds__(64) void poa_fold_sort_kernel(const FoldJob* __rest
     res->t_exp = static_cast<uint32_t>(T2 - T1);
     res->n_exam = S.n_exam;
     res->n_roots = S.n_roots;
+#ifndef SVS_FOLD_PROF_UPD
     for (int k = 0; k < 4; ++k) res->prof[k] = static_cast<uint32_t>(S.prof[k] >> SVS_PF_SHIFT(k));
+#endif
   }
 }
 

@@ -710,6 +710,12 @@ struct FoldTimes {
                  static_cast<unsigned long long>(n_exp), n_exp ? exp / n_exp : 0.0,
                  static_cast<unsigned long long>(n_fin), n_fin ? fin / n_fin : 0.0, max_fin, double(exams) / n,
                  double(roots) / n);
+#ifdef SVS_FOLD_PROF_UPD
+    std::fprintf(stderr, "[svs] update phases per fold (kclk): middle %.0f, edges %.0f, in-list %.0f, out-list %.0f\n",
+                 double(prof[0]) * 1.024 / n, double(prof[1]) * 1.024 / n, double(prof[2]) * 1.024 / n,
+                 double(prof[3]) * 1.024 / n);
+    return;
+#endif
     if (prof[0] || prof[1])
       std::fprintf(stderr,
                    "[svs] DFS profile per fold: fast roots %.0f kclk, DFS runs %.0f kclk, %.1f new-node and %.1f "
