@@ -1464,11 +1464,16 @@ __global__ __launch_bounds__(64) void poa_fold_final_kernel(const FoldJob* __res
 }
 
 // Block growth: the graph of a task moved into a larger block (capacities
-// cv1 >= cv0, ce1 >= ce0), both CSR buffers' current one only.
-__global__ __launch_bounds__(256) void poa_dgraph_move_kernel(const uint8_t* __restrict__ src, uint32_t cv0,
-                                                              uint32_t ce0, uint8_t* __restrict__ dst, uint32_t cv1,
-                                                              uint32_t ce1, uint32_t V, uint32_t E, uint32_t par) {
-  const DGraphLayout A = dgraph_layout(cv0, ce0), B = dgraph_layout(cv1, ce1);
+// cv1 >= cv0, ce1 >= ce0), both CSR buffers' current one only; one row of
+// workgroups per move (blockIdx.y), every move of a launch in one kernel
+// (one kernel per move had ~36 small kernels per launch queue up on the copy
+// stream ahead of the DP kernel).
+__global__ __launch_bounds__(256) void poa_dgraph_move_kernel(const MoveDesc* __restrict__ moves) {
+  const MoveDesc M = moves[blockIdx.y];
+  const uint8_t* __restrict__ src = M.src;
+  uint8_t* __restrict__ dst = M.dst;
+  const uint32_t V = M.V, E = M.E, par = M.par;
+  const DGraphLayout A = dgraph_layout(M.cv0, M.ce0), B = dgraph_layout(M.cv1, M.ce1);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
   auto cp = [&](size_t a, size_t b, size_t bytes) {
     const uint32_t* s = reinterpret_cast<const uint32_t*>(src + a);
@@ -1540,9 +1545,9 @@ hipError_t launch_scatter_copy(const CopyDesc* d, int n, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t launch_dgraph_move(const uint8_t* src, uint32_t cv0, uint32_t ce0, uint8_t* dst, uint32_t cv1, uint32_t ce1,
-                              uint32_t V, uint32_t E, uint32_t par, hipStream_t stream) {
-  hipLaunchKernelGGL(poa_dgraph_move_kernel, dim3(64), dim3(256), 0, stream, src, cv0, ce0, dst, cv1, ce1, V, E, par);
+hipError_t launch_dgraph_moves(const MoveDesc* d, int n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(poa_dgraph_move_kernel, dim3(16, static_cast<uint32_t>(n)), dim3(256), 0, stream, d);
   return hipGetLastError();
 }
 

@@ -112,8 +112,14 @@ hipError_t launch_poa_fold(const FoldJob* jobs, int n_jobs, uint32_t lds_words, 
 hipError_t launch_poa_final(const FoldJob* jobs, const uint32_t* idx, int n_final, uint32_t final_lds_words,
                             hipStream_t stream);
 hipError_t launch_dgraph_prep(const FoldJob* jobs, int n_jobs, const PoaScore& score, hipStream_t stream);
-hipError_t launch_dgraph_move(const uint8_t* src, uint32_t cv0, uint32_t ce0, uint8_t* dst, uint32_t cv1, uint32_t ce1,
-                              uint32_t V, uint32_t E, uint32_t par, hipStream_t stream);
+// A task's graph moved into a larger block (capacities cv1 >= cv0, ce1 >= ce0);
+// every move of a launch in one kernel
+struct MoveDesc {
+  const uint8_t* src;
+  uint8_t* dst;
+  uint32_t cv0, ce0, cv1, ce1, V, E, par, pad;
+};
+hipError_t launch_dgraph_moves(const MoveDesc* d, int n, hipStream_t stream);
 hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,
                                 hipStream_t stream);
 

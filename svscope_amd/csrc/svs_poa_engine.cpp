@@ -1382,7 +1382,8 @@ struct PoaScheduler::Impl {
     for (size_t i = npre; i < nf; ++i)
       if (D.folds[i].flags & kFoldFinal) fin_idx.push_back(static_cast<uint32_t>(i - npre));
     const size_t s_fidx = round_up(s_cp + uploads.size() * sizeof(CopyDesc), 256);
-    const size_t total = s_fidx + fin_idx.size() * sizeof(uint32_t);
+    const size_t s_mv = round_up(s_fidx + fin_idx.size() * sizeof(uint32_t), 256);
+    const size_t total = s_mv + moves.size() * sizeof(MoveDesc);
     D.s_fidx = s_fidx;
     D.n_fin = fin_idx.size();
     D.s_fold = s_fold;
@@ -1417,6 +1418,13 @@ struct PoaScheduler::Impl {
       std::memcpy(hd + s_res + i * sizeof(FoldResult), &r, sizeof(r));
     }
     if (!fin_idx.empty()) std::memcpy(hd + s_fidx, fin_idx.data(), fin_idx.size() * sizeof(uint32_t));
+    for (size_t k = 0; k < moves.size(); ++k) {
+      const auto& m = moves[k];
+      reinterpret_cast<MoveDesc*>(hd + s_mv)[k] =
+          MoveDesc{reinterpret_cast<const uint8_t*>(m[0]), reinterpret_cast<uint8_t*>(m[3]), static_cast<uint32_t>(m[1]),
+                   static_cast<uint32_t>(m[2]), static_cast<uint32_t>(m[4]), static_cast<uint32_t>(m[5]),
+                   static_cast<uint32_t>(m[6]), static_cast<uint32_t>(m[7]), static_cast<uint32_t>(m[8]), 0u};
+    }
     CopyDesc* cps = reinterpret_cast<CopyDesc*>(hd + s_cp);
     for (size_t u = 0; u < uploads.size(); ++u)
       cps[u] = CopyDesc{dd + s_up + uploads[u].first, uploads[u].second->d_static, round_up(up_bytes[u], 64)};
@@ -1430,11 +1438,7 @@ struct PoaScheduler::Impl {
     SVS_HIP(hipMemcpyAsync(dd, hd, total, hipMemcpyHostToDevice, side));
     if (!uploads.empty())
       SVS_HIP(launch_scatter_copy(reinterpret_cast<const CopyDesc*>(dd + s_cp), static_cast<int>(uploads.size()), side));
-    for (const auto& m : moves)
-      SVS_HIP(launch_dgraph_move(reinterpret_cast<const uint8_t*>(m[0]), static_cast<uint32_t>(m[1]),
-                                 static_cast<uint32_t>(m[2]), reinterpret_cast<uint8_t*>(m[3]),
-                                 static_cast<uint32_t>(m[4]), static_cast<uint32_t>(m[5]), static_cast<uint32_t>(m[6]),
-                                 static_cast<uint32_t>(m[7]), static_cast<uint32_t>(m[8]), side));
+    SVS_HIP(launch_dgraph_moves(reinterpret_cast<const MoveDesc*>(dd + s_mv), static_cast<int>(moves.size()), side));
     uint32_t lds_words = 0;
     for (const FoldJob& F : D.folds) lds_words = std::max(lds_words, static_cast<uint32_t>(sort_lds_words(F.V + F.len)));
     // (the DFS stack's LDS part is in it; deeper stacks spill)
