@@ -5,13 +5,13 @@
 // against spoa's full DFS order (the oracle's Graph::topological_sort).
 // Test tooling only (it links the CPU oracle).
 //
-//   g++ -O2 -std=c++17 -o /tmp/sort_walk_replay tools/sort_walk_replay.cpp
+//   g++ -O2 -std=c++17 -o /tmp/sort_walk_replay tests/cpp/sort_walk_replay.cpp
 //   /tmp/sort_walk_replay SEQS.txt SEED TRIALS
 //
 // SEQS.txt: one sequence per line (a task's reads in order).  Trial 0 folds
 // them all; trials 1.. fold random thirds of them (consensus-like subsets).
 // Prints the DFS examinations the walk still runs and the ranks it copies.
-#include "../oracle/spoa_oracle.cpp"
+#include "../../oracle/spoa_oracle.cpp"
 #include <fstream>
 #include <iostream>
 #include <random>
