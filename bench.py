@@ -275,9 +275,17 @@ def main():
         hostcpu.apply(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
         import torch
         import torch.distributed as dist
+        from svscope_amd.local_graph import rank_device
+        # RCCL over the node's GPUs, one per rank; SVS_DIST_BACKEND=gloo with
+        # SVS_DEVICE=d rehearses the N > 1 path with every rank on GPU d
+        backend = os.environ.get("SVS_DIST_BACKEND", "nccl")
+        local = rank_device(backend, local, os.environ)
         torch.cuda.set_device(local)
         os.environ["SVS_DEVICE"] = str(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from svscope_amd import _abi
     from svscope_amd.decision_maker import DecisionSession
@@ -308,7 +316,8 @@ def main():
     if dist is not None:
         # every rank's own elapsed time and windows (SCALE shows LPT / box
         # imbalance), then time = the max over ranks
-        mine = torch.tensor([elapsed, float(len(recs))], dtype=torch.float64, device=f"cuda:{local}")
+        gdev = f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu"
+        mine = torch.tensor([elapsed, float(len(recs))], dtype=torch.float64, device=gdev)
         every = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(every, mine)
         per = [x.tolist() for x in every]

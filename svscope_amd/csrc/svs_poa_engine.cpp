@@ -767,6 +767,19 @@ size_t active_jobs_per_group() {
   return 2048;
 }
 
+// Task groups (SVS_POA_GROUPS, 2 to 4; default 2): each with its own arena,
+// DP stream and fold chain.  With more groups a DP launch is ready more often
+// while another group folds; the default tasks per group shrink so that the
+// tasks in flight stay at 4096.
+constexpr int kMaxGroups = 4;
+int poa_groups() {
+  if (const char* e = std::getenv("SVS_POA_GROUPS")) {
+    const int v = std::atoi(e);
+    if (v >= 2 && v <= kMaxGroups) return v;
+  }
+  return 2;
+}
+
 }  // namespace
 
 struct PoaScheduler::Impl {
@@ -776,7 +789,8 @@ struct PoaScheduler::Impl {
   svs_poa_stats& st;
   std::deque<PoaTask> tasks;
   std::deque<uint32_t> queue;
-  Group groups[2];
+  const int n_groups = poa_groups();
+  Group groups[kMaxGroups];
   size_t cap;
   size_t budget;
   double host_ms = 0.0;
@@ -794,7 +808,8 @@ struct PoaScheduler::Impl {
 
   Impl(svs_context* c, const svs_poa_config& k, svs_poa_stats& s)
       : ctx(c), cfg(k), score{k.m, k.n, k.g, k.e, k.q, k.c}, st(s), cap(active_jobs_per_group()),
-        budget(c->device_budget / 2), dev(device_graphs(k)), verify(verify_graph()) {
+        budget(c->device_budget / n_groups), dev(device_graphs(k)), verify(verify_graph()) {
+    if (n_groups != 2 && !std::getenv("SVS_POA_ACTIVE_JOBS")) cap = 2 * cap / n_groups;
     if (const char* e = std::getenv("SVS_POA_SORT_STACK")) {
       const long v = std::atol(e);
       if (v >= 64 && v <= 1024) sort_stack = static_cast<uint32_t>(v) & ~1u;
@@ -812,8 +827,9 @@ struct PoaScheduler::Impl {
       darena = ctx->dgraph_arena.get();
     }
     // (both arenas start on the context's stream; the DP streams below)
-    while (ctx->poa_arenas.size() < 2) ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
-    for (int g = 0; g < 2; ++g) groups[g].arena = ctx->poa_arenas[g].get();
+    while (ctx->poa_arenas.size() < static_cast<size_t>(n_groups))
+      ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
+    for (int g = 0; g < n_groups; ++g) groups[g].arena = ctx->poa_arenas[g].get();
     split_cus();
     // Each group's DP kernel on a stream of its own (round 5), so that one
     // group's launch starts in the tail of the other's: a launch ends with its
@@ -826,20 +842,20 @@ struct PoaScheduler::Impl {
     // context's stream.
     const char* dse = std::getenv("SVS_POA_DP_STREAMS");
     if (!(dse && std::atoi(dse) == 1) && !ctx->poa_fold_cus)
-      for (int g = 0; g < 2; ++g) {
+      for (int g = 0; g < n_groups; ++g) {
         SVS_HIP(hipStreamCreateWithFlags(&own_dp[g], hipStreamNonBlocking));
         groups[g].arena->stream = own_dp[g];
       }
   }
   ~Impl() {
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < n_groups; ++g)
       if (own_dp[g]) {
         (void)hipStreamSynchronize(own_dp[g]);
         groups[g].arena->stream = ctx->stream;
         (void)hipStreamDestroy(own_dp[g]);
       }
   }
-  hipStream_t own_dp[2] = {nullptr, nullptr};
+  hipStream_t own_dp[kMaxGroups] = {nullptr, nullptr, nullptr, nullptr};
 
   // SVS_POA_FOLD_CUS=n (device-resident graphs, shared DP stream): n CUs,
   // spread evenly over the device, run the fold kernels (the groups' copy
@@ -890,9 +906,10 @@ struct PoaScheduler::Impl {
       });
       queue_dirty = false;
     }
-    const Group& o = groups[1 - gid(g)];
+    size_t others = 0;  // other groups with room: the queue is shared out among them
+    for (int k = 0; k < n_groups; ++k) others += (k != gid(g) && groups[k].active.size() < cap) ? 1u : 0u;
     const size_t room = cap - g.active.size();
-    const size_t share = o.active.size() < cap ? std::max<size_t>(1, (queue.size() + 1) / 2) : queue.size();
+    const size_t share = others ? std::max<size_t>(1, (queue.size() + others) / (others + 1)) : queue.size();
     size_t take = std::min(room, share);
     while (take-- > 0 && !queue.empty()) {
       g.active.push_back(queue.front());
@@ -1276,8 +1293,8 @@ struct PoaScheduler::Impl {
     // (hints: the carries are 16 B per 64 traceback codes, the pairs 8 B per
     // row and read base; sized once for the group's budget instead of growing
     // with the graphs)
-    A.d_tb.ensure(n_tb * (wide ? 4 : 2) + 4096, ctx->device_budget / 2);
-    A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096, ctx->device_budget / 16);
+    A.d_tb.ensure(n_tb * (wide ? 4 : 2) + 4096, ctx->device_budget / n_groups);
+    A.d_pool.ensure((n_bnd + n_pool) * 4 + 4096, ctx->device_budget / (8 * n_groups));
     A.d_aln.ensure(n_aln * 8 + 64, 256ull << 20);
     A.d_alen.ensure(nj * 12 + 64);
     // fold jobs, growing blocks that could not hold this fold
@@ -1950,10 +1967,12 @@ struct PoaScheduler::Impl {
 
   void run(const DoneFn& done, const PollFn& poll) {
     g_trace.open(ctx->stream);
-    for (Group& g : groups) advance(g, done);
+    Group* const gend = groups + n_groups;
+    for (Group* gp = groups; gp != gend; ++gp) advance(*gp, done);
     for (;;) {
       bool progressed = false;
-      for (Group& g : groups) {
+      for (Group* gp = groups; gp != gend; ++gp) {
+        Group& g = *gp;
         if (!g.pending) continue;
         if (dev) finish_dev(g);
         else finish(ctx, g.la, tasks, st, host_ms, cfg, [this] { return reap(); });
@@ -1964,9 +1983,12 @@ struct PoaScheduler::Impl {
       const auto tq0 = Clock::now();
       const bool outside = poll(false);
       g_trace.host("poll", -1, tq0, 0);
-      for (Group& g : groups)
+      bool busy = false;
+      for (Group* gp = groups; gp != gend; ++gp) {
+        Group& g = *gp;
         if (!g.pending && (!queue.empty() || !g.completed.empty() || (dev && !g.active.empty()))) advance(g, done);
-      const bool busy = groups[0].pending || groups[1].pending;
+        busy = busy || g.pending;
+      }
       if (progressed || busy) continue;
       if (outside) {
         const auto tb0 = Clock::now();
