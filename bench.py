@@ -330,6 +330,8 @@ def main():
     cells, cells_done = poa["dp_cells"], poa["cells_computed"]
     kms, launches = poa["kernel_ms"], poa["launches"]
     achieved = cells_done * BYTES_PER_CELL / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    busy_ms = poa.get("kernel_busy_ms", 0.0)
+    busy_achieved = cells_done * BYTES_PER_CELL / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
     total_windows = B * K * world
 
     em_flops = st.get("em_flops", 0.0)
@@ -364,6 +366,14 @@ def main():
                          "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(cells_done * BYTES_PER_CELL / max(1, launches)),
                          "mean_launch_ms": round(kms / max(1, launches), 4),
+                         # the same bytes over the device time during which at least one
+                         # DP launch ran (union of the launches' HIP-event intervals): two
+                         # task groups' launches overlap on their DP streams, and the
+                         # per-launch durations above count the shared time twice
+                         "dp_busy": {"busy_ms": round(busy_ms, 2),
+                                     "launch_ms_over_busy_ms": round(kms / busy_ms, 4) if busy_ms else None,
+                                     "achieved": round(busy_achieved, 2),
+                                     "frac": round(busy_achieved / HBM_PEAK_GBS, 5)},
                          # SURVEY.md §8(d) prices Σcells over every DP cell of spoa's full
                          # matrix (its "50 % needs ~2e11 cells/s, ~100 windows/s");
                          # frac above counts only the cells the pruned kernel evaluates

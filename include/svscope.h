@@ -75,6 +75,10 @@ typedef struct svs_poa_stats {
      task blocks live at once, and the HBM the arena holds (hipMalloc'ed chunks;
      never returned before svs_release) */
   uint64_t dgraph_peak_bytes, dgraph_reserved_bytes;
+  /* device time during which at least one DP launch ran: the union of the
+     launches' HIP-event intervals (kernel_ms sums them, so it counts twice the
+     time two task groups' launches overlap on their DP streams) */
+  double kernel_busy_ms;
 } svs_poa_stats;
 
 /* One context per host thread; owns a HIP stream and device arenas. */

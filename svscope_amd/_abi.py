@@ -45,7 +45,8 @@ class PoaStats(ctypes.Structure):
                 ("fold_ms", ctypes.c_double), ("fold_jobs", ctypes.c_uint64), ("wide_launches", ctypes.c_uint64),
                 ("fold_update_ms", ctypes.c_double), ("fold_sort_ms", ctypes.c_double),
                 ("fold_final_ms", ctypes.c_double), ("fold_prep_ms", ctypes.c_double),
-                ("dgraph_peak_bytes", ctypes.c_uint64), ("dgraph_reserved_bytes", ctypes.c_uint64)]
+                ("dgraph_peak_bytes", ctypes.c_uint64), ("dgraph_reserved_bytes", ctypes.c_uint64),
+                ("kernel_busy_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

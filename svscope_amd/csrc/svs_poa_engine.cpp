@@ -18,6 +18,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -113,6 +114,42 @@ struct PoaTrace {
   }
 };
 PoaTrace g_trace;
+
+// Device time during which at least one timed DP launch was running: the
+// union of the launches' [ev0, ev1] intervals on the GPU clock, placed through
+// an epoch event recorded when the scheduler starts.  With a DP stream per
+// task group two launches overlap (one group's first workgroups fill the
+// other's tail), so the sum of launch durations (kernel_ms) counts the shared
+// time twice; bench.py reports both.
+struct DpBusyClock {
+  hipEvent_t epoch = nullptr;
+  std::map<double, double> iv;  // disjoint merged intervals, start -> end (ms from epoch)
+  void start(hipStream_t s) {
+    SVS_HIP(hipEventCreate(&epoch));
+    SVS_HIP(hipEventRecord(epoch, s));
+  }
+  void add(hipEvent_t k0, hipEvent_t k1, svs_poa_stats& st) {
+    if (!epoch) return;
+    float a = 0.f, b = 0.f;
+    SVS_HIP(hipEventElapsedTime(&a, epoch, k0));
+    SVS_HIP(hipEventElapsedTime(&b, epoch, k1));
+    double lo = a, hi = std::max<double>(a, b), gone = 0.0;
+    // fold every interval that touches [lo, hi] into it
+    auto it = iv.upper_bound(lo);
+    if (it != iv.begin() && std::prev(it)->second >= lo) --it;
+    while (it != iv.end() && it->first <= hi) {
+      lo = std::min(lo, it->first);
+      hi = std::max(hi, it->second);
+      gone += it->second - it->first;
+      it = iv.erase(it);
+    }
+    iv.emplace(lo, hi);
+    st.kernel_busy_ms += (hi - lo) - gone;
+  }
+  ~DpBusyClock() {
+    if (epoch) (void)hipEventDestroy(epoch);
+  }
+};
 
 // SVS_POA_STRIP_GLOBAL_POOL=1 keeps the strip kernel's pool in global memory
 // even when it fits LDS (tests the path large graphs take).
@@ -545,7 +582,7 @@ void verify_prep_tables(const Launch& la, std::deque<PoaTask>& tasks) {
 // the launch is still running, `idle` (if given) is called for host work that
 // is off the critical path until it returns false.
 void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_stats& st, double& host_ms,
-            const svs_poa_config& cfg, const std::function<bool()>& idle = nullptr) {
+            const svs_poa_config& cfg, const std::function<bool()>& idle = nullptr, DpBusyClock* busy = nullptr) {
   PoaArena& A = *la.arena;
   const auto tw0 = Clock::now();
   if (idle) {
@@ -566,6 +603,7 @@ void finish(svs_context* ctx, Launch& la, std::deque<PoaTask>& tasks, svs_poa_st
   float ms = 0.f;
   SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
   st.kernel_ms += ms;
+  if (busy) busy->add(A.ev0, A.ev1, st);
   if (la.prep_jobs > 0) {
     float pms = 0.f;
     SVS_HIP(hipEventElapsedTime(&pms, A.evp, A.evp1));
@@ -831,6 +869,7 @@ struct PoaScheduler::Impl {
       ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
     for (int g = 0; g < n_groups; ++g) groups[g].arena = ctx->poa_arenas[g].get();
     split_cus();
+    dp_busy.start(ctx->stream);
     // Each group's DP kernel on a stream of its own (round 5), so that one
     // group's launch starts in the tail of the other's: a launch ends with its
     // longest jobs and leaves CUs idle that the other group's first
@@ -856,6 +895,7 @@ struct PoaScheduler::Impl {
       }
   }
   hipStream_t own_dp[kMaxGroups] = {nullptr, nullptr, nullptr, nullptr};
+  DpBusyClock dp_busy;
 
   // SVS_POA_FOLD_CUS=n (device-resident graphs, shared DP stream): n CUs,
   // spread evenly over the device, run the fold kernels (the groups' copy
@@ -1588,6 +1628,7 @@ struct PoaScheduler::Impl {
       float ms = 0.f;
       SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
       st.kernel_ms += ms;
+      dp_busy.add(A.ev0, A.ev1, st);
     }
     {
       float ms = 0.f, pms = 0.f;
@@ -1915,7 +1956,7 @@ struct PoaScheduler::Impl {
         sub.arena = g.arena;
         sub.gid = gid(g);
         pack_and_launch_strip(ctx, sub, tasks, score, st, host_ms);
-        finish(ctx, sub, tasks, st, host_ms, cfg);
+        finish(ctx, sub, tasks, st, host_ms, cfg, nullptr, &dp_busy);
         first = last;
       }
     }
@@ -1975,7 +2016,7 @@ struct PoaScheduler::Impl {
         Group& g = *gp;
         if (!g.pending) continue;
         if (dev) finish_dev(g);
-        else finish(ctx, g.la, tasks, st, host_ms, cfg, [this] { return reap(); });
+        else finish(ctx, g.la, tasks, st, host_ms, cfg, [this] { return reap(); }, &dp_busy);
         g.pending = false;
         advance(g, done);
         progressed = true;

@@ -208,6 +208,10 @@ def test_pruning_stats_and_exactness(slack, retries):
     assert st["fold_jobs"] > 0, st  # and folded the alignments into its graphs
     # the graph arena's footprint is reported (DevArena accounting)
     assert 0 < st["dgraph_peak_bytes"] <= st["dgraph_reserved_bytes"], st
+    # the DP busy time is the union of the launch intervals: no longer than
+    # their sum, no shorter than the sum spread over the task groups' streams
+    assert 0 < st["kernel_busy_ms"] <= st["kernel_ms"] * (1 + 1e-6), st
+    assert st["kernel_busy_ms"] >= st["kernel_ms"] / 4 - 1e-3, st
 
 
 def test_wide_slot_jobs_share_pruned_launches():
