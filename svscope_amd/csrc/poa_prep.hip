@@ -32,13 +32,15 @@
 #include "poa_graph.hpp"
 #include "svs_device.hpp"
 
-// Issue priority of the device-graph prep kernel: the DP waves' own (the
-// fold waves of poa_fold.hip issue ahead of them).  Its scalar row loops then
-// take issue slots only when the DP waves leave them, and it still ends well
-// inside the other group's DP launch: 240.5 vs 238.2 windows/s, DP launch
-// 26.8 vs 27.3 ms (profiles/r03_em1).
+// Issue priority of the device-graph prep kernel: the fold waves' (3, ahead
+// of the DP waves).  It is the last link of its group's chain DP -> fold ->
+// next DP, and the sooner that chain ends, the sooner the group's next DP
+// launch starts in the other group's tail: 448.7 / 446.9 vs 439.3 / 440.5
+// windows/s at the DP waves' priority 0, prep kernel 4.0 vs 6.4 s per run
+// (profiles/r05_pp1).  (In round 3, when the chain ended well inside the other
+// group's DP launch, 0 was 1 % faster: profiles/r03_em1.)
 #ifndef SVS_PREP_PRIO_LEVEL
-#define SVS_PREP_PRIO_LEVEL 0
+#define SVS_PREP_PRIO_LEVEL 3
 #endif
 
 namespace svs {

@@ -1194,6 +1194,8 @@ struct PoaScheduler::Impl {
           // the first read becomes a chain before this launch's DP kernel; its
           // tables are known in advance (rows in read order, each reading the
           // row above: one pool slot), so the next read aligns in this launch
+          // (deferring it to the next launch, so that the DP kernel need not
+          // wait for the chain folds, measured slower: profiles/r05_dc1)
           chain.push_back(id);
           chain_seq.push_back(static_cast<uint32_t>(t.next));
           const uint32_t len = static_cast<uint32_t>(t.seqs[t.next].size());
@@ -1329,7 +1331,7 @@ struct PoaScheduler::Impl {
     D.wpj = wpj;
     D.prune = any_prune;
     D.wide = wide;
-    st.wide_launches += wide ? 1 : 0;
+    st.wide_launches += (wide && nj) ? 1 : 0;  // DP launches only (a launch of chains alone runs no DP kernel)
     // (hints: the carries are 16 B per 64 traceback codes, the pairs 8 B per
     // row and read base; sized once for the group's budget instead of growing
     // with the graphs)
