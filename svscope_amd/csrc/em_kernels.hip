@@ -529,16 +529,8 @@ __global__ __launch_bounds__(256) void em_x_kernel(const EmWindow* __restrict__ 
   em_build_x(W, X + W.x_off, xt, xt + L.xr_rel);
 }
 
-// SVS_EM_OCC (development builds): waves per SIMD the K-parallel kernel is
-// compiled for, which caps its VGPRs (its workgroups share CUs with the DP
-// kernel's, whose waves hold 72 VGPRs each).
-#ifdef SVS_EM_OCC
-#define SVS_EM_OCC_ATTR __attribute__((amdgpu_waves_per_eu(SVS_EM_OCC)))
-#else
-#define SVS_EM_OCC_ATTR
-#endif
 template <bool MFMA>
-__global__ __launch_bounds__(256) SVS_EM_OCC_ATTR void em_k_kernel(const EmWindow* __restrict__ wins,
+__global__ __launch_bounds__(256) void em_k_kernel(const EmWindow* __restrict__ wins,
                                                    const int32_t* __restrict__ labels,
                                                    const double* __restrict__ rng, uint64_t rng_len, EmConfig cfg,
                                                    double* __restrict__ ws, double* __restrict__ outd) {
