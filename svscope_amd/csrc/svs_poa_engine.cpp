@@ -25,6 +25,7 @@
 
 #include "poa_dgraph.hpp"
 #include "poa_graph.hpp"
+#include "svs_busy.hpp"
 #include "svs_context.hpp"
 #include "svs_devarena.hpp"
 #include "svs_device.hpp"
@@ -133,18 +134,7 @@ struct DpBusyClock {
     float a = 0.f, b = 0.f;
     SVS_HIP(hipEventElapsedTime(&a, epoch, k0));
     SVS_HIP(hipEventElapsedTime(&b, epoch, k1));
-    double lo = a, hi = std::max<double>(a, b), gone = 0.0;
-    // fold every interval that touches [lo, hi] into it
-    auto it = iv.upper_bound(lo);
-    if (it != iv.begin() && std::prev(it)->second >= lo) --it;
-    while (it != iv.end() && it->first <= hi) {
-      lo = std::min(lo, it->first);
-      hi = std::max(hi, it->second);
-      gone += it->second - it->first;
-      it = iv.erase(it);
-    }
-    iv.emplace(lo, hi);
-    st.kernel_busy_ms += (hi - lo) - gone;
+    st.kernel_busy_ms += busy_union_add(iv, a, b);
   }
   ~DpBusyClock() {
     if (epoch) (void)hipEventDestroy(epoch);

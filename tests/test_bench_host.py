@@ -117,3 +117,64 @@ def test_rank_cpu_plan_splits_the_job_share():
     out = subprocess.check_output([sys.executable, "-c", code], env=env, cwd=ROOT, timeout=120).decode().split()
     n_aff = len(os.sched_getaffinity(0))
     assert out[:2] == ["2", "2"] and int(out[2]) == max(1, n_aff // 8)
+
+
+def test_dp_busy_union_matches_brute_force():
+    """kernel_busy_ms (bench.py roofline.dp_busy) is the union of the DP
+    launches' intervals, accumulated as launches complete in any order
+    (svscope_amd/csrc/svs_busy.hpp through tests/cpp/busy_union_emu.cpp),
+    checked against a sort-and-sweep union after every added interval:
+    disjoint, nested, touching, duplicate and empty intervals, two streams'
+    overlapping launches completing out of order."""
+    import ctypes
+    import random
+    src = os.path.join(ROOT, "tests", "cpp", "busy_union_emu.cpp")
+    hdr = os.path.join(ROOT, "svscope_amd", "csrc", "svs_busy.hpp")
+    lib_path = os.path.join(ROOT, "tests", "build", "libbusy_union_emu.so")
+    os.makedirs(os.path.dirname(lib_path), exist_ok=True)
+    if not os.path.exists(lib_path) or os.path.getmtime(lib_path) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", lib_path, src])
+    lib = ctypes.CDLL(lib_path)
+    D = ctypes.POINTER(ctypes.c_double)
+    lib.emu_busy_union.argtypes = [D, D, ctypes.c_int, D]
+
+    def brute(iv):
+        tot, cur = 0.0, None
+        for a, b in sorted(iv):
+            if cur is None or a > cur[1]:
+                if cur:
+                    tot += cur[1] - cur[0]
+                cur = [a, b]
+            else:
+                cur[1] = max(cur[1], b)
+        return tot + (cur[1] - cur[0] if cur else 0.0)
+
+    rng = random.Random(7)
+    cases = [[(0, 1), (2, 3), (1, 2)], [(0, 10), (2, 3), (4, 5)], [(5, 6), (5, 6), (3, 3)], [(3, 4), (0, 1), (1, 3)]]
+    for _ in range(300):
+        n = rng.randint(1, 40)
+        iv = []
+        for _ in range(n):
+            a = rng.choice([rng.uniform(0, 100), float(rng.randint(0, 20))])
+            iv.append((a, a + rng.choice([0.0, rng.uniform(0, 15), float(rng.randint(0, 5))])))
+        cases.append(iv)
+    # two DP streams: each stream's launches back to back, the streams
+    # overlapping, reported in completion order
+    for _ in range(50):
+        iv = []
+        for s in range(2):
+            t = rng.uniform(0, 5)
+            for _ in range(20):
+                d = rng.uniform(1, 4)
+                iv.append((t, t + d))
+                t += d + rng.uniform(0, 3)
+        iv.sort(key=lambda x: x[1])
+        cases.append(iv)
+    for iv in cases:
+        n = len(iv)
+        lo = (ctypes.c_double * n)(*[a for a, _ in iv])
+        hi = (ctypes.c_double * n)(*[b for _, b in iv])
+        out = (ctypes.c_double * n)()
+        lib.emu_busy_union(lo, hi, n, out)
+        for k in range(n):
+            assert abs(out[k] - brute(iv[:k + 1])) < 1e-9, (iv[:k + 1], out[k])
