@@ -157,8 +157,10 @@ def pmc_traffic_per_cell():
 def record_digests(recs, first_id):
     """SHA-256 of each timed record's Raw.bed line (local_graph.record_line,
     SVscope.py:171-180) for the windows the committed CPU-oracle fixture covers
-    (tests/golden/bench_config3_digests.json: window ids 0..255 of rank 0), and
-    whether they all match it.  None when the fixture covers none of them."""
+    (tests/golden/bench_config3_digests.json: window ids 0..255 of rank 0, and
+    every 40th id after them up to 10,239, so that every timed step is
+    checked), and whether they all match it.  None when the fixture covers none
+    of them."""
     import hashlib
     from svscope_amd.local_graph import record_line
     if not os.path.exists(GOLDEN_DIGESTS):
@@ -169,9 +171,18 @@ def record_digests(recs, first_id):
         return None
     got = [hashlib.sha256(record_line(r).encode()).hexdigest() for r in recs[:n]]
     bad = [k for k in range(n) if got[k] != gold["digests"][k]]
-    return {"windows": n, "digest": hashlib.sha256("\n".join(got).encode()).hexdigest(),
-            "oracle_digest": gold["all"] if n == len(gold["digests"]) else None,
-            "match": not bad, "mismatched_windows": bad[:16]}
+    out = {"windows": n, "digest": hashlib.sha256("\n".join(got).encode()).hexdigest(),
+           "oracle_digest": gold["all"] if n == len(gold["digests"]) else None,
+           "match": not bad, "mismatched_windows": bad[:16]}
+    # the sparse ids: window id k is recs[k] (rank 0, ids from 0)
+    sp = [(w, d) for w, d in zip(gold.get("sparse_ids", []), gold.get("sparse_digests", [])) if w < len(recs)]
+    if sp:
+        sbad = [w for w, d in sp if hashlib.sha256(record_line(recs[w]).encode()).hexdigest() != d]
+        out["sparse"] = {"windows": len(sp), "first_id": sp[0][0], "last_id": sp[-1][0], "match": not sbad,
+                         "mismatched_windows": sbad[:16]}
+        out["match"] = out["match"] and not sbad
+        out["windows_checked"] = n + len(sp)
+    return out
 
 
 def _free_port():

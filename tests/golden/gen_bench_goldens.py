@@ -6,6 +6,11 @@ SVscope.py:171-180).  Digests, not lines: the fixture stays small and the
 GPU test and bench.py hash their own lines the same way.
 
     python tests/golden/gen_bench_goldens.py [--procs 8]
+    python tests/golden/gen_bench_goldens.py --sparse-stride 40   # adds ids 256, 296, ... < 10240
+
+The sparse mode keeps the dense 0..255 digests and adds a digest for every
+S-th window id after them, up to the 10,240 windows of the driver's bench
+(20 steps x 512), so that bench.py's oracle_check covers every timed step.
 
 About 25 s of CPU per window (C++ spoa restatement + numpy EM), so ~15 min on
 8 cores.  Run here, in the container; only the JSON is committed.
@@ -44,9 +49,26 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--n", type=int, default=N_WINDOWS)
+    ap.add_argument("--sparse-stride", type=int, default=0)
+    ap.add_argument("--total", type=int, default=10240)
     args = ap.parse_args()
     from oracle import spoa_oracle
     spoa_oracle._load()
+    if args.sparse_stride:
+        with open(OUT) as fh:
+            out = json.load(fh)
+        ids = list(range(out["n"], args.total, args.sparse_stride))
+        t0 = time.time()
+        with mp.get_context("fork").Pool(args.procs, initializer=_init) as pool:
+            res = sorted(pool.map(_one, ids, chunksize=1))
+        out["sparse_ids"] = [w for w, _, _ in res]
+        out["sparse_digests"] = [d for _, d, _ in res]
+        out["sparse_flags"] = [f for _, _, f in res]
+        out["sparse_cpu_s"] = round(time.time() - t0, 1)
+        with open(OUT, "w") as fh:
+            json.dump(out, fh, indent=1)
+        print("wrote", OUT, len(ids), "sparse ids", f"{out['sparse_cpu_s']} s")
+        return
     t0 = time.time()
     with mp.get_context("fork").Pool(args.procs, initializer=_init) as pool:
         res = sorted(pool.map(_one, range(args.n), chunksize=1))
