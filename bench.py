@@ -16,17 +16,28 @@ batching: batch b+1's window MSAs fill the GPU while batch b finishes), the
 way localGraph_npz streams its windows.  Warmup steps run W batches of a
 separate, reused set of B windows through the same session before timing.
 
-For --gpus N > 1 the script re-launches itself under torch.distributed.run
-(one process per GPU, before anything touches a GPU); each rank processes its
-own K*B windows (weak scaling, no data-path collective: windows are
-independent), time = max over ranks, value = all ranks' windows / that time.
+The timed region ends with the sorted Raw.bed lines (local_graph.record_line
+and sort_lines, SVscope.py:171-180, 236).
 
-roofline: the dominant kernel is the POA DP (poa_strip_kernel); achieved =
-algorithmic bytes (20 B per evaluated DP cell: the int32 H,E,F,O,Q planes of
-convex NW) per launch / mean launch time, from HIP events on
-the engine's POA stream.  traffic = measured HBM bytes per evaluated cell from
-the committed rocprofv3 PMC summary (profiles/pmc_poa_traffic.json) x cells
-per launch, else null.
+For --gpus N > 1 the script re-launches itself under torch.distributed.run
+(one process per GPU, before anything touches a GPU).  The N ranks share one
+global set of N*K*B windows, dealt by LPT over their cost N*L^2
+(local_graph.lpt_owner, as localGraph_npz deals its windows; the costs are
+exchanged through the rendezvous store before any GPU call).  Timed on every
+rank: its windows through its own session, then one RCCL gather of every
+rank's record lines to rank 0 (local_graph.gather_lines) and rank 0's sort.
+Time = max over ranks, value = N*K*B / that time (weak scaling: K*B windows
+per GPU on average).
+
+roofline: the dominant kernel is the POA DP (poa_strip_kernel).  achieved /
+frac = algorithmic bytes (20 B per evaluated DP cell: the int32 H,E,F,O,Q
+planes of convex NW) of the timed DP launches over the device
+time during which at least one of them ran (the union of their HIP-event
+intervals on the two task groups' DP streams; tools/rocprof_timed.py restates
+it from a rocprofv3 kernel trace); per_launch divides by the summed launch
+durations instead, and frac_over_wall by the timed region.  traffic = measured
+HBM bytes per evaluated cell from the committed rocprofv3 PMC summary
+(profiles/pmc_poa_traffic.json) x cells per launch, else null.
 
 cpu_baseline: the CPU oracle (C++ spoa restatement standing in for pyspoa, the
 numpy EM restatement of ReadsCluster.py, the literal Decision) on a bounded
@@ -154,30 +165,38 @@ def pmc_traffic_per_cell():
         return None
 
 
-def record_digests(recs, first_id):
+def record_digests(lines):
     """SHA-256 of each timed record's Raw.bed line (local_graph.record_line,
     SVscope.py:171-180) for the windows the committed CPU-oracle fixture covers
-    (tests/golden/bench_config3_digests.json: window ids 0..255 of rank 0, and
-    every 40th id after them up to 10,239, so that every timed step is
-    checked), and whether they all match it.  None when the fixture covers none
-    of them."""
+    (tests/golden/bench_config3_digests.json: window ids 0..255, and every 40th
+    id after them up to 10,239, so that every timed step of rank 0's N = 1 run
+    is checked), found among the sorted lines by their window's chrom / start /
+    end (synth.window_key), and whether they all match it.  None when the
+    fixture covers none of them."""
     import hashlib
-    from svscope_amd.local_graph import record_line
+    from svscope_amd import synth
     if not os.path.exists(GOLDEN_DIGESTS):
         return None
     gold = json.load(open(GOLDEN_DIGESTS))
-    n = min(len(recs), len(gold["digests"]) - first_id)
-    if first_id != 0 or n <= 0:
+    by_key = {"\t".join(x.split("\t")[0:3]): x for x in lines}
+
+    def digest(w):
+        line = by_key.get(synth.window_key(w, REF_LEN))
+        return hashlib.sha256(line.encode()).hexdigest() if line is not None else None
+    n = 0
+    while n < len(gold["digests"]) and synth.window_key(n, REF_LEN) in by_key:
+        n += 1
+    if n == 0:
         return None
-    got = [hashlib.sha256(record_line(r).encode()).hexdigest() for r in recs[:n]]
+    got = [digest(k) for k in range(n)]
     bad = [k for k in range(n) if got[k] != gold["digests"][k]]
     out = {"windows": n, "digest": hashlib.sha256("\n".join(got).encode()).hexdigest(),
            "oracle_digest": gold["all"] if n == len(gold["digests"]) else None,
            "match": not bad, "mismatched_windows": bad[:16]}
-    # the sparse ids: window id k is recs[k] (rank 0, ids from 0)
-    sp = [(w, d) for w, d in zip(gold.get("sparse_ids", []), gold.get("sparse_digests", [])) if w < len(recs)]
+    sp = [(w, d) for w, d in zip(gold.get("sparse_ids", []), gold.get("sparse_digests", []))
+          if synth.window_key(w, REF_LEN) in by_key]
     if sp:
-        sbad = [w for w, d in sp if hashlib.sha256(record_line(recs[w]).encode()).hexdigest() != d]
+        sbad = [w for w, d in sp if digest(w) != d]
         out["sparse"] = {"windows": len(sp), "first_id": sp[0][0], "last_id": sp[-1][0], "match": not sbad,
                          "mismatched_windows": sbad[:16]}
         out["match"] = out["match"] and not sbad
@@ -226,6 +245,38 @@ def run_steps(session, batches, depth):
     return out
 
 
+def deal_global(world, rank, K, B, gen_procs, store):
+    """N > 1: one global set of world*K*B window ids dealt to the ranks by
+    local_graph.lpt_owner (LPT over N*L^2, what localGraph_npz does with its
+    windows, local_graph.shard_lpt).  Each rank generates every world-th id,
+    the ranks exchange those windows' costs through the rendezvous store (no
+    GPU is touched yet), every rank computes the same deal, and each rank then
+    generates the owned windows it does not hold.  Returns this rank's owned
+    ids (ascending), their rows, and every rank's window count and cost."""
+    import numpy as np
+    from svscope_amd.local_graph import lpt_owner, window_cost
+    n_all = world * K * B
+    stripe = list(range(rank, n_all, world))
+    rows = generate(stripe, gen_procs)
+    mine = np.array([window_cost(r) for r in rows], dtype=np.float64)
+    store.set(f"cost{rank}", mine.tobytes())
+    costs = np.empty(n_all, dtype=np.float64)
+    for r in range(world):
+        costs[r::world] = np.frombuffer(store.get(f"cost{r}"), dtype=np.float64)
+    owner = lpt_owner(costs.tolist(), world)
+    have = dict(zip(stripe, rows))
+    ids = [w for w in range(n_all) if owner[w] == rank]
+    missing = [w for w in ids if w not in have]
+    extra = dict(zip(missing, generate(missing, gen_procs)))
+    out = [have[w] if w in have else extra[w] for w in ids]
+    per_n = [0] * world
+    per_cost = [0.0] * world
+    for w, r in enumerate(owner):
+        per_n[r] += 1
+        per_cost[r] += float(costs[w])
+    return ids, out, per_n, per_cost
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -264,13 +315,25 @@ def main():
     cores = host_cores()
     gen_procs = args.gen_procs or max(1, cores // max(1, world) if world > 1 else cores)
     t_gen = time.time()
-    timed_ids = list(range(rank * K * B, (rank + 1) * K * B))
-    rows = generate(timed_ids, gen_procs)
+    store = None
+    deal = None
+    if world > 1:
+        # the rendezvous store (torchrun's agent store, or rank 0's): the cost
+        # exchange of the deal, then the process group below
+        import torch.distributed as dist
+        from torch.distributed import PrefixStore
+        store = next(dist.rendezvous("env://", rank, world))[0]
+        timed_ids, rows, per_n, per_cost = deal_global(world, rank, K, B, gen_procs,
+                                                       PrefixStore("svs_bench_deal", store))
+        deal = {"windows": per_n, "lpt_cost": per_cost}
+    else:
+        timed_ids = list(range(K * B))
+        rows = generate(timed_ids, gen_procs)
     warm = generate(list(range(WARMUP_ID_BASE + rank * B, WARMUP_ID_BASE + (rank + 1) * B)), gen_procs) if W else []
     # bundle rows [sequenceList, ReadIDs, flank_5, flank_3, TDRecord] -> the
     # TDscope_npz arguments, as localGraph_npz passes them (SVscope.py:212-217)
     from svscope_amd.local_graph import _window
-    batches = [[_window(r) for r in rows[s * B:(s + 1) * B]] for s in range(K)]
+    batches = [[_window(r) for r in rows[s:s + B]] for s in range(0, len(rows), B)]
     warm = [_window(r) for r in warm]
     gen_s = time.time() - t_gen
 
@@ -279,6 +342,7 @@ def main():
         cpu = cpu_baseline(rows, cores)
 
     dist = None
+    device = None
     if world > 1:
         # this rank's CPU slice and engine pool size (svscope_amd/hostcpu.py),
         # before the library creates its context
@@ -294,12 +358,15 @@ def main():
         torch.cuda.set_device(local)
         os.environ["SVS_DEVICE"] = str(local)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            device = torch.device("cuda", local)
+            dist.init_process_group("nccl", store=store, rank=rank, world_size=world, device_id=device)
         else:
-            dist.init_process_group(backend)
+            device = torch.device("cpu")
+            dist.init_process_group(backend, store=store, rank=rank, world_size=world)
 
     from svscope_amd import _abi
     from svscope_amd.decision_maker import DecisionSession
+    from svscope_amd.local_graph import gather_lines, record_line, sort_lines
     ctx = _abi.default_context(local if world > 1 else None)
     session = DecisionSession(ctx)
 
@@ -309,12 +376,21 @@ def main():
     warm_s = time.time() - t_warm
     st0 = session.stats()
 
+    # Timed: every owned window through the session, the Raw.bed lines, then
+    # (N > 1) rank 0 receives every rank's lines with one RCCL gather
+    # (local_graph.gather_lines, after an 8-B all_gather of the sizes), and
+    # rank 0 sorts them like sort -k1,1 -k2,2n (SVscope.py:158-180, 236).
     if dist is not None:
         import torch
         dist.barrier()
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     recs = run_steps(session, batches, args.depth)
+    lines = [record_line(r) for r in recs]
+    t_own = time.perf_counter() - t0
+    if dist is not None:
+        lines = gather_lines(lines, device)
+    out_lines = sort_lines(lines) if rank == 0 else []
     if dist is not None:
         dist.barrier()
         torch.cuda.synchronize()
@@ -322,27 +398,35 @@ def main():
     st = diff_stats(st0, session.stats())
     session.close()
     n_em = sum(1 for r in recs if str(r[-1]).endswith("|EMOutput"))
-    assert len(recs) == K * B, (len(recs), K * B)
+    assert len(recs) == len(timed_ids), (len(recs), len(timed_ids))
+    if rank == 0:
+        assert len(out_lines) == K * B * world, (len(out_lines), K * B * world)
     ranks = None
     if dist is not None:
-        # every rank's own elapsed time and windows (SCALE shows LPT / box
-        # imbalance), then time = the max over ranks
-        gdev = f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu"
-        mine = torch.tensor([elapsed, float(len(recs))], dtype=torch.float64, device=gdev)
+        # every rank's own figures (SCALE shows LPT / box imbalance), then
+        # time = the max over ranks
+        gdev = device if dist.get_backend() == "nccl" else "cpu"
+        mine = torch.tensor([elapsed, t_own, float(len(recs))], dtype=torch.float64, device=gdev)
         every = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(every, mine)
         per = [x.tolist() for x in every]
         elapsed = max(p[0] for p in per)
-        mean = sum(p[0] for p in per) / len(per)
-        ranks = {"elapsed_s": [round(p[0], 3) for p in per], "windows": [int(p[1]) for p in per],
-                 "max_over_mean": round(elapsed / mean, 4) if mean > 0 else None}
+        own = [p[1] for p in per]
+        ranks = {"elapsed_s": [round(p[0], 3) for p in per], "own_windows_s": [round(x, 3) for x in own],
+                 "windows": [int(p[2]) for p in per], "lpt_windows": deal["windows"],
+                 "lpt_cost": [round(c / 1e9, 3) for c in deal["lpt_cost"]], "lpt_cost_unit": "G (reads x len^2)",
+                 "own_max_over_mean": round(max(own) / (sum(own) / len(own)), 4),
+                 "gather_and_sort_s": round(elapsed - max(own), 3),
+                 "note": "own_windows_s: a rank's windows through its session to their record lines; "
+                         "elapsed_s adds the RCCL gather of every rank's lines to rank 0 and rank 0's sort"}
 
     poa = st["poa"]
     cells, cells_done = poa["dp_cells"], poa["cells_computed"]
     kms, launches = poa["kernel_ms"], poa["launches"]
-    achieved = cells_done * BYTES_PER_CELL / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    algo_bytes = cells_done * BYTES_PER_CELL
+    per_launch = algo_bytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     busy_ms = poa.get("kernel_busy_ms", 0.0)
-    busy_achieved = cells_done * BYTES_PER_CELL / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
+    busy_achieved = algo_bytes / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
     total_windows = B * K * world
 
     em_flops = st.get("em_flops", 0.0)
@@ -350,7 +434,7 @@ def main():
     em_tflops = em_flops / em_s / 1e12 if em_s > 0 else 0.0
     if rank == 0:
         value = total_windows / elapsed
-        digests = record_digests(recs, timed_ids[0])
+        digests = record_digests(out_lines)
         per_cell = pmc_traffic_per_cell()
         traffic = round(per_cell * cells_done / max(1, launches)) if per_cell is not None else None
         out = {
@@ -367,24 +451,34 @@ def main():
             "dtype": "int32",
             "data": "synthetic (SURVEY.md §8(d) generator: ONT-like 8% error, somatic INS/DEL, seeded)",
             "config": {"workload": f"config3: {K * B} candidate windows per GPU (64 reads x 3 kb), {B} per step, "
-                                   f"localGraph end to end (MSA POA + features + EM K=1..9 + consensus POA)",
+                                   f"localGraph end to end (MSA POA + features + EM K=1..9 + consensus POA) "
+                                   f"to the sorted Raw.bed lines"
+                                   + (f"; {K * B * world} windows dealt to {world} ranks by LPT, records "
+                                      f"gathered to rank 0 over {dist.get_backend()}" if world > 1 else ""),
                        "windows_per_step_per_gpu": B, "windows_per_gpu": K * B, "reads_per_window": N_READS,
                        "ref_len": REF_LEN, "batches_in_flight": args.depth,
                        "parallelism": f"window shards x{world}"},
+            # frac: the DP kernel's algorithmic bytes (20 B per evaluated cell,
+            # SURVEY.md §8(d)) over the device time during which at least one of
+            # the timed DP launches ran (the union of their HIP-event intervals,
+            # kernel_busy_ms; tools/rocprof_timed.py restates it from a
+            # rocprofv3 kernel trace).  The two task groups' launches overlap on
+            # their DP streams, so per-launch durations count the shared time
+            # twice; that figure is per_launch below.
             "roofline": {"bound": "hbm", "kernel": "poa_strip_kernel",
-                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic,
-                         "algorithmic_bytes_per_launch": int(cells_done * BYTES_PER_CELL / max(1, launches)),
-                         "mean_launch_ms": round(kms / max(1, launches), 4),
-                         # the same bytes over the device time during which at least one
-                         # DP launch ran (union of the launches' HIP-event intervals): two
-                         # task groups' launches overlap on their DP streams, and the
-                         # per-launch durations above count the shared time twice
-                         "dp_busy": {"busy_ms": round(busy_ms, 2),
-                                     "launch_ms_over_busy_ms": round(kms / busy_ms, 4) if busy_ms else None,
-                                     "achieved": round(busy_achieved, 2),
-                                     "frac": round(busy_achieved / HBM_PEAK_GBS, 5)},
+                         "achieved": round(busy_achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(busy_achieved / HBM_PEAK_GBS, 5),
+                         "basis": "algorithmic bytes of the timed DP launches / union of their intervals",
+                         "busy_ms": round(busy_ms, 2),
+                         "traffic": traffic, "traffic_basis": "HBM bytes per DP launch (PMC bytes per evaluated "
+                                                              "cell, profiles/pmc_poa_traffic.json, x cells per launch)",
+                         "algorithmic_bytes_per_launch": int(algo_bytes / max(1, launches)),
+                         # the same bytes over the whole timed region (rank 0's GPU)
+                         "frac_over_wall": round(algo_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
+                         "per_launch": {"achieved": round(per_launch, 2),
+                                        "frac": round(per_launch / HBM_PEAK_GBS, 5),
+                                        "mean_launch_ms": round(kms / max(1, launches), 4),
+                                        "launch_ms_over_busy_ms": round(kms / busy_ms, 4) if busy_ms else None},
                          # SURVEY.md §8(d) prices Σcells over every DP cell of spoa's full
                          # matrix (its "50 % needs ~2e11 cells/s, ~100 windows/s");
                          # frac above counts only the cells the pruned kernel evaluates
@@ -408,6 +502,7 @@ def main():
                                              "poa_dgraph_prep_kernel": round(poa["fold_prep_ms"], 1)},
                           "poa_table_exports": poa.get("prep_jobs", 0),
                           "poa_kernel_ms": round(kms, 2), "poa_launches": launches,
+                          "poa_deferred_tasks": poa.get("deferred_tasks", 0),
                           "dgraph_peak_gb": round(poa.get("dgraph_peak_bytes", 0) / 2**30, 2),
                           "dgraph_reserved_gb": round(poa.get("dgraph_reserved_bytes", 0) / 2**30, 2),
                           "gcups": round(cells_done / (kms * 1e-3) / 1e9, 3) if kms else None,

@@ -26,6 +26,10 @@
 extern "C" {
 #endif
 
+/* Bumped whenever a public struct's layout or a signature changes; a
+ * binding checks svs_abi_version() against the value it was written for. */
+#define SVS_ABI_VERSION 6
+
 #define SVS_OK 0
 #define SVS_E_INVALID (-1)     /* bad argument */
 #define SVS_E_NOMEM (-2)       /* host or device allocation failed */
@@ -71,6 +75,10 @@ typedef struct svs_poa_stats {
      poa_fold_update_kernel, poa_fold_sort_kernel, poa_fold_final_kernel,
      poa_dgraph_prep_kernel */
   double fold_update_ms, fold_sort_ms, fold_final_ms, fold_prep_ms;
+  /* tasks whose graph block did not fit the arena while other tasks held it,
+     run in a later launch instead (this slot held dual_launches until round
+     4; it keeps the offsets of the fields below) */
+  uint64_t deferred_tasks;
   /* device-resident POA graphs (the context's graph arena): the most bytes of
      task blocks live at once, and the HBM the arena holds (hipMalloc'ed chunks;
      never returned before svs_release) */
@@ -86,6 +94,7 @@ int svs_init(int device_ordinal, svs_context** out);
 void svs_release(svs_context* ctx);
 const char* svs_last_error(void);
 int svs_device_count(int* out);
+int svs_abi_version(void); /* SVS_ABI_VERSION of the library */
 
 /* Batched POA: job j aligns sequences [job_seq_start[j], job_seq_start[j+1])
  * in order (pyspoa semantics: empty sequences are skipped and produce no MSA

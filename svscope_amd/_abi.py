@@ -45,6 +45,7 @@ class PoaStats(ctypes.Structure):
                 ("fold_ms", ctypes.c_double), ("fold_jobs", ctypes.c_uint64), ("wide_launches", ctypes.c_uint64),
                 ("fold_update_ms", ctypes.c_double), ("fold_sort_ms", ctypes.c_double),
                 ("fold_final_ms", ctypes.c_double), ("fold_prep_ms", ctypes.c_double),
+                ("deferred_tasks", ctypes.c_uint64),
                 ("dgraph_peak_bytes", ctypes.c_uint64), ("dgraph_reserved_bytes", ctypes.c_uint64),
                 ("kernel_busy_ms", ctypes.c_double)]
 
@@ -93,6 +94,9 @@ _lib = None
 _lib_lock = threading.Lock()
 
 
+ABI_VERSION = 6  # SVS_ABI_VERSION of include/svscope.h
+
+
 def load_library():
     """Loads libsvscope_hip.so and declares its prototypes (no device needed)."""
     global _lib
@@ -104,6 +108,12 @@ def load_library():
                            "(the MI355X engine has no CPU fallback)")
         lib = ctypes.CDLL(LIB_PATH)
         P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        # the struct layouts below are those of include/svscope.h at ABI_VERSION
+        lib.svs_abi_version.argtypes = []
+        lib.svs_abi_version.restype = ctypes.c_int
+        if lib.svs_abi_version() != ABI_VERSION:
+            raise SvsError(f"{LIB_PATH} has ABI version {lib.svs_abi_version()}, this binding expects "
+                           f"{ABI_VERSION}: rebuild it with `python -m svscope_amd.build`")
         lib.svs_init.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
         lib.svs_init.restype = ctypes.c_int
         lib.svs_release.argtypes = [P]

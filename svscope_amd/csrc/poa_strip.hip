@@ -193,7 +193,8 @@ __device__ __forceinline__ uint32_t pred_slot_of(const RowIn& d, uint32_t k, con
 // 128-B carry lines (8 rows x 16 B), so a consumer's scalar load never shares
 // a cache line with a carry its producer has not yet stored.  Strip blocks are
 // VP = round_up(V, 8) rows (a multiple of 128 B) and every job's carry region
-// starts 256-B aligned (bnd_off, svs_poa_engine.cpp, checked there).
+// starts 256-B aligned (bnd_off; svs_poa_engine.cpp check_carry_aligned and
+// check_carry_base throw before a launch where it would not).
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "poa_strip.hip is written for gfx950 (the s_waitcnt encoding below is gfx9's)"
 #endif

@@ -65,6 +65,8 @@ extern "C" {
 
 const char* svs_last_error(void) { return g_last_error.c_str(); }
 
+int svs_abi_version(void) { return SVS_ABI_VERSION; }
+
 int svs_device_count(int* out) {
   if (!out) return fail(SVS_E_INVALID, "null out");
   return guarded([&] {
@@ -89,23 +91,6 @@ int svs_init(int device_ordinal, svs_context** out) {
     ctx->device = device_ordinal;
     SVS_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     SVS_HIP(hipStreamCreateWithFlags(&ctx->em_stream, hipStreamNonBlocking));
-    // SVS_EM_CUS=n (measurement): the EM stream confined
-    // to n CUs spread over the device, so that its workgroups never share a
-    // CU with the DP kernel's on the others
-    if (const char* e = std::getenv("SVS_EM_CUS")) {
-      const int want = std::atoi(e);
-      hipDeviceProp_t prop;
-      SVS_HIP(hipGetDeviceProperties(&prop, device_ordinal));
-      const int n_cu = prop.multiProcessorCount;
-      if (want > 0 && want < n_cu) {
-        std::vector<uint32_t> mask((n_cu + 31) / 32, 0);
-        const int step = n_cu / want;
-        for (int i = 0; i < n_cu; ++i)
-          if (i % step == step - 1 && i / step < want) mask[i / 32] |= 1u << (i % 32);
-        SVS_HIP(hipStreamDestroy(ctx->em_stream));
-        SVS_HIP(hipExtStreamCreateWithCUMask(&ctx->em_stream, static_cast<uint32_t>(n_cu), mask.data()));
-      }
-    }
     SVS_HIP(hipEventCreate(&ctx->ev_start));
     SVS_HIP(hipEventCreate(&ctx->ev_stop));
     SVS_HIP(hipEventCreate(&ctx->ev_mid));
@@ -147,10 +132,6 @@ void svs_release(svs_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->em_stream) (void)hipStreamSynchronize(ctx->em_stream);
   ctx->poa_arenas.clear();
-  if (ctx->poa_dp_stream) {
-    (void)hipStreamSynchronize(ctx->poa_dp_stream);
-    (void)hipStreamDestroy(ctx->poa_dp_stream);
-  }
   ctx->dgraph_arena.reset();
   for (svs::DeviceBuf* b : {&ctx->d_em_in, &ctx->d_em_ws, &ctx->d_em_out, &ctx->d_rng, &ctx->d_ms_pairs,
                             &ctx->d_ms_seq, &ctx->d_ms_nib, &ctx->d_ms_carry, &ctx->d_ms_stack, &ctx->d_ms_out})

@@ -146,8 +146,8 @@ struct PoaArena {
   // after the update, sort and final fold kernels: of the folds after the DP
   // kernel (evk) and of the new tasks' chains before it (evpk)
   hipEvent_t evk[3] = {nullptr, nullptr, nullptr}, evpk[3] = {nullptr, nullptr, nullptr};
-  // the final kernel on a stream of its own beside the table completion
-  // (SVS_POA_FINAL_STREAM): forked after the sort, joined before the copies
+  // the final kernel on a stream of its own beside the table completion,
+  // forked after the sort, joined before the copies
   hipStream_t fin_stream = nullptr;
   hipEvent_t ev_sorted = nullptr, ev_fin0 = nullptr, ev_fin1 = nullptr;
   // Staging of the next launch's strip tables in h_in: the fold exports each
@@ -232,10 +232,6 @@ struct svs_context {
   std::vector<std::unique_ptr<svs::PoaArena>> poa_arenas;
   // blocks of the device-resident POA graphs (svs_devarena.hpp)
   std::unique_ptr<svs::DevArena> dgraph_arena;
-  // SVS_POA_FOLD_CUS=n: the POA kernels split the CUs, n for the groups' fold
-  // kernels (their copy streams), the rest for the DP kernel (this stream)
-  int poa_fold_cus = 0;
-  hipStream_t poa_dp_stream = nullptr;
   // EM arenas
   svs::DeviceBuf d_em_in, d_em_ws, d_em_out, d_rng;
   svs::PinnedBuf h_em_in, h_em_out;

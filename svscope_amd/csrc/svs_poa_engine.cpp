@@ -181,6 +181,21 @@ struct PruneEnv {
   }
 };
 
+// The DP kernel's carry handoff publishes whole 128-B carry lines and relies
+// on every job's carry region starting 256-B aligned (poa_strip.hip, before
+// wait_vm_stores): the region offsets are built as multiples of
+// kCarryAlignInts and the buffer base comes from hipMalloc; both are checked
+// here rather than assumed.
+uint64_t check_carry_aligned(uint64_t off_ints) {
+  if (off_ints % kCarryAlignInts)
+    throw SvsError(SVS_E_INTERNAL, "DP carry region at int offset " + std::to_string(off_ints) + " is not 256-B aligned");
+  return off_ints;
+}
+void check_carry_base(const int32_t* p) {
+  if (reinterpret_cast<uintptr_t>(p) % (kCarryAlignInts * sizeof(int32_t)))
+    throw SvsError(SVS_E_INTERNAL, "DP carry buffer base is not 256-B aligned");
+}
+
 int32_t prune_bound(const PoaTask& t, const PoaScore& P, uint32_t n_rows, uint32_t len, const PruneEnv& pv) {
   const bool on = pv.on;
   const int32_t cg = std::max(std::max(P.g, P.e), std::max(P.q, P.c));
@@ -354,7 +369,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
     if (static_cast<uint64_t>(J.n_rows) * J.ls > 0x7FFFFFFFull)  // the strip kernel's 32-bit code offsets
       throw SvsError(SVS_E_UNSUPPORTED, "a job's traceback matrix exceeds 2^31 cells");
     J.tb_off = n_tb;
-    J.bnd_off = n_bnd;
+    J.bnd_off = check_carry_aligned(n_bnd);
     J.pool_off = n_pool;
     J.aln_off = n_aln;
     J.lb = prune_bound(tasks[la.ids[k]], score, J.n_rows, J.len, penv);
@@ -506,6 +521,7 @@ void pack_and_launch_strip(svs_context* ctx, Launch& la, std::deque<PoaTask>& ta
   pl.prune = any_prune;
   pl.wide = la.code_bytes == 4;
   pl.waves_per_job = wpj;
+  check_carry_base(pl.bnd);
   la.wpj = wpj;
   SVS_HIP(hipEventRecord(A.ev0, A.stream));
   SVS_HIP(launch_poa_strip(pl, A.stream));
@@ -761,18 +777,12 @@ bool sync_check() {
   const char* e = std::getenv("SVS_POA_SYNC_CHECK");
   return e && std::string(e) == "1";
 }
-// The final fold kernel on a stream of its own, beside the table completion
-// of the same launch (a finishing task needs no tables, a continuing one no
-// consensus), so the fold chain the group's next DP launch waits for is
-// update, sort, then the longer of the two: 427.3 / 429.9 vs 418.0 / 419.7
-// windows/s same box (profiles/r05_g1).  SVS_POA_FINAL_STREAM=0: in line.
-bool final_stream() {
-  static const bool on = [] {
-    const char* e = std::getenv("SVS_POA_FINAL_STREAM");
-    return !(e && std::string(e) == "0");
-  }();
-  return on;
-}
+// The final fold kernel runs on a stream of its own, beside the table
+// completion of the same launch (a finishing task needs no tables, a
+// continuing one no consensus), so the fold chain the group's next DP launch
+// waits for is update, sort, then the longer of the two: 427.3 / 429.9 vs
+// 418.0 / 419.7 windows/s same box against running it in line
+// (profiles/r05_g1; the in-line switch was removed in round 6).
 
 size_t active_jobs_per_group() {
   if (const char* e = std::getenv("SVS_POA_ACTIVE_JOBS")) {
@@ -795,18 +805,12 @@ size_t active_jobs_per_group() {
   return 2048;
 }
 
-// Task groups (SVS_POA_GROUPS, 2 to 4; default 2): each with its own arena,
-// DP stream and fold chain.  With more groups a DP launch is ready more often
-// while another group folds; the default tasks per group shrink so that the
-// tasks in flight stay at 4096.
-constexpr int kMaxGroups = 4;
-int poa_groups() {
-  if (const char* e = std::getenv("SVS_POA_GROUPS")) {
-    const int v = std::atoi(e);
-    if (v >= 2 && v <= kMaxGroups) return v;
-  }
-  return 2;
-}
+// Two task groups, each with its own arena, DP stream and fold chain: while
+// one group folds, the other's DP launch runs.  Three and four groups (the
+// same 4096 tasks in flight shared out) made smaller launches, each with its
+// own tail: 366.1 / 362.3 and 390.2 vs 447.1 / 440.1 windows/s same box
+// (profiles/r05_gr1; the switch was removed in round 6).
+constexpr int kMaxGroups = 2;
 
 }  // namespace
 
@@ -817,7 +821,7 @@ struct PoaScheduler::Impl {
   svs_poa_stats& st;
   std::deque<PoaTask> tasks;
   std::deque<uint32_t> queue;
-  const int n_groups = poa_groups();
+  static constexpr int n_groups = kMaxGroups;
   Group groups[kMaxGroups];
   size_t cap;
   size_t budget;
@@ -837,7 +841,6 @@ struct PoaScheduler::Impl {
   Impl(svs_context* c, const svs_poa_config& k, svs_poa_stats& s)
       : ctx(c), cfg(k), score{k.m, k.n, k.g, k.e, k.q, k.c}, st(s), cap(active_jobs_per_group()),
         budget(c->device_budget / n_groups), dev(device_graphs(k)), verify(verify_graph()) {
-    if (n_groups != 2 && !std::getenv("SVS_POA_ACTIVE_JOBS")) cap = 2 * cap / n_groups;
     if (const char* e = std::getenv("SVS_POA_SORT_STACK")) {
       const long v = std::atol(e);
       if (v >= 64 && v <= 1024) sort_stack = static_cast<uint32_t>(v) & ~1u;
@@ -858,23 +861,18 @@ struct PoaScheduler::Impl {
     while (ctx->poa_arenas.size() < static_cast<size_t>(n_groups))
       ctx->poa_arenas.emplace_back(new PoaArena(ctx->device, ctx->stream));
     for (int g = 0; g < n_groups; ++g) groups[g].arena = ctx->poa_arenas[g].get();
-    split_cus();
     dp_busy.start(ctx->stream);
     // Each group's DP kernel on a stream of its own (round 5), so that one
     // group's launch starts in the tail of the other's: a launch ends with its
     // longest jobs and leaves CUs idle that the other group's first
     // workgroups now take.  Same-box driver-shape A/B 378.4 / 375.7 vs 362.3 /
-    // 361.7 windows/s (profiles/r05_a6), 382.1 vs 365.7 (r05_a8); the DP
-    // launches' mean event time grows by ~1 % where they overlap.  Round 3
-    // measured no gain (237.4 vs 240.2, r03_s3c) when the host fold still paced
-    // the launches.  SVS_POA_DP_STREAMS=1 alternates both groups on the
-    // context's stream.
-    const char* dse = std::getenv("SVS_POA_DP_STREAMS");
-    if (!(dse && std::atoi(dse) == 1) && !ctx->poa_fold_cus)
-      for (int g = 0; g < n_groups; ++g) {
-        SVS_HIP(hipStreamCreateWithFlags(&own_dp[g], hipStreamNonBlocking));
-        groups[g].arena->stream = own_dp[g];
-      }
+    // 361.7 windows/s against both groups on one stream (profiles/r05_a6),
+    // 382.1 vs 365.7 (r05_a8); the DP launches' mean event time grows by ~1 %
+    // where they overlap.
+    for (int g = 0; g < n_groups; ++g) {
+      SVS_HIP(hipStreamCreateWithFlags(&own_dp[g], hipStreamNonBlocking));
+      groups[g].arena->stream = own_dp[g];
+    }
   }
   ~Impl() {
     for (int g = 0; g < n_groups; ++g)
@@ -884,41 +882,8 @@ struct PoaScheduler::Impl {
         (void)hipStreamDestroy(own_dp[g]);
       }
   }
-  hipStream_t own_dp[kMaxGroups] = {nullptr, nullptr, nullptr, nullptr};
+  hipStream_t own_dp[kMaxGroups] = {nullptr, nullptr};
   DpBusyClock dp_busy;
-
-  // SVS_POA_FOLD_CUS=n (device-resident graphs, shared DP stream): n CUs,
-  // spread evenly over the device, run the fold kernels (the groups' copy
-  // streams) and the DP kernel gets the others, so that fold waves never take
-  // the register file or LDS a DP workgroup needs on its CU.
-  void split_cus() {
-    const char* e = std::getenv("SVS_POA_FOLD_CUS");
-    const int want = e ? std::atoi(e) : 0;
-    if (!dev || want <= 0 || want == ctx->poa_fold_cus) return;
-    hipDeviceProp_t prop;
-    SVS_HIP(hipGetDeviceProperties(&prop, ctx->device));
-    const int n_cu = prop.multiProcessorCount;
-    if (want >= n_cu) return;
-    const int words = (n_cu + 31) / 32, step = n_cu / want;
-    std::vector<uint32_t> fold(words, 0), dp(words, 0);
-    for (int i = 0; i < n_cu; ++i) {
-      const bool f = (i % step) == step - 1 && i / step < want;
-      (f ? fold : dp)[i / 32] |= 1u << (i % 32);
-    }
-    for (auto& a : ctx->poa_arenas) SVS_HIP(hipStreamSynchronize(a->copy_stream));
-    if (ctx->poa_dp_stream) {
-      SVS_HIP(hipStreamSynchronize(ctx->poa_dp_stream));
-      SVS_HIP(hipStreamDestroy(ctx->poa_dp_stream));
-    }
-    SVS_HIP(hipExtStreamCreateWithCUMask(&ctx->poa_dp_stream, static_cast<uint32_t>(n_cu), dp.data()));
-    for (auto& a : ctx->poa_arenas) {
-      SVS_HIP(hipStreamSynchronize(a->stream));
-      SVS_HIP(hipStreamDestroy(a->copy_stream));
-      SVS_HIP(hipExtStreamCreateWithCUMask(&a->copy_stream, static_cast<uint32_t>(n_cu), fold.data()));
-      a->stream = ctx->poa_dp_stream;
-    }
-    ctx->poa_fold_cus = want;
-  }
 
   // Moves queued tasks into the group, up to `cap` active tasks; when the
   // other group also has room, at most half of the queue, so that both groups
@@ -1038,14 +1003,33 @@ struct PoaScheduler::Impl {
   // block of each task that starts, the graph block of each first-read chain
   // (sized for the chain and its next read's fold in the same launch), and a
   // larger graph block wherever this launch's fold could overflow the current
-  // one.  A task whose block would take the graph arena past its limit fails
-  // alone (fail_task), and the launch goes on without it.
+  // one.  A task whose block can never fit (larger than the arena's limit, or
+  // the test cap) fails alone (fail_task).  A task whose block
+  // does not fit only because other tasks hold the arena right now waits for
+  // a later launch (whether a window fails must not depend on
+  // timing): its chain state is undone (`undo`, saved by advance_dev before it
+  // was changed) and it stays active.  It fails only when nothing could free
+  // a block first: no other work in this launch and no launch of the other
+  // group in flight.
+  struct ChainUndo {
+    uint32_t id;
+    DGraphRef dg;
+    size_t next;
+    uint32_t n_paths, n_slots_next, max_preds_next;
+    bool tables_ok;
+  };
   void reserve_blocks(Group& g, std::vector<uint32_t>& dp, std::vector<uint32_t>& chain,
-                      std::vector<uint32_t>& chain_seq) {
+                      std::vector<uint32_t>& chain_seq, const std::vector<ChainUndo>& undo) {
+    // 1: can never fit, 2: does not fit now
     std::vector<uint8_t> bad(tasks.size(), 0);
     size_t n_bad = 0;
+    uint8_t miss = 0;
     auto reserve = [&](size_t bytes) -> uint8_t* {
-      if (bytes > test_block_cap) return nullptr;
+      if (bytes > test_block_cap || BlockArena::size_class(bytes) > darena->limit()) {
+        miss = 1;
+        return nullptr;
+      }
+      miss = 2;
       return static_cast<uint8_t*>(darena->try_alloc(bytes));
     };
     std::vector<uint8_t> is_chain(tasks.size(), 0);
@@ -1057,7 +1041,7 @@ struct PoaScheduler::Impl {
         const size_t pa = layout_static(t);
         t.d_static = reserve(t.static_bytes);
         if (!t.d_static) {
-          bad[id] = 1;
+          bad[id] = miss;
           ++n_bad;
           continue;
         }
@@ -1074,7 +1058,7 @@ struct PoaScheduler::Impl {
       t.dg.cv = cv1;
       t.dg.ce = ce1;
       if (!t.dg.blk) {
-        bad[id] = 1;
+        bad[id] = miss;
         ++n_bad;
       }
     }
@@ -1090,7 +1074,7 @@ struct PoaScheduler::Impl {
         t.grow_bytes = dgraph_layout(t.grow_cv, t.grow_ce).bytes;
         t.grow_blk = reserve(t.grow_bytes);
         if (!t.grow_blk) {
-          bad[id] = 1;
+          bad[id] = miss;
           ++n_bad;
         }
       }
@@ -1106,13 +1090,41 @@ struct PoaScheduler::Impl {
       v.resize(o);
       if (w) w->resize(o);
     };
-    for (uint32_t id = 0; id < tasks.size(); ++id)
-      if (bad[id])
-        fail_task(g, id, "the device graph arena is full: this task's graph block would pass its limit of " +
-                             std::to_string(darena->limit()) + " bytes (SVS_DEVICE_BUDGET_GB, fewer tasks in flight)");
+    // wait for a later launch where some block can be freed before it
+    size_t n_good = 0;
+    for (uint32_t id : dp) n_good += bad[id] ? 0u : 1u;
+    for (uint32_t id : chain) n_good += bad[id] ? 0u : 1u;
+    bool other_in_flight = false;
+    for (int k = 0; k < n_groups; ++k) other_in_flight = other_in_flight || (k != gid(g) && groups[k].pending);
+    const bool can_wait = n_good > 0 || other_in_flight;
+    std::vector<uint8_t> waits(tasks.size(), 0);
+    for (const ChainUndo& u : undo)
+      if (bad[u.id] == 2 && can_wait) {
+        PoaTask& t = tasks[u.id];
+        t.dg = u.dg;
+        t.next = u.next;
+        t.n_paths = u.n_paths;
+        t.n_slots_next = u.n_slots_next;
+        t.max_preds_next = u.max_preds_next;
+        t.tables_ok = u.tables_ok;
+      }
+    for (uint32_t id = 0; id < tasks.size(); ++id) {
+      if (!bad[id]) continue;
+      if (bad[id] == 2 && can_wait) {
+        waits[id] = 1;
+        ++st.deferred_tasks;
+        continue;
+      }
+      fail_task(g, id, "the device graph arena is full: this task's graph block would pass its limit of " +
+                           std::to_string(darena->limit()) + " bytes (SVS_DEVICE_BUDGET_GB, fewer tasks in flight)");
+    }
     drop(dp, nullptr);
     drop(chain, &chain_seq);
-    drop(g.active, nullptr);
+    // a waiting task stays active (its blocks so far stay reserved)
+    size_t o = 0;
+    for (size_t i = 0; i < g.active.size(); ++i)
+      if (!bad[g.active[i]] || waits[g.active[i]]) g.active[o++] = g.active[i];
+    g.active.resize(o);
   }
 
   // Prepares the group's next device launch, completing the tasks with nothing
@@ -1178,9 +1190,11 @@ struct PoaScheduler::Impl {
         host_ms += ms_since(th0);
         continue;
       }
+      std::vector<ChainUndo> undo;
       for (uint32_t id : g.active) {
         PoaTask& t = tasks[id];
         if (t.dg.V == 0) {
+          undo.push_back(ChainUndo{id, t.dg, t.next, t.n_paths, t.n_slots_next, t.max_preds_next, t.tables_ok});
           // the first read becomes a chain before this launch's DP kernel; its
           // tables are known in advance (rows in read order, each reading the
           // row above: one pool slot), so the next read aligns in this launch
@@ -1219,8 +1233,12 @@ struct PoaScheduler::Impl {
         total += b;
       }
       dp.resize(fit);
-      reserve_blocks(g, dp, chain, chain_seq);
-      if (dp.empty() && chain.empty()) continue;  // every task of the launch failed alone
+      reserve_blocks(g, dp, chain, chain_seq, undo);
+      // every task of the launch failed alone (or waits for the other group)
+      if (dp.empty() && chain.empty()) {
+        if (groups[1 - gid(g)].pending) return;
+        continue;
+      }
       const auto tp0 = Clock::now();
       pack_and_launch_dev(g, dp, chain, chain_seq);
       g_trace.host("pack", gid(g), tp0, dp.size() + chain.size());
@@ -1302,7 +1320,7 @@ struct PoaScheduler::Impl {
       if (static_cast<uint64_t>(J.n_rows) * J.ls > 0x7FFFFFFFull)
         throw SvsError(SVS_E_UNSUPPORTED, "a job's traceback matrix exceeds 2^31 cells");
       J.tb_off = n_tb;
-      J.bnd_off = n_bnd;
+      J.bnd_off = check_carry_aligned(n_bnd);
       J.pool_off = n_pool;
       J.aln_off = n_aln;
       J.lb = prune_bound(t, score, J.n_rows, J.len, penv);
@@ -1541,7 +1559,8 @@ struct PoaScheduler::Impl {
       pl.lds_slots = lds_pool ? max_slots : 0;
       pl.prune = any_prune;
       pl.wide = wide;
-          pl.waves_per_job = wpj;
+      pl.waves_per_job = wpj;
+      check_carry_base(pl.bnd);
       // the pool slots per wave the launch's LDS is sized for (its occupancy)
       g_trace.host("slots", gid(g), Clock::now(), pl.lds_slots);
       SVS_HIP(hipStreamWaitEvent(A.stream, A.h2d, 0));
@@ -1553,7 +1572,7 @@ struct PoaScheduler::Impl {
     // graph update, sort, export and table completion beside the other group's DP
     SVS_HIP(hipEventRecord(A.evf0, side));
     const uint32_t fin_lds = nj ? final_lds(npre, npre + nj) : 0u;
-    D.split_final = fin_lds && final_stream();
+    D.split_final = fin_lds;
     if (nj) {
       SVS_HIP(launch_poa_fold(dfold + npre, static_cast<int>(nj), lds_words, D.split_final ? 0u : fin_lds, side, A.evk));
       if (D.split_final) {
@@ -1956,17 +1975,12 @@ struct PoaScheduler::Impl {
 
   int gid(const Group& g) const { return static_cast<int>(&g - groups); }
 
-  // Longest expected job first (SVS_POA_JOB_ORDER=0: task order).  A launch
-  // holds more waves than the GPU keeps resident, and workgroups start in job
-  // order, so the jobs that start last should be short ones.  Expected cost:
-  // the strip rows the task's previous alignment computed; for a retry or a
-  // task with no history, the unpruned strip rows.
+  // Longest expected job first: a launch holds more waves than the GPU keeps
+  // resident, and workgroups start in job order, so the jobs that start last
+  // should be short ones.  Expected cost: the strip rows the task's previous
+  // alignment computed; for a retry or a task with no history, the unpruned
+  // strip rows.
   void order_by_cost(std::vector<uint32_t>& ids) {
-    static const bool on = [] {
-      const char* e = std::getenv("SVS_POA_JOB_ORDER");
-      return !(e && std::string(e) == "0");
-    }();
-    if (!on) return;
     std::vector<std::pair<uint64_t, uint32_t>> c(ids.size());
     for (size_t i = 0; i < ids.size(); ++i) {
       const PoaTask& t = tasks[ids[i]];

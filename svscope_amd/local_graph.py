@@ -53,13 +53,22 @@ def window_cost(row):
 
 def shard_lpt(rows, world):
     """Longest-processing-time-first assignment of windows to ranks."""
-    order = sorted(range(len(rows)), key=lambda i: -window_cost(rows[i]))
-    load = [0.0] * world
-    owner = [0] * len(rows)
+    return lpt_owner([window_cost(r) for r in rows], world)
+
+
+def lpt_owner(costs, world):
+    """LPT over window costs: the costliest window first, each to the least
+    loaded rank (lowest rank on ties); returns each window's rank.  Every
+    rank computes the same deal from the same costs (bench.py deals its
+    global window set this way from costs exchanged before the GPU starts)."""
+    import heapq
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    heap = [(0.0, k) for k in range(world)]
+    owner = [0] * len(costs)
     for i in order:
-        r = min(range(world), key=lambda k: (load[k], k))
+        load, r = heapq.heappop(heap)
         owner[i] = r
-        load[r] += window_cost(rows[i])
+        heapq.heappush(heap, (load + costs[i], r))
     return owner
 
 

@@ -95,10 +95,15 @@ def make_window(w, n_reads, ref_len, offset=50, chrom="chrS", sample_t="T1", sam
         reads.append(_to_str(_mutate(ref, rrs, **mut)))
         ids.append(f"{sample_n}_normal|w{w}_r{i}")
     ref_s = _to_str(ref)
-    start = 1_000_000 + w * 10_000 + offset
-    end = start + ref_len - 2 * offset
-    record = f"{chrom}\t{start}\t{end}\t{n_tumor}"
+    record = f"{window_key(w, ref_len, offset, chrom)}\t{n_tumor}"
     return [[ref_s] + reads, np.array(ids), ref_s[:offset], ref_s[ref_len - offset:], record]
+
+
+def window_key(w, ref_len, offset=50, chrom="chrS"):
+    """chrom, start, end of window w's TDRecord, tab-separated: the first three
+    fields of its Raw.bed record (what local_graph.window_key reads back)."""
+    start = 1_000_000 + w * 10_000 + offset
+    return f"{chrom}\t{start}\t{start + ref_len - 2 * offset}"
 
 
 def make_windows(config=None, n_windows=None, n_reads=None, ref_len=None, start=0, offset=50):

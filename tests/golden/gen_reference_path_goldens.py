@@ -27,6 +27,10 @@ For the config-3 windows it also runs the reference's
 MSA produces, and writes K, Rclust and BICList (json) and the seqdatamx itself
 (npz): the EM goldens at the headline size (ReadsCluster.py:221-277).
 Only inputs and outputs are written; no reference source travels.
+
+Because the POA here is the repo's own spoa restatement, these goldens pin
+the reference's decision, feature, EM and record code, not POA/consensus
+parity with spoa itself, which stays unpinned (pyspoa is absent).
 """
 import argparse
 import hashlib

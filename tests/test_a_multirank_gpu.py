@@ -50,3 +50,28 @@ def test_local_graph_npz_two_ranks_on_gpu(tmp_path):
     assert all(shards) and sorted(shards[0] + shards[1]) == sorted(local_graph.window_key(r) for r in rows)
     # the per-rank journals are gone once rank 0 has the records
     assert not [x for x in os.listdir(savedir) if ".part" in x]
+
+
+def test_bench_two_ranks_on_gpu_runs_the_multi_gpu_path(tmp_path):
+    """bench.py --gpus 2 rehearsed on the box's one GPU (SVS_DIST_BACKEND=gloo,
+    SVS_DEVICE=0): one global set of 2 x 2 x 8 config-3
+    windows dealt by LPT, each rank's shard through its own session, the
+    record lines gathered to rank 0 and sorted inside the timed region.  The
+    JSON line must report both ranks (windows, LPT cost, elapsed, the gather)
+    and rank 0's gathered records must match the oracle's digests of windows
+    0..31."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(SVS_DEVICE="0", SVS_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--batch", "8",
+           "--warmup", "1", "--depth", "2", "--cpu-sample", "0", "--gen-procs", "4"]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    print(line)
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    r = out["ranks"]
+    assert sum(r["windows"]) == 32 and r["windows"] == r["lpt_windows"] and min(r["windows"]) > 0
+    assert len(r["elapsed_s"]) == 2 and r["gather_and_sort_s"] >= 0 and len(r["lpt_cost"]) == 2
+    assert out["oracle_check"]["match"] and out["oracle_check"]["windows"] == 32
+    assert 0 < out["roofline"]["frac"] < 1

@@ -178,3 +178,96 @@ def test_dp_busy_union_matches_brute_force():
         lib.emu_busy_union(lo, hi, n, out)
         for k in range(n):
             assert abs(out[k] - brute(iv[:k + 1])) < 1e-9, (iv[:k + 1], out[k])
+
+
+def test_block_arena_never_hands_out_overlapping_blocks():
+    """The device graph arena's block logic (svscope_amd/csrc/
+    svs_block_arena.hpp) under a fake chunk allocator, at limits
+    between 1 and 100 GiB, most of them giving a chunk size that the old
+    arena did not round to a power of two: random task-sized allocations and
+    frees run it past its limit, so chunk tails are filed, split_larger
+    halves blocks and try_alloc returns null; no live block may overlap
+    another or leave its chunk (tests/cpp/block_arena_emu.cpp)."""
+    import ctypes
+    src = os.path.join(ROOT, "tests", "cpp", "block_arena_emu.cpp")
+    hdr = os.path.join(ROOT, "svscope_amd", "csrc", "svs_block_arena.hpp")
+    lib_path = os.path.join(ROOT, "tests", "build", "libblock_arena_emu.so")
+    os.makedirs(os.path.dirname(lib_path), exist_ok=True)
+    if not os.path.exists(lib_path) or os.path.getmtime(lib_path) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", lib_path, src])
+    lib = ctypes.CDLL(lib_path)
+    lib.emu_block_arena.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    GiB = 1 << 30
+    total_null = 0
+    for limit in (1 * GiB, int(5.3 * GiB), 6 * GiB, int(20.7 * GiB), 48 * GiB, int(63.9 * GiB), 100 * GiB):
+        for seed in range(3):
+            n_null, n_checked = ctypes.c_int(), ctypes.c_int()
+            bad = lib.emu_block_arena(limit, seed, 20000, ctypes.byref(n_null), ctypes.byref(n_checked))
+            assert bad == 0, (limit, seed, bad)
+            assert n_checked.value > 1000
+            total_null += n_null.value
+    assert total_null > 0  # the limit was reached: split_larger and null returns ran
+
+
+def test_bench_deals_one_global_window_set_by_lpt(monkeypatch):
+    """bench.py --gpus N: the ranks share one global set
+    of N*K*B windows dealt by local_graph.lpt_owner over N*L^2, each rank
+    generating every N-th window, exchanging their costs through the
+    rendezvous store and generating the owned windows it lacks.  Two ranks as
+    threads over one in-process store (small windows): the deal covers every
+    id once, equals shard_lpt over the whole set, and every owned row is that
+    window."""
+    import threading
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setattr(bench, "N_READS", 6)
+    monkeypatch.setattr(bench, "REF_LEN", 160)
+    world, K, B = 2, 3, 5
+    store = dist.HashStore()
+    got = {}
+
+    def run(r):
+        got[r] = bench.deal_global(world, r, K, B, 1, dist.PrefixStore("svs_bench_deal", store))
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert set(got) == {0, 1}
+    allrows = [synth.make_window(w, 6, 160) for w in range(world * K * B)]
+    owner = local_graph.shard_lpt(allrows, world)
+    for r in range(world):
+        ids, rows, per_n, per_cost = got[r]
+        assert ids == [w for w in range(world * K * B) if owner[w] == r]
+        assert [local_graph.window_key(x) for x in rows] == [synth.window_key(w, 160) for w in ids]
+        assert all(list(x[0]) == list(allrows[w][0]) for w, x in zip(ids, rows))
+        assert per_n == [owner.count(k) for k in range(world)]
+    assert sorted(got[0][0] + got[1][0]) == list(range(world * K * B))
+
+
+def test_bench_oracle_check_finds_windows_among_sorted_lines(tmp_path, monkeypatch):
+    """record_digests locates the fixture's windows among rank 0's gathered,
+    sorted lines by chrom / start / end, whatever rank produced them."""
+    import hashlib
+    sys.path.insert(0, ROOT)
+    import bench
+    gold = {"digests": [], "sparse_ids": [7], "sparse_digests": []}
+    lines = []
+    for w in range(10):
+        line = synth.window_key(w, bench.REF_LEN) + "\t3\tX\tY|EMOutput"
+        lines.append(line)
+        if w < 4:
+            gold["digests"].append(hashlib.sha256(line.encode()).hexdigest())
+        if w == 7:
+            gold["sparse_digests"].append(hashlib.sha256(line.encode()).hexdigest())
+    gold["all"] = None
+    path = tmp_path / "g.json"
+    path.write_text(json.dumps(gold))
+    monkeypatch.setattr(bench, "GOLDEN_DIGESTS", str(path))
+    out = bench.record_digests(local_graph.sort_lines(lines[::-1]))
+    assert out["match"] and out["windows"] == 4 and out["windows_checked"] == 5
+    lines[2] = lines[2].replace("X", "Z")
+    out = bench.record_digests(lines)
+    assert not out["match"] and out["mismatched_windows"] == [2]

@@ -297,7 +297,13 @@ def test_session_reproduces_reference_records_at_baseline_sizes():
     gen_reference_path_goldens.py: the reference's code run in the build
     container with the oracle POA standing in for pyspoa) for 16 config-3
     windows (64 reads x 3 kb), 16 config-2 windows (32 x 2 kb) and 4 windows of
-    the harsh pruning profile, all in one streaming session."""
+    the harsh pruning profile, all in one streaming session.
+
+    What this pins and what it does not: the reference's own Decision,
+    MSAFeatureSelection, EMCluster and record code.  The POA inside those
+    records is this repo's spoa restatement (oracle/spoa_oracle.cpp), not
+    pyspoa (absent here), so POA and consensus parity with spoa itself stays
+    unpinned by these goldens."""
     from svscope_amd import synth
     ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_path_goldens.json")))
     rows, want = [], []
