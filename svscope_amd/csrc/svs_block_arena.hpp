@@ -4,7 +4,7 @@
 //
 // Size classes are powers of two, at least 64 KiB, and so is the chunk size
 // (a sixteenth of the limit, 256 MiB .. 4 GiB, rounded down to a power of
-// two).  A chunk is cut front to back in request order.  What keeps live
+// two, and no more than the limit).  A chunk is cut front to back in request order.  What keeps live
 // blocks disjoint is that every free-list key is a power of two and every
 // block filed under key k spans exactly k bytes: a chunk's unused tail is
 // filed as a descending run of powers of two, and split_larger halves a
@@ -33,6 +33,7 @@ class BlockArena {
 
   BlockArena(size_t limit, ChunkAlloc a, ChunkFree f, void* user) : limit_(limit), alloc_(a), free_chunk_(f), user_(user) {
     chunk_ = floor_pow2(std::min<size_t>(size_t(4) << 30, std::max<size_t>(size_t(256) << 20, limit / 16)));
+    chunk_ = std::max(kMinClass, std::min(chunk_, floor_pow2(std::max<size_t>(limit, 1))));  // one chunk fits the limit
   }
   ~BlockArena() {
     for (void* c : chunks_) free_chunk_(c, user_);

@@ -854,7 +854,17 @@ struct PoaScheduler::Impl {
       if (v > 0) test_block_cap = static_cast<size_t>(v);
     }
     if (dev) {
-      if (!ctx->dgraph_arena) ctx->dgraph_arena.reset(new DevArena(ctx->dgraph_budget));
+      if (!ctx->dgraph_arena) {
+        // SVS_POA_TEST_ARENA_BYTES (tests) lowers the limit of a context's
+        // graph arena when its first scheduler creates it, so that tasks must
+        // wait for blocks other tasks hold (reserve_blocks)
+        size_t lim = ctx->dgraph_budget;
+        if (const char* e = std::getenv("SVS_POA_TEST_ARENA_BYTES")) {
+          const long long v = std::atoll(e);
+          if (v > 0) lim = std::min(lim, static_cast<size_t>(v));
+        }
+        ctx->dgraph_arena.reset(new DevArena(lim));
+      }
       darena = ctx->dgraph_arena.get();
     }
     // (both arenas start on the context's stream; the DP streams below)
@@ -1008,9 +1018,10 @@ struct PoaScheduler::Impl {
   // does not fit only because other tasks hold the arena right now waits for
   // a later launch (whether a window fails must not depend on
   // timing): its chain state is undone (`undo`, saved by advance_dev before it
-  // was changed) and it stays active.  It fails only when nothing could free
-  // a block first: no other work in this launch and no launch of the other
-  // group in flight.
+  // was changed) and it stays active.  Only when nothing could free a block
+  // first (no other work in this launch, no launch of the other group in
+  // flight) does one task, the one holding the most, give its blocks up and
+  // fail; advance_dev then tries the rest again.
   struct ChainUndo {
     uint32_t id;
     DGraphRef dg;
@@ -1097,9 +1108,28 @@ struct PoaScheduler::Impl {
     bool other_in_flight = false;
     for (int k = 0; k < n_groups; ++k) other_in_flight = other_in_flight || (k != gid(g) && groups[k].pending);
     const bool can_wait = n_good > 0 || other_in_flight;
+    if (debug_launches())
+      std::fprintf(stderr, "[svs] group %d: %zu blocks missing (%zu jobs placed), other group in flight %d, arena %zu of %zu B in use, %zu reserved\n",
+                   gid(g), n_bad, n_good, int(other_in_flight), darena->in_use(), darena->limit(), darena->reserved());
+    // nothing can free a block first (every task of both groups waits for
+    // one): one task gives up its blocks, the one holding the most, and
+    // fails; the caller then tries the others again
+    uint32_t victim = ~0u;
+    if (!can_wait) {
+      size_t most = 0;
+      for (uint32_t id : g.active)
+        if (bad[id] == 2) {
+          const PoaTask& t = tasks[id];
+          const size_t held = (t.dg.blk ? t.dg_bytes : 0) + (t.d_static && !t.static_up ? t.static_bytes : 0);
+          if (victim == ~0u || held > most) {
+            victim = id;
+            most = held;
+          }
+        }
+    }
     std::vector<uint8_t> waits(tasks.size(), 0);
     for (const ChainUndo& u : undo)
-      if (bad[u.id] == 2 && can_wait) {
+      if (bad[u.id] == 2 && u.id != victim) {
         PoaTask& t = tasks[u.id];
         t.dg = u.dg;
         t.next = u.next;
@@ -1107,10 +1137,16 @@ struct PoaScheduler::Impl {
         t.n_slots_next = u.n_slots_next;
         t.max_preds_next = u.max_preds_next;
         t.tables_ok = u.tables_ok;
+        if (t.static_up && t.d_static) {  // reserved by this call, not yet uploaded: give it back
+          darena->free(t.d_static, t.static_bytes);
+          t.d_static = nullptr;
+          t.d_path_off = t.d_paths = nullptr;
+          t.static_up = false;
+        }
       }
     for (uint32_t id = 0; id < tasks.size(); ++id) {
       if (!bad[id]) continue;
-      if (bad[id] == 2 && can_wait) {
+      if (bad[id] == 2 && id != victim) {
         waits[id] = 1;
         ++st.deferred_tasks;
         continue;

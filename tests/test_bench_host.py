@@ -200,7 +200,7 @@ def test_block_arena_never_hands_out_overlapping_blocks():
                                     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
     GiB = 1 << 30
     total_null = 0
-    for limit in (1 * GiB, int(5.3 * GiB), 6 * GiB, int(20.7 * GiB), 48 * GiB, int(63.9 * GiB), 100 * GiB):
+    for limit in (64 << 20, 300 << 20, 1 * GiB, int(5.3 * GiB), 6 * GiB, int(20.7 * GiB), 48 * GiB, int(63.9 * GiB), 100 * GiB):
         for seed in range(3):
             n_null, n_checked = ctypes.c_int(), ctypes.c_int()
             bad = lib.emu_block_arena(limit, seed, 20000, ctypes.byref(n_null), ctypes.byref(n_checked))

@@ -1,5 +1,6 @@
 """GPU parity of the whole per-window path (Decision / TDscope_npz): records
 identical to the reference's own records (goldens) and to the CPU oracle."""
+import hashlib
 import json
 import os
 
@@ -387,3 +388,29 @@ def test_window_past_an_engine_limit_fails_alone(env, why):
     got = [record_line(x) for k, x in enumerate(e.records) if k != 3]
     assert got == exp
     assert [record_line(x) for x in again] == exp
+
+
+def test_tasks_wait_for_a_full_graph_arena():
+    """a task whose graph block does not fit only because other
+    tasks hold the arena right now waits for a later launch instead of
+    failing, so whether a window fails does not depend on timing.  With the
+    context's graph arena held to 8 MiB (SVS_POA_TEST_ARENA_BYTES; one chunk,
+    about three 32-read x 800-bp window tasks), 16 such windows cannot all
+    hold their blocks at once: tasks are deferred (poa deferred_tasks > 0),
+    none fails, and every record is the oracle's."""
+    from svscope_amd import _abi, synth
+    from svscope_amd.decision_maker import DecisionSession
+    from svscope_amd.local_graph import _window, record_line
+    rows = [synth.make_window(w, 32, 800) for w in range(300, 316)]
+    os.environ["SVS_POA_TEST_ARENA_BYTES"] = str(8 << 20)
+    try:
+        ctx = _abi.Context(0)
+        with DecisionSession(ctx) as s:
+            t = s.submit([_window(r) for r in rows])
+            recs = s.wait(t)
+            st = s.stats()
+    finally:
+        os.environ.pop("SVS_POA_TEST_ARENA_BYTES", None)
+    assert st["poa"]["deferred_tasks"] > 0, st["poa"]
+    assert st["poa"]["dgraph_reserved_bytes"] <= 8 << 20
+    assert [record_line(x) for x in recs] == [_oracle_record(r) for r in rows]

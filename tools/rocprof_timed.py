@@ -5,6 +5,7 @@ mean launch duration, and the DP busy time (the union of the timed launches'
     python tools/rocprof_timed.py TRACE_DIR BENCH_LOG > bench_under_rocprof.json
 
 TRACE_DIR holds the `--kernel-trace --stats --output-format csv` output of
+(its kernel_trace.csv may be gzipped, as committed under profiles/)
 `bench.py` run under rocprofv3; BENCH_LOG is that run's stdout (the JSON line).
 bench.py times the DP launches of its timed steps only; those are the last
 `poa_launches` DP dispatches of the trace, so their rocprofv3 mean is the one to
@@ -15,6 +16,7 @@ launches overlap on their DP streams).
 import collections
 import csv
 import glob
+import gzip
 import json
 import os
 import sys
@@ -38,10 +40,12 @@ def main():
     line = [l for l in open(log) if l.startswith("{")][-1]
     b = json.loads(line)
     n_timed = b["breakdown"]["poa_launches"]
-    trace = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True))
+    trace = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True) +
+                   glob.glob(os.path.join(d, "**", "*kernel_trace.csv.gz"), recursive=True))
     rows = []
     for f in trace:
-        for r in csv.DictReader(open(f)):
+        fh = gzip.open(f, "rt") if f.endswith(".gz") else open(f)
+        for r in csv.DictReader(fh):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     per = collections.defaultdict(list)
