@@ -500,6 +500,8 @@ def main():
                                              "poa_fold_sort_kernel": round(poa["fold_sort_ms"], 1),
                                              "poa_fold_final_kernel": round(poa["fold_final_ms"], 1),
                                              "poa_dgraph_prep_kernel": round(poa["fold_prep_ms"], 1)},
+                          # the group's next launch waits for this after each DP launch
+                          "dp_end_to_launch_done_ms": round(poa.get("dp_to_done_ms", 0.0), 1),
                           "poa_table_exports": poa.get("prep_jobs", 0),
                           "poa_kernel_ms": round(kms, 2), "poa_launches": launches,
                           "poa_deferred_tasks": poa.get("deferred_tasks", 0),

@@ -87,6 +87,9 @@ typedef struct svs_poa_stats {
      launches' HIP-event intervals (kernel_ms sums them, so it counts twice the
      time two task groups' launches overlap on their DP streams) */
   double kernel_busy_ms;
+  /* device time from the end of each DP launch to the end of its launch's
+     fold chain and copies (what the group's next launch waits for) */
+  double dp_to_done_ms;
 } svs_poa_stats;
 
 /* One context per host thread; owns a HIP stream and device arenas. */

@@ -47,7 +47,7 @@ class PoaStats(ctypes.Structure):
                 ("fold_final_ms", ctypes.c_double), ("fold_prep_ms", ctypes.c_double),
                 ("deferred_tasks", ctypes.c_uint64),
                 ("dgraph_peak_bytes", ctypes.c_uint64), ("dgraph_reserved_bytes", ctypes.c_uint64),
-                ("kernel_busy_ms", ctypes.c_double)]
+                ("kernel_busy_ms", ctypes.c_double), ("dp_to_done_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -141,6 +141,7 @@ struct PoaArena {
   hipStream_t stream = nullptr;       // kernel stream (shared by both groups)
   hipStream_t copy_stream = nullptr;  // this group's copies
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr, h2d = nullptr;
+  hipEvent_t ev_end = nullptr;  // timed twin of done (device-resident graphs)
   hipEvent_t evp = nullptr, evp1 = nullptr;  // around the launch's poa_strip_prep_kernel
   hipEvent_t evf0 = nullptr, evf1 = nullptr;  // around the launch's fold kernels (device-resident graphs)
   // after the update, sort and final fold kernels: of the folds after the DP
@@ -183,6 +184,7 @@ struct PoaArena {
       SVS_HIP(hipEventCreate(&evpk[k]));
     }
     SVS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    SVS_HIP(hipEventCreate(&ev_end));
     SVS_HIP(hipEventCreateWithFlags(&h2d, hipEventDisableTiming));
   }
   ~PoaArena() {
@@ -202,6 +204,7 @@ struct PoaArena {
       if (evpk[k]) (void)hipEventDestroy(evpk[k]);
     }
     if (done) (void)hipEventDestroy(done);
+    if (ev_end) (void)hipEventDestroy(ev_end);
     if (h2d) (void)hipEventDestroy(h2d);
     if (ev_sorted) (void)hipEventDestroy(ev_sorted);
     if (ev_fin0) (void)hipEventDestroy(ev_fin0);

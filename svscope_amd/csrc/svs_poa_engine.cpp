@@ -1633,6 +1633,7 @@ struct PoaScheduler::Impl {
       A.h_aln.ensure(n_aln * 8 + 64);
       if (nj) SVS_HIP(hipMemcpyAsync(A.h_aln.ptr, A.d_aln.ptr, n_aln * 8, hipMemcpyDeviceToHost, side));
     }
+    SVS_HIP(hipEventRecord(A.ev_end, side));
     SVS_HIP(hipEventRecord(A.done, side));
     if (debug_launches()) {
       uint32_t vmax = 0;
@@ -1676,6 +1677,9 @@ struct PoaScheduler::Impl {
       SVS_HIP(hipEventElapsedTime(&ms, A.ev0, A.ev1));
       st.kernel_ms += ms;
       dp_busy.add(A.ev0, A.ev1, st);
+      float tail = 0.f;
+      SVS_HIP(hipEventElapsedTime(&tail, A.ev1, A.ev_end));
+      st.dp_to_done_ms += tail;
     }
     {
       float ms = 0.f, pms = 0.f;
