@@ -295,7 +295,7 @@ __device__ void e_accumulate_mfma(const EmWindow& W, int K, const uint8_t* __res
 // A[i,k] = sum_f log theta'[k,f,x_if].  Lane = read, each of the 4 waves sums
 // a quarter of the features (gathers LT rows (f, x_if) of K contiguous
 // doubles), then the quarters are added in wave order.
-template <bool MFMA>
+template <bool MFMA, int KC>
 __device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xr, const double* __restrict__ pi,
                        const double* __restrict__ lt, double* __restrict__ A, double* __restrict__ M,
                        double* __restrict__ g, EmLds* L) {
@@ -332,8 +332,10 @@ __device__ void e_step(const EmWindow& W, int K, const uint8_t* __restrict__ xr,
       const int f0 = slice * fs, f1 = min(nf, f0 + fs);
       const uint8_t* xi = xr + static_cast<int64_t>(i) * nfp;
       double* out = L->part + (slice * N + i) * K;
+      // (cases up to KC only: the launch's largest K; the register count of
+      // the kernel is that of its largest case)
       switch (K) {
-#define SVS_EK(KK) case KK: e_accumulate<KK>(xi, lt, f0, f1, out); break;
+#define SVS_EK(KK) case KK: if constexpr (KK <= KC) e_accumulate<KK>(xi, lt, f0, f1, out); break;
         SVS_EK(1) SVS_EK(2) SVS_EK(3) SVS_EK(4) SVS_EK(5) SVS_EK(6) SVS_EK(7) SVS_EK(8)
         SVS_EK(9) SVS_EK(10) SVS_EK(11) SVS_EK(12) SVS_EK(13) SVS_EK(14) SVS_EK(15)
 #undef SVS_EK
@@ -401,7 +403,7 @@ __device__ void em_build_x(const EmWindow& W, const uint8_t* __restrict__ x, uin
 
 // EM for one K (EMCluster's loop body :245-256, EM :190-209), NaN retries
 // included; the workgroup's RNG position is sh->rng_off.  bic[K-1] is written.
-template <bool MFMA>
+template <bool MFMA, int KC>
 __device__ void em_run_k(const EmWindow& W, int K, const EmK& P, const uint8_t* __restrict__ xt,
                          const uint8_t* __restrict__ xr, const int32_t* __restrict__ lab,
                          const double* __restrict__ rng, uint64_t rng_len, const EmConfig& cfg, EmShared* sh,
@@ -414,10 +416,10 @@ __device__ void em_run_k(const EmWindow& W, int K, const EmK& P, const uint8_t* 
     for (int r = tid; r < N * K; r += blockDim.x) P.g[r] = (lk[r / K] - 1 == r % K) ? 1.0 : 0.0;
     __syncthreads();
     m_step(W, K, xt, P.g, P.pi, P.gsum, P.th, P.lt, rng, rng_len, cfg.eps, sh, lds);
-    e_step<MFMA>(W, K, xr, P.pi, P.lt, P.A, P.M, P.g, lds);
+    e_step<MFMA, KC>(W, K, xr, P.pi, P.lt, P.A, P.M, P.g, lds);
     for (int it = 0; it < cfg.n_step; ++it) {
       m_step(W, K, xt, P.g, P.pi, P.gsum, P.th, P.lt, rng, rng_len, cfg.eps, sh, lds);
-      e_step<MFMA>(W, K, xr, P.pi, P.lt, P.A, P.M, P.g, lds);
+      e_step<MFMA, KC>(W, K, xr, P.pi, P.lt, P.A, P.M, P.g, lds);
       for (int i = tid; i < N; i += blockDim.x) {
         double s = 0.0;
         for (int k = 0; k < K; ++k) s += (P.A[i * K + k] + log(clip_eps(P.pi[k], cfg.eps))) * P.g[i * K + k];
@@ -508,7 +510,7 @@ __global__ __launch_bounds__(256) void em_cluster_kernel(const EmWindow* __restr
   for (int K = 1; K <= nk; ++K) {
     const EmK P = em_k_ptrs(W, ws, K);
     EmLds lds = em_lds(W, P, lds_dyn);
-    em_run_k<MFMA>(W, K, P, xt, xr, labels + W.lab_off, rng, rng_len, cfg, &sh, &lds, outd + W.outd_off);
+    em_run_k<MFMA, 15>(W, K, P, xt, xr, labels + W.lab_off, rng, rng_len, cfg, &sh, &lds, outd + W.outd_off);
   }
   if (threadIdx.x == 0) em_select(W, ws, outd, outi, sh.rng_off, sh.error != 0);
 }
@@ -529,7 +531,7 @@ __global__ __launch_bounds__(256) void em_x_kernel(const EmWindow* __restrict__ 
   em_build_x(W, X + W.x_off, xt, xt + L.xr_rel);
 }
 
-template <bool MFMA>
+template <bool MFMA, int KC>
 __global__ __launch_bounds__(256) void em_k_kernel(const EmWindow* __restrict__ wins,
                                                    const int32_t* __restrict__ labels,
                                                    const double* __restrict__ rng, uint64_t rng_len, EmConfig cfg,
@@ -546,7 +548,7 @@ __global__ __launch_bounds__(256) void em_k_kernel(const EmWindow* __restrict__ 
   if (threadIdx.x == 0) { sh.rng_off = 0; sh.error = 0; sh.reinit = 0; }
   __threadfence_block();
   __syncthreads();
-  em_run_k<MFMA>(W, K, P, xt, xt + L.xr_rel, labels + W.lab_off, rng, rng_len, cfg, &sh, &lds, outd + W.outd_off);
+  em_run_k<MFMA, KC>(W, K, P, xt, xt + L.xr_rel, labels + W.lab_off, rng, rng_len, cfg, &sh, &lds, outd + W.outd_off);
   if (threadIdx.x == 0) {
     uint64_t* spec = reinterpret_cast<uint64_t*>(ws + W.ws_off + L.spec) + 2 * (K - 1);
     spec[0] = sh.rng_off;
@@ -610,12 +612,20 @@ hipError_t launch_em_parallel(const EmWindow* wins, int n, int max_nk, const uin
   const char* me = std::getenv("SVS_EM_MFMA");
   const bool mfma = me && me[0] == '1';
   hipLaunchKernelGGL(em_x_kernel, dim3(n), dim3(256), 0, stream, wins, X, ws);
+  // the kernel instance whose largest E-step case is the launch's largest K:
+  // K <= 9 (the reference's max_C 10) holds 125 VGPRs instead of 154, so an
+  // EM wave displaces two DP waves (72 VGPRs) on its SIMD instead of three:
+  // EM kernel 5.1 / 5.3 vs 6.0 / 6.6 s per driver run, windows/s within the
+  // spread (profiles/r06_c1)
   if (mfma)
-    hipLaunchKernelGGL(em_k_kernel<true>, dim3(n, max_nk), dim3(256), lds, stream, wins, labels, rng, rng_len, cfg,
-                       ws, outd);
+    hipLaunchKernelGGL((em_k_kernel<true, 15>), dim3(n, max_nk), dim3(256), lds, stream, wins, labels, rng, rng_len,
+                       cfg, ws, outd);
+  else if (max_nk <= 9)
+    hipLaunchKernelGGL((em_k_kernel<false, 9>), dim3(n, max_nk), dim3(256), lds, stream, wins, labels, rng, rng_len,
+                       cfg, ws, outd);
   else
-    hipLaunchKernelGGL(em_k_kernel<false>, dim3(n, max_nk), dim3(256), lds, stream, wins, labels, rng, rng_len, cfg,
-                       ws, outd);
+    hipLaunchKernelGGL((em_k_kernel<false, 15>), dim3(n, max_nk), dim3(256), lds, stream, wins, labels, rng, rng_len,
+                       cfg, ws, outd);
   hipLaunchKernelGGL(em_select_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, wins, n, ws, outd, outi);
   return hipGetLastError();
 }
