@@ -25,7 +25,8 @@ global set of N*K*B windows, dealt by LPT over their cost N*L^2
 (local_graph.lpt_owner, as localGraph_npz deals its windows; the costs are
 exchanged through the rendezvous store before any GPU call).  Timed on every
 rank: its windows through its own session, then one RCCL gather of every
-rank's record lines to rank 0 (local_graph.gather_lines) and rank 0's sort.
+rank's record lines to rank 0 (local_graph.gather_payloads) and rank 0's sort
+(local_graph.sort_payloads).
 Time = max over ranks, value = N*K*B / that time (weak scaling: K*B windows
 per GPU on average).
 
@@ -366,7 +367,7 @@ def main():
 
     from svscope_amd import _abi
     from svscope_amd.decision_maker import DecisionSession
-    from svscope_amd.local_graph import gather_lines, record_line, sort_lines
+    from svscope_amd.local_graph import gather_payloads, record_line, sort_lines, sort_payloads
     ctx = _abi.default_context(local if world > 1 else None)
     session = DecisionSession(ctx)
 
@@ -378,7 +379,7 @@ def main():
 
     # Timed: every owned window through the session, the Raw.bed lines, then
     # (N > 1) rank 0 receives every rank's lines with one RCCL gather
-    # (local_graph.gather_lines, after an 8-B all_gather of the sizes), and
+    # (local_graph.gather_payloads, after an 8-B all_gather of the sizes), and
     # rank 0 sorts them like sort -k1,1 -k2,2n (SVscope.py:158-180, 236).
     if dist is not None:
         import torch
@@ -389,8 +390,12 @@ def main():
     lines = [record_line(r) for r in recs]
     t_own = time.perf_counter() - t0
     if dist is not None:
-        lines = gather_lines(lines, device)
-    out_lines = sort_lines(lines) if rank == 0 else []
+        # every rank's record bytes to rank 0, which sorts them without a
+        # Python string per record (local_graph.sort_payloads)
+        payloads = gather_payloads("\n".join(lines).encode(), device)
+        out = sort_payloads(payloads) if rank == 0 else b""
+    else:
+        out = sort_lines(lines)
     if dist is not None:
         dist.barrier()
         torch.cuda.synchronize()
@@ -400,6 +405,7 @@ def main():
     n_em = sum(1 for r in recs if str(r[-1]).endswith("|EMOutput"))
     assert len(recs) == len(timed_ids), (len(recs), len(timed_ids))
     if rank == 0:
+        out_lines = out if dist is None else out.decode().split("\n")
         assert len(out_lines) == K * B * world, (len(out_lines), K * B * world)
     ranks = None
     if dist is not None:

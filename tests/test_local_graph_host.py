@@ -186,3 +186,24 @@ def test_rank_device_ignores_stale_svs_device_under_nccl():
     assert local_graph.rank_device("nccl", 2, {}) == 2
     assert local_graph.rank_device("gloo", 1, {"SVS_DEVICE": "0"}) == 0
     assert local_graph.rank_device("gloo", 1, {}) == 1
+
+
+def test_sort_payloads_matches_sort_lines():
+    """local_graph.sort_payloads (rank 0 of bench.py --gpus N sorts the gathered
+    record bytes without a Python string per record) gives sort_lines' order
+    (sort -k1,1 -k2,2n, C locale, whole-line last resort) on random ASCII
+    lines split over 1-4 payloads: ties, missing second fields, signs, leading
+    blanks, non-numeric keys, empty payloads."""
+    import random
+    rng = random.Random(5)
+    for _ in range(2000):
+        lines = []
+        for _ in range(rng.randint(0, 25)):
+            c = rng.choice(["chr1", "chr10", "chr2", "chrX", "chr1_alt", "a", "Z", ""])
+            st = rng.choice([str(rng.randint(0, 50)), " 7", "-3", "+4", "x", "", "007", "12a"])
+            rest = "".join(rng.choice("AC\tG;,") for _ in range(rng.randint(0, 6)))
+            lines.append(c + ("\t" + st if rng.random() < 0.95 else "") + ("\t" + rest if rest else ""))
+        parts = rng.randint(1, 4)
+        pay = ["\n".join(lines[i::parts]).encode() for i in range(parts)]
+        want = local_graph.sort_lines([x for p in pay if p for x in p.decode().split("\n")])
+        assert local_graph.sort_payloads(pay) == "\n".join(want).encode()
