@@ -72,6 +72,30 @@ def _gen(ws):
     return [synth.make_window(w, N_READS, REF_LEN) for w in ws]
 
 
+def _costs(ws):
+    from svscope_amd import synth
+    from svscope_amd.local_graph import cost_of_lengths
+    return [cost_of_lengths(synth.window_lengths(w, N_READS, REF_LEN)) for w in ws]
+
+
+def window_costs(ids, procs):
+    """LPT costs of windows ids (local_graph.window_cost of each row) from
+    their lengths alone (synth.window_lengths), in `procs` processes."""
+    if procs <= 1 or len(ids) < 2:
+        return _costs(ids)
+    chunks = [ids[i::procs] for i in range(procs)]
+    pool = mp.get_context("fork").Pool(procs)
+    try:
+        parts = pool.map(_costs, chunks)
+    finally:
+        pool.close()
+        pool.join()
+    out = [0.0] * len(ids)
+    for i, part in enumerate(parts):
+        out[i::procs] = part
+    return out
+
+
 def generate(ids, procs):
     if procs <= 1 or len(ids) < 2:
         return _gen(ids)
@@ -249,27 +273,24 @@ def run_steps(session, batches, depth):
 def deal_global(world, rank, K, B, gen_procs, store):
     """N > 1: one global set of world*K*B window ids dealt to the ranks by
     local_graph.lpt_owner (LPT over N*L^2, what localGraph_npz does with its
-    windows, local_graph.shard_lpt).  Each rank generates every world-th id,
-    the ranks exchange those windows' costs through the rendezvous store (no
-    GPU is touched yet), every rank computes the same deal, and each rank then
-    generates the owned windows it does not hold.  Returns this rank's owned
-    ids (ascending), their rows, and every rank's window count and cost."""
+    windows, local_graph.shard_lpt).  Each rank computes the costs of every
+    world-th id (from the windows' lengths alone, synth.window_lengths), the
+    ranks exchange them through the rendezvous store (no GPU is touched yet),
+    every rank computes the same deal, and each rank then generates the
+    windows it owns.  Returns this rank's owned ids (ascending), their rows,
+    and every rank's window count and cost."""
     import numpy as np
-    from svscope_amd.local_graph import lpt_owner, window_cost
+    from svscope_amd.local_graph import lpt_owner
     n_all = world * K * B
     stripe = list(range(rank, n_all, world))
-    rows = generate(stripe, gen_procs)
-    mine = np.array([window_cost(r) for r in rows], dtype=np.float64)
+    mine = np.array(window_costs(stripe, gen_procs), dtype=np.float64)
     store.set(f"cost{rank}", mine.tobytes())
     costs = np.empty(n_all, dtype=np.float64)
     for r in range(world):
         costs[r::world] = np.frombuffer(store.get(f"cost{r}"), dtype=np.float64)
     owner = lpt_owner(costs.tolist(), world)
-    have = dict(zip(stripe, rows))
     ids = [w for w in range(n_all) if owner[w] == rank]
-    missing = [w for w in ids if w not in have]
-    extra = dict(zip(missing, generate(missing, gen_procs)))
-    out = [have[w] if w in have else extra[w] for w in ids]
+    out = generate(ids, gen_procs)
     per_n = [0] * world
     per_cost = [0.0] * world
     for w, r in enumerate(owner):

@@ -45,9 +45,14 @@ def load_bundles(savedir):
 
 
 def window_cost(row):
-    seqs = row[0]
-    n = max(1, len(seqs) - 1)
-    mean_len = (sum(len(s) for s in seqs) / max(1, len(seqs)))
+    return cost_of_lengths([len(s) for s in row[0]])
+
+
+def cost_of_lengths(lens):
+    """A window's LPT cost from its sequence lengths (reference row first):
+    reads x mean length^2."""
+    n = max(1, len(lens) - 1)
+    mean_len = sum(lens) / max(1, len(lens))
     return n * mean_len * mean_len
 
 

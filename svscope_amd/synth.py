@@ -58,6 +58,26 @@ def _mutate(hap, rs, p_sub=0.035, p_del=0.025, p_ins=0.02):
     return out
 
 
+def _mutated_len(hap, rs, p_sub=0.035, p_del=0.025, p_ins=0.02):
+    """len(_mutate(hap, rs, ...)) with the same random draws, without building
+    the read."""
+    n = hap.shape[0]
+    u = rs.random_sample(n)
+    keep = u >= p_del
+    n_sub = int((keep & (u < p_del + p_sub)).sum())
+    if n_sub:
+        rs.randint(1, 4, size=n_sub)
+    homo = np.zeros(n, dtype=bool)
+    if n > 1:
+        eq = hap[1:] == hap[:-1]
+        homo[1:] |= eq
+        homo[:-1] |= eq
+    frac_h = homo.mean() if n else 0.0
+    base_rate = p_ins / (1.0 + frac_h)
+    ins = rs.random_sample(n) < np.where(homo, 2 * base_rate, base_rate)
+    return int(keep.sum()) + int(ins.sum())
+
+
 def _to_str(codes):
     return _ALPHA[codes].tobytes().decode("ascii")
 
@@ -97,6 +117,30 @@ def make_window(w, n_reads, ref_len, offset=50, chrom="chrS", sample_t="T1", sam
     ref_s = _to_str(ref)
     record = f"{window_key(w, ref_len, offset, chrom)}\t{n_tumor}"
     return [[ref_s] + reads, np.array(ids), ref_s[:offset], ref_s[ref_len - offset:], record]
+
+
+def window_lengths(w, n_reads, ref_len, offset=50):
+    """[len(s) for s in make_window(w, n_reads, ref_len)[0]] at the default
+    error profile, from the same random draws but without building the reads
+    (about 2/3 of make_window's time; bench.py deals windows by these)."""
+    seed = (20250509 + w) % (2 ** 32)
+    rs = np.random.RandomState(seed)
+    ref = rs.randint(0, 4, size=ref_len)
+    mid = ref_len // 2
+    if w % 2 == 0:
+        ins_len = int(rs.randint(200, 801))
+        som = np.concatenate([ref[:mid], rs.randint(0, 4, size=ins_len), ref[mid:]])
+    else:
+        del_len = min(int(rs.randint(100, 601)), max(0, ref_len - 2 * offset - 2))
+        a = mid - del_len // 2
+        som = np.concatenate([ref[:a], ref[a + del_len:]])
+    n_tumor = n_reads - n_reads // 2
+    n_som = min(n_tumor, -(-n_reads // 4))
+    lens = [ref_len]
+    for i in range(n_reads):
+        hap = som if i < n_som else ref
+        lens.append(_mutated_len(hap, np.random.RandomState((seed * 1000 + i) % (2 ** 32))))
+    return lens
 
 
 def window_key(w, ref_len, offset=50, chrom="chrS"):
