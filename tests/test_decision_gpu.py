@@ -414,3 +414,23 @@ def test_tasks_wait_for_a_full_graph_arena():
     assert st["poa"]["deferred_tasks"] > 0, st["poa"]
     assert st["poa"]["dgraph_reserved_bytes"] <= 8 << 20
     assert [record_line(x) for x in recs] == [_oracle_record(r) for r in rows]
+
+
+def test_consensus_prior_off_gives_the_same_records():
+    """SVS_POA_CONS_PRIOR < 0 turns off the pruning prior of a window's
+    consensus tasks (their first alignment then runs unpruned): the records
+    of 16 config-3 windows (bench ids 0..15) are still the oracle's
+    (tests/golden/bench_config3_digests.json), since the pruning is exact
+    either way."""
+    from svscope_amd import synth
+    from svscope_amd.decision_maker import DecisionSession
+    from svscope_amd.local_graph import _window, record_line
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_config3_digests.json")))
+    rows = [synth.make_window(w, 64, 3000) for w in range(16)]
+    os.environ["SVS_POA_CONS_PRIOR"] = "-1"
+    try:
+        with DecisionSession() as s:
+            recs = s.wait(s.submit([_window(r) for r in rows]))
+    finally:
+        os.environ.pop("SVS_POA_CONS_PRIOR", None)
+    assert [hashlib.sha256(record_line(x).encode()).hexdigest() for x in recs] == gold["digests"][:16]

@@ -103,6 +103,7 @@ def test_genmsa_false_and_min_coverage():
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "none"},
     {"SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_PRUNE_RETRY_SLACK": "-0.3", "SVS_POA_PRUNE_MAX_RETRIES": "100"},
     {"SVS_POA_VERIFY_GRAPH": "1"},
+    {"SVS_POA_SYNC_CHECK": "1", "SVS_POA_WPJ": "4"},
     {"SVS_POA_VERIFY_GRAPH": "1", "SVS_POA_PRUNE_SLACK": "-0.3", "SVS_POA_WPJ": "2"},
     {"SVS_POA_VERIFY_GRAPH": "1", "SVS_POA_SORT_STACK": "64"},
     {"SVS_POA_HOST_GRAPH": "1"},
