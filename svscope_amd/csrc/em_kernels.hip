@@ -531,8 +531,18 @@ __global__ __launch_bounds__(256) void em_x_kernel(const EmWindow* __restrict__ 
   em_build_x(W, X + W.x_off, xt, xt + L.xr_rel);
 }
 
+// Held to 6 waves per SIMD (80 VGPRs; the gathers' load batches shrink and a
+// few values spill to scratch): an EM wave then takes about one DP wave's
+// registers (72) instead of 125, and the EM kernel time of the driver's run
+// falls from 4.8-5.0 to 3.4-3.5 s with windows/s and the DP busy frac within
+// the spread (446.4 vs 444.9 / 441.9 windows/s, frac 0.460 vs 0.453 / 0.456,
+// profiles/r06_em2; 5 waves, 96 VGPRs: 3.7-3.9 s, r06_em1).  SVS_EM_OCC
+// overrides it in development builds.
+#ifndef SVS_EM_OCC
+#define SVS_EM_OCC 6
+#endif
 template <bool MFMA, int KC>
-__global__ __launch_bounds__(256) void em_k_kernel(const EmWindow* __restrict__ wins,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SVS_EM_OCC))) void em_k_kernel(const EmWindow* __restrict__ wins,
                                                    const int32_t* __restrict__ labels,
                                                    const double* __restrict__ rng, uint64_t rng_len, EmConfig cfg,
                                                    double* __restrict__ ws, double* __restrict__ outd) {

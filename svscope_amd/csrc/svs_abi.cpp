@@ -90,6 +90,9 @@ int svs_init(int device_ordinal, svs_context** out) {
     ctx = new svs_context();
     ctx->device = device_ordinal;
     SVS_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    // (the EM stream at the lowest priority, 1, so that its workgroups only
+    // take slots no DP workgroup waits for: windows/s and the DP busy frac
+    // within the spread, EM kernel 5.4 vs 4.8-4.9 s, profiles/r06_em2; not kept)
     SVS_HIP(hipStreamCreateWithFlags(&ctx->em_stream, hipStreamNonBlocking));
     SVS_HIP(hipEventCreate(&ctx->ev_start));
     SVS_HIP(hipEventCreate(&ctx->ev_stop));

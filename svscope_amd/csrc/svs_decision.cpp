@@ -61,7 +61,52 @@ struct Batch {
   std::vector<int32_t> cons_left;  // consensus tasks still running, per window
   int32_t left = 0;                // windows not yet complete
   Clock::time_point t0;
+  std::vector<PoaTask> built;      // the windows' MSA tasks (prepare_batch), until queued
 };
+
+// Builds a submitted batch's window MSA tasks and per-window state, on the
+// session's builder thread: a batch's reads are ~100 MB of copies and letter
+// checks, 15-60 ms that were spent on the worker thread, which also issues the
+// POA launches, so a group whose fold chain ended meanwhile waited for it.
+void prepare_batch(Batch& b, const svs_decision_config& cfg, bool device_features_on, ThreadPool* pool) {
+  b.t0 = Clock::now();
+  b.res.reset(new svs_decision_result());
+  b.res->w.resize(b.n);
+  b.feats.resize(b.n);
+  b.read_lens.resize(b.n);
+  b.f5.resize(b.n);
+  b.f3.resize(b.n);
+  b.msa_rate.assign(b.n, 0.0);
+  b.msa_has_rate.assign(b.n, 0);
+  b.cons_left.assign(b.n, 0);
+  b.left = b.n;
+  const uint32_t prio = static_cast<uint32_t>(b.ticket);
+  b.built.resize(static_cast<size_t>(b.n));
+  pool->parallel_for(static_cast<size_t>(b.n), [&](size_t wi) {
+    const int32_t w = static_cast<int32_t>(wi);
+    const svs_decision_window& W = b.wins[w];
+    PoaTask& t = b.built[wi];
+    t.genmsa = true;
+    t.prio = prio;
+    for (int32_t k = 0; k < W.n_seqs; ++k) {
+      const int64_t x = b.seq_byte_start[W.seq_start + k], y = b.seq_byte_start[W.seq_start + k + 1];
+      // (ranges checked on submit, check_decision_windows)
+      t.seqs.emplace_back(y > x ? b.seq_bytes + x : "", static_cast<size_t>(y - x));
+      if (k > 0) b.read_lens[w].push_back(static_cast<int32_t>(y - x));
+    }
+    b.f5[w].assign(W.flank5_len ? b.text + W.flank5_off : "", W.flank5_len);
+    b.f3[w].assign(W.flank3_len ? b.text + W.flank3_off : "", W.flank3_len);
+    // the window's feature selection on the device when its graph is there
+    // (else, or for a letter SeqEncoder rejects, the host's from the MSA rows)
+    t.features = device_features_on;
+    try {
+      t.feat_params = device_feature_params(t.seqs, b.f5[w], b.f3[w], b.read_lens[w], W.n_ids, cfg.hcutoff,
+                                            cfg.scutoff);
+    } catch (const SvsError&) {
+      t.feat_params.ok = false;
+    }
+  });
+}
 
 struct WinRef {
   Batch* b;
@@ -92,17 +137,25 @@ struct svs_decision_session {
   std::thread worker;
   std::mutex mu;
   std::condition_variable cv_work, cv_done;
-  std::deque<std::unique_ptr<svs::Batch>> inbox;               // submitted, not yet queued
+  std::deque<std::unique_ptr<svs::Batch>> to_build;            // submitted, tasks not yet built
+  std::deque<std::unique_ptr<svs::Batch>> inbox;               // built, not yet queued
   std::map<int64_t, std::unique_ptr<svs::Batch>> in_flight;    // queued in the scheduler
   std::map<int64_t, std::unique_ptr<svs::Batch>> finished;     // complete, not yet waited for
   std::set<int64_t> waited;                                    // tickets already returned by wait
   int64_t next_ticket = 1;
+  int64_t building = 0;    // batches submitted and not yet in the inbox
   bool closing = false;
   bool em_signal = false;  // the EM worker finished a launch
+  bool device_features_on = true;
   std::exception_ptr error;
   svs_decision_stats published{};  // cumulative statistics, as of the last completed batch
+  std::thread builder;
+  std::condition_variable cv_build;
 
-  void run();  // worker thread body
+  void run();         // worker thread body
+  void build_loop();  // builder thread body (prepare_batch)
+  // (under mu) nothing submitted is still on its way to the worker
+  bool nothing_arriving() const { return inbox.empty() && building == 0; }
 };
 
 namespace svs {
@@ -124,10 +177,6 @@ class Pipeline {
     // unpruned).
     const char* e = std::getenv("SVS_POA_CONS_PRIOR");
     cons_prior = e ? std::atof(e) : 1.5;
-    // SVS_DEVICE_FEATURES=0: the window MSA rows come back and the host
-    // selects the features (the round-3 path)
-    const char* df = std::getenv("SVS_DEVICE_FEATURES");
-    device_features_on = !(df && std::string(df) == "0");
     ecfg = cfg.em;
     ecfg.want_params = 0;
     t_wall = Clock::now();
@@ -161,53 +210,15 @@ class Pipeline {
     return static_cast<uint32_t>(refs.size() - 1);
   }
 
-  // Queues a submitted batch's window MSAs (worker thread).
+  // Queues a built batch's window MSAs in window order (worker thread; the
+  // tasks were built by prepare_batch on the builder thread).
   void ingest(std::unique_ptr<Batch> bp) {
     Batch& b = *bp;
-    b.t0 = Clock::now();
-    b.res.reset(new svs_decision_result());
-    b.res->w.resize(b.n);
-    b.feats.resize(b.n);
-    b.read_lens.resize(b.n);
-    b.f5.resize(b.n);
-    b.f3.resize(b.n);
-    b.msa_rate.assign(b.n, 0.0);
-    b.msa_has_rate.assign(b.n, 0);
-    b.cons_left.assign(b.n, 0);
-    b.left = b.n;
-    const uint32_t prio = static_cast<uint32_t>(b.ticket);
-    // the windows' tasks are built on the pool (a batch's reads are ~100 MB of
-    // copies and letter checks: 30-60 ms on this thread, which also drives the
-    // POA launches, profiles/r04_g8), then queued in window order
-    std::vector<PoaTask> built(static_cast<size_t>(b.n));
-    ctx->pool->parallel_for(static_cast<size_t>(b.n), [&](size_t wi) {
-      const int32_t w = static_cast<int32_t>(wi);
-      const svs_decision_window& W = b.wins[w];
-      PoaTask& t = built[wi];
-      t.genmsa = true;
-      t.prio = prio;
-      for (int32_t k = 0; k < W.n_seqs; ++k) {
-        const int64_t x = b.seq_byte_start[W.seq_start + k], y = b.seq_byte_start[W.seq_start + k + 1];
-        // (ranges checked on submit, check_decision_windows)
-        t.seqs.emplace_back(y > x ? b.seq_bytes + x : "", static_cast<size_t>(y - x));
-        if (k > 0) b.read_lens[w].push_back(static_cast<int32_t>(y - x));
-      }
-      b.f5[w].assign(W.flank5_len ? b.text + W.flank5_off : "", W.flank5_len);
-      b.f3[w].assign(W.flank3_len ? b.text + W.flank3_off : "", W.flank3_len);
-      // the window's feature selection on the device when its graph is there
-      // (else, or for a letter SeqEncoder rejects, the host's from the MSA rows)
-      t.features = device_features_on;
-      try {
-        t.feat_params = device_feature_params(t.seqs, b.f5[w], b.f3[w], b.read_lens[w], W.n_ids, cfg.hcutoff,
-                                              cfg.scutoff);
-      } catch (const SvsError&) {
-        t.feat_params.ok = false;
-      }
-    });
     for (int32_t w = 0; w < b.n; ++w) {
-      built[w].tag = new_ref(TaskRef{&b, w, -1});
-      sched.add(std::move(built[w]));
+      b.built[w].tag = new_ref(TaskRef{&b, w, -1});
+      sched.add(std::move(b.built[w]));
     }
+    std::vector<PoaTask>().swap(b.built);
     st.msa_tasks += b.n;
     msa_outstanding += static_cast<size_t>(b.n);
     Batch* raw = bp.get();
@@ -445,7 +456,7 @@ class Pipeline {
   // with block=true (the scheduler is idle) it waits for such work.
   bool poll(bool block) {
     take_inbox();
-    if (em && (em_ready_now() || (block && msa_outstanding == 0 && !have_inbox()))) {
+    if (em && (em_ready_now() || (block && msa_outstanding == 0 && !batches_arriving()))) {
       // blocking on the EM result is only worth it when nothing else can arrive
       consume_em();
       block = false;  // new consensus tasks can run while the next EM batch does
@@ -453,21 +464,22 @@ class Pipeline {
     if (!em && !em_ready.empty() && (em_ready.size() >= em_batch || msa_outstanding == 0)) start_em();
     if (block) {
       std::unique_lock<std::mutex> lk(S->mu);
-      S->cv_work.wait(lk, [&] { return !S->inbox.empty() || S->closing || S->em_signal; });
-      const bool closing = S->closing && S->inbox.empty();
+      // (a closing session still waits for batches its builder has not handed over)
+      S->cv_work.wait(lk, [&] { return !S->inbox.empty() || (S->closing && S->building == 0) || S->em_signal; });
+      const bool closing = S->closing && S->nothing_arriving();
       lk.unlock();
       take_inbox();
       if (em && (em_ready_now() || closing)) consume_em();
       if (!em && !em_ready.empty() && (em_ready.size() >= em_batch || msa_outstanding == 0)) start_em();
     }
     std::lock_guard<std::mutex> lk(S->mu);
-    const bool open = !S->closing || !S->inbox.empty();
+    const bool open = !S->closing || !S->nothing_arriving();
     return open || em != nullptr || !em_ready.empty();
   }
 
-  bool have_inbox() {
+  bool batches_arriving() {
     std::lock_guard<std::mutex> lk(S->mu);
-    return !S->inbox.empty();
+    return !S->nothing_arriving();
   }
 
   svs_decision_session* S;
@@ -477,7 +489,6 @@ class Pipeline {
   PoaScheduler sched;
   size_t em_batch = 512;
   double cons_prior = 1.5;
-  bool device_features_on = true;
   svs_em_config ecfg{};
   Clock::time_point t_wall;
   size_t msa_outstanding = 0;  // window MSAs queued or running, all batches
@@ -490,6 +501,41 @@ class Pipeline {
 }  // namespace
 
 }  // namespace svs
+
+void svs_decision_session::build_loop() {
+  // the builder's own pool: the context's belongs to the worker thread
+  // (ThreadPool::parallel_for is not reentrant across threads)
+  svs::ThreadPool pool(4);
+  for (;;) {
+    std::unique_ptr<svs::Batch> b;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv_build.wait(lk, [&] { return !to_build.empty() || closing; });
+      if (to_build.empty()) return;  // closing, every batch handed over
+      b = std::move(to_build.front());
+      to_build.pop_front();
+    }
+    try {
+      svs::prepare_batch(*b, cfg, device_features_on, &pool);
+    } catch (...) {
+      // the batch is dropped: its waiters see the error
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!error) error = std::current_exception();
+        --building;
+      }
+      cv_work.notify_all();
+      cv_done.notify_all();
+      continue;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      inbox.push_back(std::move(b));
+      --building;
+    }
+    cv_work.notify_all();
+  }
+}
 
 void svs_decision_session::run() {
   try {
@@ -510,7 +556,12 @@ svs_decision_session* open_decision_session(svs_context* ctx, const svs_decision
   std::unique_ptr<svs_decision_session> s(new svs_decision_session());
   s->ctx = ctx;
   s->cfg = cfg;
+  // SVS_DEVICE_FEATURES=0: the window MSA rows come back and the host
+  // selects the features (the round-3 path)
+  const char* df = std::getenv("SVS_DEVICE_FEATURES");
+  s->device_features_on = !(df && std::string(df) == "0");
   svs_decision_session* raw = s.get();
+  s->builder = std::thread([raw] { raw->build_loop(); });
   s->worker = std::thread([raw] { raw->run(); });
   return s.release();
 }
@@ -532,9 +583,10 @@ int64_t submit_decision_batch(svs_decision_session* s, int32_t n, const svs_deci
     if (s->closing) throw SvsError(SVS_E_INVALID, "decision session is closing");
     ticket = s->next_ticket++;
     b->ticket = ticket;
-    s->inbox.push_back(std::move(b));
+    s->to_build.push_back(std::move(b));
+    ++s->building;
   }
-  s->cv_work.notify_all();
+  s->cv_build.notify_all();
   return ticket;
 }
 
@@ -564,7 +616,9 @@ std::exception_ptr close_decision_session(svs_decision_session* s) {
     std::lock_guard<std::mutex> lk(s->mu);
     s->closing = true;
   }
+  s->cv_build.notify_all();
   s->cv_work.notify_all();
+  if (s->builder.joinable()) s->builder.join();
   if (s->worker.joinable()) s->worker.join();
   std::exception_ptr e = s->error;
   delete s;
