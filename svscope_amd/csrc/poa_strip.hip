@@ -31,6 +31,8 @@
 #include <cstdint>
 #include <algorithm>
 #include <type_traits>
+#include <cstdio>
+#include <vector>
 
 #include "poa_graph.hpp"
 #include "poa_wave.hpp"
@@ -270,7 +272,15 @@ template <bool LDSP, int WPJ, bool PRUNE, class CodeT>
 #define SVS_PRUNE_OCC 7
 #endif
 #define SVS_PRUNE_ATTR __attribute__((amdgpu_waves_per_eu(PRUNE ? SVS_PRUNE_OCC : 1)))
+// SVS_WG_TIMES (development builds, tools/build_variant.py): the kernel body
+// becomes a device function and the kernel records each wave's start and end
+// (s_memrealtime, 100 MHz) into svs_wg_times, dumped at session close
+// (tools/dp_occupancy.py reads the dump)
+#ifdef SVS_WG_TIMES
+__device__ __forceinline__ void poa_strip_body(
+#else
 __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
+#endif
     const PoaJob* __restrict__ jobs, int n_jobs, PoaScore Parg,
     CodeT* __restrict__ tb, int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
     int32_t* __restrict__ gpool, int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
@@ -962,6 +972,39 @@ __global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
 #endif
 }
 
+#ifdef SVS_WG_TIMES
+constexpr unsigned kWgTimesCap = 1u << 23;
+__device__ unsigned long long svs_wg_times[kWgTimesCap][8];
+__device__ unsigned int svs_wg_n;
+template <bool LDSP, int WPJ, bool PRUNE, class CodeT>
+__global__ __launch_bounds__(64 * WPJ) SVS_PRUNE_ATTR void poa_strip_kernel(
+    const PoaJob* __restrict__ jobs, int n_jobs, PoaScore Parg,
+    CodeT* __restrict__ tb, int32_t* __restrict__ bnd_all, const int32_t* __restrict__ bnd_rd,
+    int32_t* __restrict__ gpool, int32_t* __restrict__ aln, int32_t* __restrict__ aln_len, uint32_t lds_slots) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  poa_strip_body<LDSP, WPJ, PRUNE, CodeT>(jobs, n_jobs, Parg, tb, bnd_all, bnd_rd, gpool, aln, aln_len, lds_slots);
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) {
+    const unsigned i = atomicAdd(&svs_wg_n, 1u);
+    if (i < kWgTimesCap) {
+      svs_wg_times[i][0] = t0;
+      svs_wg_times[i][1] = t1;
+      svs_wg_times[i][2] = (static_cast<unsigned long long>(blockIdx.x) << 32) | (threadIdx.x >> 6);
+      svs_wg_times[i][3] = (static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(jobs)) & 0xFFFFFFFFFFFFull) |
+                           (static_cast<unsigned long long>(WPJ) << 56) | (static_cast<unsigned long long>(n_jobs >> 4) << 48);
+      // the job's rows and read length; wave 0 (which ends with the
+      // traceback): the strip rows the job computed and its best score
+      const PoaJob& J = jobs[blockIdx.x];
+      const bool w0 = threadIdx.x < 64 && static_cast<int>(blockIdx.x) < n_jobs;
+      svs_wg_times[i][4] = J.n_rows;
+      svs_wg_times[i][5] = J.len;
+      svs_wg_times[i][6] = w0 ? static_cast<unsigned long long>(static_cast<uint32_t>(aln_len[2 * n_jobs + blockIdx.x])) : 0ull;
+      svs_wg_times[i][7] = w0 ? static_cast<unsigned long long>(static_cast<uint32_t>(J.lb)) : 0ull;
+    }
+  }
+}
+#endif
+
 hipError_t launch_poa_strip(const PoaLaunch& a, hipStream_t stream) {
   if (a.n_jobs <= 0) return hipSuccess;
   const int w = a.waves_per_job;
@@ -1035,6 +1078,29 @@ extern "C" int svs_debug_strip_prof(unsigned long long* out, int reset) {
   for (int i = 0; i < 10; ++i) out[i] = 0;
 #endif
   return 0;
+}
+
+// SVS_WG_TIMES builds: writes the recorded wave times (n x 8 uint64) to path
+// and resets the count; other builds write nothing.
+extern "C" int svs_debug_wg_times_dump(const char* path) {
+#ifdef SVS_WG_TIMES
+  unsigned n = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -3;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(svs_wg_n), sizeof(n)) != hipSuccess) return -3;
+  n = std::min(n, kWgTimesCap);
+  std::vector<unsigned long long> h(static_cast<size_t>(n) * 8);
+  if (n && hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(svs_wg_times), h.size() * 8) != hipSuccess) return -3;
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return -1;
+  std::fwrite(h.data(), 8, h.size(), f);
+  std::fclose(f);
+  const unsigned z = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(svs_wg_n), &z, sizeof(z)) != hipSuccess) return -3;
+  return static_cast<int>(n);
+#else
+  (void)path;
+  return 0;
+#endif
 }
 
 hipError_t launch_wave_selftest(const int32_t* in, int32_t* scan, int32_t* shift, int n_waves,

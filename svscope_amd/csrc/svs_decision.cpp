@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -611,6 +612,10 @@ void session_stats(svs_decision_session* s, svs_decision_stats* out) {
 
 // Finishes every submitted batch, joins the worker and frees the session.
 // Returns the worker's error, if any.
+#ifdef SVS_WG_TIMES
+extern "C" int svs_debug_wg_times_dump(const char* path);
+#endif
+
 std::exception_ptr close_decision_session(svs_decision_session* s) {
   {
     std::lock_guard<std::mutex> lk(s->mu);
@@ -620,6 +625,9 @@ std::exception_ptr close_decision_session(svs_decision_session* s) {
   s->cv_work.notify_all();
   if (s->builder.joinable()) s->builder.join();
   if (s->worker.joinable()) s->worker.join();
+#ifdef SVS_WG_TIMES
+  if (const char* p = std::getenv("SVS_WG_TIMES_OUT")) std::fprintf(stderr, "[svs] wg times: %d\n", svs_debug_wg_times_dump(p));
+#endif
   std::exception_ptr e = s->error;
   delete s;
   return e;
