@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -119,6 +120,10 @@ int svs_init(int device_ordinal, svs_context** out) {
     const size_t used = ctx->device_budget + ctx->device_budget / 8 + (4ull << 30);
     const size_t rest = free_b > used ? free_b - used : 0;
     ctx->dgraph_budget = std::max<size_t>(rest, 1ull << 30);
+    if (std::getenv("SVS_POA_DEBUG"))
+      std::fprintf(stderr, "[svs] context: free %.1f of %.1f GiB, launch budget %.1f GiB, graph arena %.1f GiB\n",
+                   free_b / 1073741824.0, total_b / 1073741824.0, ctx->device_budget / 1073741824.0,
+                   ctx->dgraph_budget / 1073741824.0);
     ctx->pool = new svs::ThreadPool(host_threads());
   });
   if (rc != SVS_OK) {
