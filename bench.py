@@ -178,6 +178,24 @@ def cpu_baseline(rows, cores):
             "modes": modes, "cpu_model": model, "nproc": os.cpu_count()}
 
 
+def cpu_baseline_process():
+    """cpu_baseline in a child Python process (same windows: ids 0 .. cores-1),
+    started before this process touches the GPU.  Run in the bench's own
+    process, 9 of 17 driver runs fell into a slower schedule (753-784 vs
+    660-666 DP launches, 419-430 vs 439-448 windows/s; none of ~25 runs with
+    --cpu-sample 0 did; 0 of 4 with this child process, profiles/r06_cb;
+    DESIGN §7 item 2)."""
+    import tempfile
+    fd, path = tempfile.mkstemp(suffix=".json")
+    os.close(fd)
+    try:
+        subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-json", path], check=True)
+        with open(path) as fh:
+            return json.load(fh)
+    finally:
+        os.unlink(path)
+
+
 def pmc_traffic_per_cell():
     """Measured HBM bytes per evaluated DP cell of the POA kernel from the
     committed rocprofv3 PMC summary (FETCH_SIZE and WRITE_SIZE passes), or None."""
@@ -316,7 +334,15 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=-1, help="CPU baseline: -1 both modes, 0 off")
     ap.add_argument("--gen-procs", type=int, default=0, help="window generator processes (0: all host cores)")
     ap.add_argument("--probe-env", default="", help=argparse.SUPPRESS)  # launcher test: record rank env, exit
+    ap.add_argument("--cpu-baseline-json", default="", help=argparse.SUPPRESS)  # the baseline's own process
     args = ap.parse_args()
+
+    if args.cpu_baseline_json:
+        # the CPU baseline in a process of its own (see cpu_baseline_process)
+        cores = host_cores()
+        with open(args.cpu_baseline_json, "w") as fh:
+            json.dump(cpu_baseline(generate(list(range(cores)), cores), cores), fh)
+        return
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -361,7 +387,7 @@ def main():
 
     cpu = None
     if args.cpu_sample != 0 and world == 1 and rank == 0:  # the CPU baseline is an N=1 figure
-        cpu = cpu_baseline(rows, cores)
+        cpu = cpu_baseline_process()
 
     dist = None
     device = None
