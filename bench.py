@@ -180,11 +180,10 @@ def cpu_baseline(rows, cores):
 
 def cpu_baseline_process():
     """cpu_baseline in a child Python process (same windows: ids 0 .. cores-1),
-    started before this process touches the GPU.  Run in the bench's own
-    process, 9 of 17 driver runs fell into a slower schedule (753-784 vs
-    660-666 DP launches, 419-430 vs 439-448 windows/s; none of ~25 runs with
-    --cpu-sample 0 did; 0 of 4 with this child process, profiles/r06_cb;
-    DESIGN §7 item 2)."""
+    started before this process touches the GPU, so that the bench's own
+    process carries none of the baseline's imports, oracle library or fork
+    pools.  (It was first taken for the cause of the slow final-drain runs,
+    DESIGN §7 item 2; those also occur with --cpu-sample 0, profiles/r06_eb.)"""
     import tempfile
     fd, path = tempfile.mkstemp(suffix=".json")
     os.close(fd)
